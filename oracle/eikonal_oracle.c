@@ -1,0 +1,701 @@
+/*
+ * eikonal_oracle.c -- CPU restatement of the reference Eikonal path.
+ *
+ * *** TEST INFRASTRUCTURE ONLY. ***  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library, and only as the checker / timed CPU baseline.
+ * The product (planning-motion_planning_amd/, libeikonal) never links or calls it.
+ *
+ * Pinned against fixtures produced by the reference itself (tests/golden/make_golden.py,
+ * which imports /root/reference/src/FastMarching): fp64 outputs are bit-identical.
+ *
+ * What it restates (reference = /root/reference/src/FastMarching/):
+ *   getEikonal        FastMarching.py:17-29      -> eik2()
+ *   updateNode        FastMarching.py:44-80      -> update2d()   (sorted list -> lazy heap)
+ *   getMinNB          FastMarching.py:82-89      -> heap_pop()
+ *   computeTmap       FastMarching.py:92-112     -> orc_fmm2d()  (intended semantics: the
+ *                                                   reference raises at :107)
+ *   biComputeTmap     FastMarching.py:114-162    -> orc_fmm2d_bidir()
+ *   getPathGDM        FastMarching.py:164-236    -> orc_gdm2d()
+ *   computeGradient   FastMarching.py:242-300    -> grad_at(), orc_gradient2d()
+ *   interpolatePoint  FastMarching.py:305-338    -> interp2()
+ *   FM3D updateNode   FastMarching3D.py:19-101   -> update3d()
+ *   FM3D computeTmap  FastMarching3D.py:126-145  -> orc_fmm3d()
+ *   FM3D getPathGDM   FastMarching3D.py:198-271  -> orc_gdm3d()
+ *   FM3D interpolate  FastMarching3D.py:275-314  -> interp3()
+ *
+ * Narrow band: the reference keeps a list sorted with bisect_left and pops index 0, so among
+ * equal T the most recently inserted node pops first.  A binary heap keyed (T, -seq) with a
+ * per-node "live seq" (lazy deletion) gives the identical pop order.  The reference's
+ * decrease-key searches from bisect_left(nbT, oldT) but the generator at :73 only probes
+ * index 0 when that position is 0, so a node tied at the band minimum that is not first in
+ * the list makes the reference raise StopIteration: reproduced as ORC_REF_STOPITERATION.
+ *
+ * Rounding fidelity: numpy's np.power(x, 2) ufunc and ndarray**2 are exact products, but a
+ * numpy float64 *scalar* `x**2` goes through libm pow(), which is not always correctly
+ * rounded; each site below uses whichever the reference line uses.
+ *
+ * Grid convention (reference): arrays are row-major [y][x](+[z]); nodes are (x, y(, z)).
+ * Out-of-range neighbours read as +inf (the reference relies on an inf border instead).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ORC_OK 0
+#define ORC_ERR_ARG (-1)
+#define ORC_ERR_NOMEM (-2)
+#define ORC_REF_STOPITERATION 2 /* reference raises StopIteration (FastMarching.py:73 / 3D:89)   */
+#define ORC_REF_UNBOUND 3       /* biComputeTmap: fronts never met -> UnboundLocalError (:161)   */
+#define ORC_REF_VALUEERROR 4    /* FM3D: max() of an empty Tarray (cost == 0), 3D:64             */
+#define ORC_REF_INDEXERROR 5    /* reference would index out of range                            */
+
+/* path status (orc_gdm2d / orc_gdm3d) */
+#define GDM_DONE 0      /* loop ended (stop radius or budget) and endWaypoint appended     */
+#define GDM_FALLBACK 1  /* 2D: NaN fallback, numpy-2 OverflowError caught, truncated path    */
+#define GDM_ERROR 2     /* the reference raises out of getPathGDM (uncaught)                */
+
+/* strict = 1 (default): reproduce the reference's StopIteration on a tied decrease-key.
+ * strict = 0: proceed with the intended decrease-key (used by property tests on tie-heavy
+ * symmetric maps, where the reference itself would crash). */
+static int g_strict = 1;
+void orc_set_strict(int strict) { g_strict = strict; }
+
+/* ------------------------------------------------------------------------------ heap */
+typedef struct {
+    double t;
+    uint64_t seq;
+    int64_t node;
+} hent;
+
+typedef struct {
+    hent *a;
+    int64_t n, cap;
+    uint64_t seq;
+    uint64_t *live; /* live seq per node (0 = none) */
+    const uint8_t *closed;
+} heap_t;
+
+static inline int hless(const hent *x, const hent *y) {
+    return x->t < y->t || (x->t == y->t && x->seq > y->seq);
+}
+
+static int heap_init(heap_t *h, int64_t nnodes, const uint8_t *closed) {
+    h->cap = 1024;
+    h->n = 0;
+    h->seq = 0;
+    h->a = (hent *)malloc(sizeof(hent) * h->cap);
+    h->live = (uint64_t *)calloc((size_t)nnodes, sizeof(uint64_t));
+    h->closed = closed;
+    return (h->a && h->live) ? 0 : -1;
+}
+static void heap_free(heap_t *h) {
+    free(h->a);
+    free(h->live);
+}
+static int heap_push(heap_t *h, double t, int64_t node) {
+    if (h->n == h->cap) {
+        h->cap *= 2;
+        hent *na = (hent *)realloc(h->a, sizeof(hent) * h->cap);
+        if (!na) return -1;
+        h->a = na;
+    }
+    hent e = {t, ++h->seq, node};
+    h->live[node] = e.seq;
+    int64_t i = h->n++;
+    while (i > 0) {
+        int64_t p = (i - 1) >> 1;
+        if (!hless(&e, &h->a[p])) break;
+        h->a[i] = h->a[p];
+        i = p;
+    }
+    h->a[i] = e;
+    return 0;
+}
+static void heap_pop_raw(heap_t *h) {
+    hent e = h->a[--h->n];
+    int64_t i = 0;
+    for (;;) {
+        int64_t l = 2 * i + 1, r = l + 1, m = i;
+        const hent *best = &e;
+        if (l < h->n && hless(&h->a[l], best)) { m = l; best = &h->a[l]; }
+        if (r < h->n && hless(&h->a[r], best)) { m = r; best = &h->a[r]; }
+        if (m == i) break;
+        h->a[i] = h->a[m];
+        i = m;
+    }
+    if (h->n > 0) h->a[i] = e;
+}
+/* drop stale entries at the top; returns 1 if a live entry is at the top */
+static int heap_clean(heap_t *h) {
+    while (h->n > 0) {
+        const hent *t = &h->a[0];
+        if (h->live[t->node] == t->seq && !h->closed[t->node]) return 1;
+        heap_pop_raw(h);
+    }
+    return 0;
+}
+static int64_t heap_pop(heap_t *h) { /* getMinNB: FastMarching.py:82-89 */
+    int64_t node = h->a[0].node;
+    h->live[node] = 0;
+    heap_pop_raw(h);
+    return node;
+}
+
+/* --------------------------------------------------------------------- getEikonal (2D) */
+double orc_eikonal(double thor, double tver, double c) { /* FastMarching.py:17-29 */
+    if (isinf(thor)) {
+        if (isinf(tver)) return INFINITY;
+        return tver + c;
+    }
+    if (isinf(tver)) return thor + c;
+    if (c < fabs(thor - tver)) return fmin(thor, tver) + c;
+    /* np.power(.,2) on numpy scalars via the ufunc = exact product */
+    return .5 * (thor + tver + sqrt(2 * (c * c) - (thor - tver) * (thor - tver)));
+}
+
+/* -------------------------------------------------------------------------- 2D FMM */
+typedef struct {
+    const double *cost;
+    double *T;
+    uint8_t *closed;
+    int64_t H, W;
+    heap_t hp;
+} fmm2d_t;
+
+static inline double tget2(const fmm2d_t *f, int64_t x, int64_t y) {
+    if (x < 0 || y < 0 || x >= f->W || y >= f->H) return INFINITY;
+    return f->T[y * f->W + x];
+}
+
+/* updateNode FastMarching.py:44-80 ; children y-1, y+1, x-1, x+1 (:46-54) */
+static int update2d(fmm2d_t *f, int64_t nx, int64_t ny) {
+    static const int dxy[4][2] = {{0, -1}, {0, 1}, {-1, 0}, {1, 0}};
+    for (int k = 0; k < 4; ++k) {
+        int64_t cx = nx + dxy[k][0], cy = ny + dxy[k][1];
+        if (cx < 0 || cy < 0 || cx >= f->W || cy >= f->H) continue;
+        int64_t c = cy * f->W + cx;
+        if (f->closed[c]) continue; /* :56 */
+        double thor = fmin(tget2(f, cx + 1, cy), tget2(f, cx - 1, cy)); /* :57-59 */
+        double tver = fmin(tget2(f, cx, cy + 1), tget2(f, cx, cy - 1)); /* :60-62 */
+        double tn = orc_eikonal(thor, tver, f->cost[c]);                  /* :63 */
+        if (isinf(f->T[c])) {                                             /* :64-68 */
+            if (heap_push(&f->hp, tn, c)) return ORC_ERR_NOMEM;
+            f->T[c] = tn;
+        } else if (tn < f->T[c]) { /* :69-79 decrease-key */
+            heap_clean(&f->hp);
+            if (g_strict && f->hp.a[0].t == f->T[c] && f->hp.a[0].node != c) return ORC_REF_STOPITERATION;
+            if (heap_push(&f->hp, tn, c)) return ORC_ERR_NOMEM;
+            f->T[c] = tn;
+        }
+    }
+    return ORC_OK;
+}
+
+/* computeTmap, intended semantics (FastMarching.py:92-112): full field if start is outside
+ * the grid or never popped; otherwise stops right after start is popped (:108-109). */
+int orc_fmm2d(const double *cost, int64_t H, int64_t W, int64_t gx, int64_t gy, int64_t sx, int64_t sy,
+              double *T, int64_t *pops_out) {
+    if (!cost || !T || H < 1 || W < 1 || gx < 0 || gy < 0 || gx >= W || gy >= H) return ORC_ERR_ARG;
+    int64_t N = H * W;
+    fmm2d_t f = {cost, T, (uint8_t *)calloc((size_t)N, 1), H, W};
+    if (!f.closed || heap_init(&f.hp, N, f.closed)) return ORC_ERR_NOMEM;
+    for (int64_t i = 0; i < N; ++i) {
+        T[i] = INFINITY;
+        f.closed[i] = (cost[i] == INFINITY); /* :93-94 */
+    }
+    T[gy * W + gx] = 0; /* :98-99 */
+    f.closed[gy * W + gx] = 1;
+    int rc = update2d(&f, gx, gy); /* :101 */
+    int64_t pops = 0;
+    while (rc == ORC_OK && heap_clean(&f.hp)) { /* :104 */
+        int64_t node = heap_pop(&f.hp);         /* :105 */
+        f.closed[node] = 1;                     /* :106 */
+        int64_t x = node % W, y = node / W;
+        rc = update2d(&f, x, y); /* :107 */
+        ++pops;
+        if (x == sx && y == sy) break; /* :108-109 */
+    }
+    if (pops_out) *pops_out = pops;
+    heap_free(&f.hp);
+    free(f.closed);
+    return rc;
+}
+
+/* biComputeTmap FastMarching.py:114-162 */
+int orc_fmm2d_bidir(const double *cost, int64_t H, int64_t W, int64_t gx, int64_t gy, int64_t sx, int64_t sy,
+                    double *TG, double *TS, uint32_t *join) {
+    if (!cost || !TG || !TS || !join || H < 1 || W < 1) return ORC_ERR_ARG;
+    if (gx < 0 || gy < 0 || gx >= W || gy >= H || sx < 0 || sy < 0 || sx >= W || sy >= H) return ORC_ERR_ARG;
+    int64_t N = H * W;
+    fmm2d_t g = {cost, TG, (uint8_t *)calloc((size_t)N, 1), H, W};
+    fmm2d_t s = {cost, TS, (uint8_t *)calloc((size_t)N, 1), H, W};
+    if (!g.closed || !s.closed || heap_init(&g.hp, N, g.closed) || heap_init(&s.hp, N, s.closed)) return ORC_ERR_NOMEM;
+    for (int64_t i = 0; i < N; ++i) {
+        TG[i] = TS[i] = INFINITY; /* :131,134 */
+        g.closed[i] = s.closed[i] = isinf(cost[i]) ? 1 : 0; /* :121,124 */
+    }
+    g.closed[gy * W + gx] = 1; /* :120 */
+    s.closed[sy * W + sx] = 1; /* :123 */
+    TG[gy * W + gx] = 0;
+    int rc = update2d(&g, gx, gy); /* :133 */
+    TS[sy * W + sx] = 0;
+    if (rc == ORC_OK) rc = update2d(&s, sx, sy); /* :136 */
+    int64_t ng = gy * W + gx, ns = sy * W + sx;    /* nodeTargetG / nodeTargetS (:116-117) */
+    int found = 0;
+    while (rc == ORC_OK) {
+        int hg = heap_clean(&g.hp), hs = heap_clean(&s.hp);
+        if (!hg && !hs) break; /* :141 */
+        if (hg) {              /* :142-145 */
+            ng = heap_pop(&g.hp);
+            g.closed[ng] = 1;
+            rc = update2d(&g, ng % W, ng / W);
+            if (rc != ORC_OK) break;
+        }
+        if (heap_clean(&s.hp)) { /* :146-149 (nbTS re-tested after the G update) */
+            ns = heap_pop(&s.hp);
+            s.closed[ns] = 1;
+            rc = update2d(&s, ns % W, ns / W);
+            if (rc != ORC_OK) break;
+        }
+        if (s.closed[ng]) { /* :150-152 */
+            join[0] = (uint32_t)(ng % W);
+            join[1] = (uint32_t)(ng / W);
+            found = 1;
+            break;
+        }
+        if (g.closed[ns]) { /* :153-155 */
+            join[0] = (uint32_t)(ns % W);
+            join[1] = (uint32_t)(ns / W);
+            found = 1;
+            break;
+        }
+    }
+    heap_free(&g.hp);
+    heap_free(&s.hp);
+    free(g.closed);
+    free(s.closed);
+    if (rc != ORC_OK) return rc;
+    return found ? ORC_OK : ORC_REF_UNBOUND;
+}
+
+/* ----------------------------------------------------------------- 2D gradient + GDM */
+static inline double TT(const double *T, int64_t W, int64_t j, int64_t i) { return T[j * W + i]; }
+
+/* computeGradient body for one (j, i), FastMarching.py:262-297 */
+static void grad_at(const double *T, int64_t m, int64_t n, int64_t j, int64_t i, double *gnx, double *gny) {
+    double gy, gx;
+    if (j == 0)
+        gy = TT(T, n, 1, i) - TT(T, n, 0, i);
+    else if (j == m - 1)
+        gy = TT(T, n, j, i) - TT(T, n, j - 1, i);
+    else if (isinf(TT(T, n, j + 1, i)))
+        gy = isinf(TT(T, n, j - 1, i)) ? 0.0 : TT(T, n, j, i) - TT(T, n, j - 1, i);
+    else
+        gy = isinf(TT(T, n, j - 1, i)) ? TT(T, n, j + 1, i) - TT(T, n, j, i)
+                                       : (TT(T, n, j + 1, i) - TT(T, n, j - 1, i)) / 2;
+    if (i == 0)
+        gx = TT(T, n, j, 1) - TT(T, n, j, 0);
+    else if (i == n - 1)
+        gx = TT(T, n, j, i) - TT(T, n, j, i - 1);
+    else if (isinf(TT(T, n, j, i + 1)))
+        gx = isinf(TT(T, n, j, i - 1)) ? 0.0 : TT(T, n, j, i) - TT(T, n, j, i - 1);
+    else
+        gx = isinf(TT(T, n, j, i - 1)) ? TT(T, n, j, i + 1) - TT(T, n, j, i)
+                                       : (TT(T, n, j, i + 1) - TT(T, n, j, i - 1)) / 2;
+    /* :296-297  Gx[j,i]**2 on a numpy scalar -> libm pow */
+    *gnx = gx / sqrt(pow(gx, 2) + pow(gy, 2));
+    *gny = gy / sqrt(pow(gx, 2) + pow(gy, 2));
+}
+
+/* computeGradient(cost, point) FastMarching.py:242-300.  has_point=0 -> whole field. */
+int orc_gradient2d(const double *T, int64_t H, int64_t W, int has_point, double px, double py, double *gnx,
+                   double *gny) {
+    if (!T || !gnx || !gny || H < 2 || W < 2) return ORC_ERR_ARG;
+    int64_t jmin = 0, imin = 0, jmax = H, imax = W;
+    if (has_point) { /* :250-252 */
+        jmax = (int64_t)py + 3 < H ? (int64_t)py + 3 : H;
+        imax = (int64_t)px + 3 < W ? (int64_t)px + 3 : W;
+        jmin = (int64_t)(py - 3) > 0 ? (int64_t)(py - 3) : 0;
+        imin = (int64_t)(px - 3) > 0 ? (int64_t)(px - 3) : 0;
+    }
+    memset(gnx, 0, sizeof(double) * H * W);
+    memset(gny, 0, sizeof(double) * H * W);
+    for (int64_t i = imin; i < imax; ++i)
+        for (int64_t j = jmin; j < jmax; ++j) grad_at(T, H, W, j, i, &gnx[j * W + i], &gny[j * W + i]);
+    return ORC_OK;
+}
+
+/* interpolatePoint FastMarching.py:305-338 on a 2x2 corner patch g[jj][ii] (jj,ii in {0,1});
+ * the caller fills the patch from the field. */
+static double interp2_patch(double a, double b, const double g[2][2]) {
+    double a00 = g[0][0];
+    double a10 = g[0][1] - g[0][0];
+    double a01 = g[1][0] - g[0][0];
+    double a11 = g[1][1] + g[0][0] - g[0][1] - g[1][0];
+    if (a == 0) return b == 0 ? a00 : a00 + a01 * b;
+    return b == 0 ? a00 + a10 * a : a00 + a10 * a + a01 * b + a11 * a * b;
+}
+
+/* interpolatePoint on a full map (helper-fixture entry point); returns NaN + sets *err on
+ * an access the reference would fault on. */
+double orc_interp2(double px, double py, const double *M, int64_t m, int64_t n, int *err) {
+    uint32_t i = (uint32_t)trunc(px), j = (uint32_t)trunc(py);
+    double a = px - i, b = py - j;
+    *err = 0;
+    if (i == n) {
+        if (j == m) { *err = ORC_REF_INDEXERROR; return NAN; }
+        if (j + 1 >= m) { *err = ORC_REF_INDEXERROR; return NAN; }
+        *err = ORC_REF_INDEXERROR; /* mapI[j, n] is out of range as well */
+        return NAN;
+    }
+    if (j == m || i + 1 >= (uint32_t)n || j + 1 >= (uint32_t)m) { *err = ORC_REF_INDEXERROR; return NAN; }
+    double g[2][2] = {{M[j * n + i], M[j * n + i + 1]}, {M[(j + 1) * n + i], M[(j + 1) * n + i + 1]}};
+    return interp2_patch(a, b, g);
+}
+
+static inline double norm2(double a, double b) { return sqrt(a * a + b * b); }
+
+/* getPathGDM FastMarching.py:164-236 (numpy-2 semantics of the NaN fallback).
+ * out: (max_out x 2) row-major; *n_out rows written; *status GDM_*. */
+int orc_gdm2d(const double *T, int64_t H, int64_t W, double ix, double iy, double ex, double ey, double tau,
+              double *out, int64_t max_out, int64_t *n_out, int *status) {
+    if (!T || !out || !n_out || !status || H < 3 || W < 3 || max_out < 2 || !(tau > 0)) return ORC_ERR_ARG;
+    int64_t n = 0;
+#define PUSH(X, Y)                                  \
+    do {                                            \
+        if (n >= max_out) return ORC_ERR_ARG;       \
+        out[2 * n] = (X);                           \
+        out[2 * n + 1] = (Y);                       \
+        ++n;                                        \
+    } while (0)
+    PUSH(ix, iy); /* :168-169 */
+    long steps = (long)nearbyint(15000.0 / tau); /* round(15000/tau), half-even */
+    *status = GDM_DONE;
+    for (long k = 0; k < steps; ++k) { /* :173 */
+        double px = out[2 * (n - 1)], py = out[2 * (n - 1) + 1];
+        /* computeGradient's int(point) raises ValueError on NaN (:250, outside the try) */
+        if (isnan(px) || isnan(py)) { *status = GDM_ERROR; *n_out = n; return ORC_REF_VALUEERROR; }
+        uint32_t i = (uint32_t)trunc(px), j = (uint32_t)trunc(py);
+        double dx, dy;
+        if (i + 1 >= (uint32_t)W || j + 1 >= (uint32_t)H) { /* interpolatePoint IndexError */
+            *status = GDM_ERROR;
+            *n_out = n;
+            return ORC_REF_INDEXERROR;
+        } else {
+            double gx[2][2], gy[2][2];
+            for (int jj = 0; jj < 2; ++jj)
+                for (int ii = 0; ii < 2; ++ii) grad_at(T, H, W, j + jj, i + ii, &gx[jj][ii], &gy[jj][ii]);
+            double a = px - i, b = py - j;
+            dx = interp2_patch(a, b, gx); /* :175 */
+            dy = interp2_patch(a, b, gy); /* :176 */
+        }
+        if (isnan(dx) || isnan(dy)) { /* :178-218 */
+            /* try: */
+            int64_t nx = (int64_t)nearbyint(px), ny = (int64_t)nearbyint(py); /* :180-181 */
+            for (;;) { /* :182-185 */
+                int64_t wx = nx < 0 ? nx + W : nx, wy = ny < 0 ? ny + H : ny; /* python wrap */
+                if (wx < 0 || wy < 0 || wx >= W || wy >= H) { *status = GDM_FALLBACK; *n_out = n; return ORC_OK; }
+                if (!isinf(T[wy * W + wx])) break;
+                --n; /* np.delete(gamma, -1) */
+                if (n == 0) { *status = GDM_FALLBACK; *n_out = 0; return ORC_OK; } /* gamma[-1] IndexError */
+                double qx = out[2 * (n - 1)], qy = out[2 * (n - 1) + 1];
+                nx = (int64_t)nearbyint(qx);
+                ny = (int64_t)nearbyint(qy);
+            }
+            if (n > 0) { /* :187-191 */
+                while (norm2(out[2 * (n - 1)] - (double)nx, out[2 * (n - 1) + 1] - (double)ny) < 1) {
+                    --n;
+                    if (n == 0) break;
+                }
+            }
+            PUSH((double)nx, (double)ny); /* :193 */
+            /* :194-197  np.uint32(nearN + [0,-1]) is a list concatenation with a -1 in it:
+             * numpy 2 raises OverflowError, the bare except at :217 returns gamma. */
+            *status = GDM_FALLBACK;
+            *n_out = n;
+            return ORC_OK;
+        }
+        double sx_, sy_;
+        if (norm2(dx, dy) < 0.01) { /* :220-224 */
+            double dnx = dx / sqrt(pow(dx, 2) + pow(dy, 2));
+            double dny = dy / sqrt(pow(dx, 2) + pow(dy, 2));
+            sx_ = px - tau * dnx;
+            sy_ = py - tau * dny;
+        } else { /* :225-229 -- dy normalised with the already-normalised dx */
+            dx = dx / sqrt(pow(dx, 2) + pow(dy, 2));
+            dy = dy / sqrt(pow(dx, 2) + pow(dy, 2));
+            sx_ = px - tau * dx;
+            sy_ = py - tau * dy;
+        }
+        PUSH(sx_, sy_);
+        if (norm2(sx_ - ex, sy_ - ey) < 1.5) break; /* :231-232 */
+    }
+    PUSH(ex, ey); /* :234 */
+    *n_out = n;
+    return ORC_OK;
+#undef PUSH
+}
+
+/* ---------------------------------------------------------------------------- 3D FMM */
+typedef struct {
+    const double *cost;
+    double *T;
+    uint8_t *closed;
+    int64_t H, W, L;
+    heap_t hp;
+} fmm3d_t;
+
+static inline double tget3(const fmm3d_t *f, int64_t x, int64_t y, int64_t z) {
+    if (x < 0 || y < 0 || z < 0 || x >= f->W || y >= f->H || z >= f->L) return INFINITY;
+    return f->T[(y * f->W + x) * f->L + z];
+}
+
+/* sumlist FastMarching3D.py:103-107: right-associated */
+static double sumlist(const double *v, int n) { return n == 1 ? v[0] : v[0] + sumlist(v + 1, n - 1); }
+
+/* FastMarching3D.py:59-75 : drop-the-largest n-D Godunov solve */
+static int solve3(double tx, double ty, double tz, double C, double *out) {
+    double arr[3] = {tx, ty, tz};
+    int n = 3;
+    double tr = INFINITY;
+    while (tr == INFINITY) { /* :62 */
+        if (n == 0) return ORC_REF_VALUEERROR; /* max([]) */
+        double tmax = arr[0]; /* :64 max(): first maximal element */
+        for (int a = 1; a < n; ++a)
+            if (arr[a] > tmax) tmax = arr[a];
+        double sumT = 0; /* :66-68 left fold, scalar **2 -> pow */
+        for (int a = 0; a < n; ++a) sumT = sumT + pow(tmax - arr[a], 2);
+        if (pow(C, 2) > sumT) { /* :70-71 */
+            double sq[3];
+            for (int a = 0; a < n; ++a) sq[a] = arr[a] * arr[a]; /* array(Tarray)**2: exact */
+            double S = sumlist(arr, n), Q = sumlist(sq, n);
+            tr = (S + sqrt(n * pow(C, 2) + pow(S, 2) - n * Q)) / n;
+        }
+        /* :73 list.remove(Tmax): first element equal to Tmax */
+        for (int a = 0; a < n; ++a)
+            if (arr[a] == tmax) {
+                for (int b = a; b + 1 < n; ++b) arr[b] = arr[b + 1];
+                --n;
+                break;
+            }
+    }
+    *out = tr;
+    return ORC_OK;
+}
+
+/* FM3D updateNode :19-101 ; children z-1, z+1, x-1, x+1, y+1, y-1 (:21-33) */
+static int update3d(fmm3d_t *f, int64_t nx, int64_t ny, int64_t nz) {
+    static const int d[6][3] = {{0, 0, -1}, {0, 0, 1}, {-1, 0, 0}, {1, 0, 0}, {0, 1, 0}, {0, -1, 0}};
+    for (int k = 0; k < 6; ++k) {
+        int64_t cx = nx + d[k][0], cy = ny + d[k][1], cz = nz + d[k][2];
+        if (cx < 0 || cy < 0 || cz < 0 || cx >= f->W || cy >= f->H || cz >= f->L) continue;
+        int64_t c = (cy * f->W + cx) * f->L + cz;
+        if (f->closed[c]) continue; /* :35 */
+        double C = f->cost[c];
+        double tx1 = tget3(f, cx - 1, cy, cz), tx2 = tget3(f, cx + 1, cy, cz);
+        double ty1 = tget3(f, cx, cy - 1, cz), ty2 = tget3(f, cx, cy + 1, cz);
+        double tz1 = tget3(f, cx, cy, cz - 1), tz2 = tget3(f, cx, cy, cz + 1);
+        double tx = tx1 < tx2 ? tx1 : tx2; /* :44-57 */
+        double ty = ty1 < ty2 ? ty1 : ty2;
+        double tz = tz1 < tz2 ? tz1 : tz2;
+        double tn;
+        int rc = solve3(tx, ty, tz, C, &tn);
+        if (rc) return rc;
+        if (isinf(f->T[c])) { /* :77-81 */
+            if (heap_push(&f->hp, tn, c)) return ORC_ERR_NOMEM;
+            f->T[c] = tn;
+        } else if (tn < f->T[c]) { /* :85-95 */
+            heap_clean(&f->hp);
+            if (g_strict && f->hp.a[0].t == f->T[c] && f->hp.a[0].node != c) return ORC_REF_STOPITERATION;
+            if (heap_push(&f->hp, tn, c)) return ORC_ERR_NOMEM;
+            f->T[c] = tn;
+        }
+    }
+    return ORC_OK;
+}
+
+/* FM3D computeTmap :126-145 (early exit when start is popped, :141) */
+int orc_fmm3d(const double *cost, int64_t H, int64_t W, int64_t L, const int64_t *goal, const int64_t *start,
+              double *T) {
+    if (!cost || !T || !goal || H < 1 || W < 1 || L < 1) return ORC_ERR_ARG;
+    int64_t gx = goal[0], gy = goal[1], gz = goal[2];
+    if (gx < 0 || gy < 0 || gz < 0 || gx >= W || gy >= H || gz >= L) return ORC_ERR_ARG;
+    int64_t N = H * W * L;
+    fmm3d_t f = {cost, T, (uint8_t *)calloc((size_t)N, 1), H, W, L};
+    if (!f.closed || heap_init(&f.hp, N, f.closed)) return ORC_ERR_NOMEM;
+    for (int64_t i = 0; i < N; ++i) {
+        T[i] = INFINITY;
+        f.closed[i] = (cost[i] == INFINITY);
+    }
+    int64_t g = (gy * W + gx) * L + gz;
+    T[g] = 0;
+    f.closed[g] = 1;
+    int rc = update3d(&f, gx, gy, gz);
+    while (rc == ORC_OK && heap_clean(&f.hp)) {
+        int64_t node = heap_pop(&f.hp);
+        f.closed[node] = 1;
+        int64_t z = node % L, xy = node / L, x = xy % W, y = xy / W;
+        rc = update3d(&f, x, y, z);
+        if (start && x == start[0] && y == start[1] && z == start[2]) break;
+    }
+    heap_free(&f.hp);
+    free(f.closed);
+    return rc;
+}
+
+/* np.gradient(T) (uniform spacing 1, edge_order 1) along one axis at one node */
+static double npgrad(const double *T, int64_t H, int64_t W, int64_t L, int axis, int64_t y, int64_t x, int64_t z) {
+    int64_t len = axis == 0 ? H : axis == 1 ? W : L;
+    int64_t p = axis == 0 ? y : axis == 1 ? x : z;
+    int64_t st = axis == 0 ? W * L : axis == 1 ? L : 1;
+    const double *c = T + (y * W + x) * L + z;
+    if (p == 0) return (c[st] - c[0]) / 1.0;
+    if (p == len - 1) return (c[0] - c[-st]) / 1.0;
+    return (c[st] - c[-st]) / 2.0;
+}
+
+/* FM3D interpolatePoint :275-314 for the interior branch (the one the path can reach) */
+static double interp3_field(double px, double py, double pz, const double *T, int64_t H, int64_t W, int64_t L,
+                            int axis, int *err) {
+    uint32_t i = (uint32_t)trunc(px), j = (uint32_t)trunc(py), k = (uint32_t)trunc(pz);
+    *err = 0;
+    if (i + 1 >= (uint32_t)W || j + 1 >= (uint32_t)H || k + 1 >= (uint32_t)L) {
+        *err = ORC_REF_INDEXERROR; /* a0..a7 are evaluated before the edge tests (:283-290) */
+        return NAN;
+    }
+    double a = px - i, b = py - j, c = pz - k;
+#define M(J, I, K) npgrad(T, H, W, L, axis, (J), (I), (K))
+    double m000 = M(j, i, k), m010 = M(j, i + 1, k), m100 = M(j + 1, i, k), m001 = M(j, i, k + 1);
+    double m110 = M(j + 1, i + 1, k), m011 = M(j, i + 1, k + 1), m101 = M(j + 1, i, k + 1), m111 = M(j + 1, i + 1, k + 1);
+#undef M
+    double a0 = m000;
+    double a1 = m010 - m000;
+    double a2 = m100 - m000;
+    double a3 = m001 - m000;
+    double a4 = m110 + m000 - m010 - m100;
+    double a5 = m011 + m000 - m010 - m001;
+    double a6 = m101 + m000 - m100 - m001;
+    double a7 = m111 + m000 - m100 - m001 - m010; /* :290 (sic) */
+    return a0 + a1 * a + a2 * b + a3 * c + a4 * a * b + a5 * a * c + a6 * b * c + a7 * a * b * c;
+}
+
+/* FM3D interpolatePoint on a plain map (helper fixture) */
+double orc_interp3(double px, double py, double pz, const double *M_, int64_t m, int64_t n, int64_t o, int *err) {
+    uint32_t i = (uint32_t)trunc(px), j = (uint32_t)trunc(py), k = (uint32_t)trunc(pz);
+    *err = 0;
+    if (i + 1 >= (uint32_t)n || j + 1 >= (uint32_t)m || k + 1 >= (uint32_t)o) { *err = ORC_REF_INDEXERROR; return NAN; }
+    double a = px - i, b = py - j, c = pz - k;
+#define M(J, I, K) M_[((J) * n + (I)) * o + (K)]
+    double a0 = M(j, i, k);
+    double a1 = M(j, i + 1, k) - M(j, i, k);
+    double a2 = M(j + 1, i, k) - M(j, i, k);
+    double a3 = M(j, i, k + 1) - M(j, i, k);
+    double a4 = M(j + 1, i + 1, k) + M(j, i, k) - M(j, i + 1, k) - M(j + 1, i, k);
+    double a5 = M(j, i + 1, k + 1) + M(j, i, k) - M(j, i + 1, k) - M(j, i, k + 1);
+    double a6 = M(j + 1, i, k + 1) + M(j, i, k) - M(j + 1, i, k) - M(j, i, k + 1);
+    double a7 = M(j + 1, i + 1, k + 1) + M(j, i, k) - M(j + 1, i, k) - M(j, i, k + 1) - M(j, i + 1, k);
+#undef M
+    return a0 + a1 * a + a2 * b + a3 * c + a4 * a * b + a5 * a * c + a6 * b * c + a7 * a * b * c;
+}
+
+static inline double norm3(double a, double b, double c) { return sqrt(a * a + b * b + c * c); }
+
+/* FM3D getPathGDM :198-271.  init/end are (x, y, z). out: (max_out x 3). */
+int orc_gdm3d(const double *T, int64_t H, int64_t W, int64_t L, const double *init, const double *end, double tau,
+              double *out, int64_t max_out, int64_t *n_out, int *status) {
+    if (!T || !init || !end || !out || !n_out || !status || max_out < 2 || !(tau > 0)) return ORC_ERR_ARG;
+    int64_t n = 0;
+#define PUSH3(X, Y, Z)                               \
+    do {                                             \
+        if (n >= max_out) return ORC_ERR_ARG;        \
+        out[3 * n] = (X);                            \
+        out[3 * n + 1] = (Y);                        \
+        out[3 * n + 2] = (Z);                        \
+        ++n;                                         \
+    } while (0)
+    PUSH3(init[0], init[1], init[2]);
+    long steps = (long)nearbyint(15000.0 / tau); /* int(round(15000/tau)) :207 */
+    *status = GDM_DONE;
+    static const int off[6][3] = {{0, -1, 0}, {0, 1, 0}, {-1, 0, 0}, {1, 0, 0}, {0, 0, -1}, {0, 0, 1}};
+    for (long k = 0; k < steps; ++k) {
+        const double *g = out + 3 * (n - 1);
+        int e1, e2, e3;
+        double dx = interp3_field(g[0], g[1], g[2], T, H, W, L, 1, &e1); /* G1: axis 1 (x) */
+        double dy = interp3_field(g[0], g[1], g[2], T, H, W, L, 0, &e2); /* G2: axis 0 (y) */
+        double dz = interp3_field(g[0], g[1], g[2], T, H, W, L, 2, &e3); /* G3: axis 2 (z) */
+        if (e1 || e2 || e3) { *status = GDM_ERROR; *n_out = n; return ORC_REF_INDEXERROR; }
+        if (isnan(dx) || isnan(dy) || isnan(dz)) { /* :212-253 */
+            int64_t nx = (int64_t)nearbyint(g[0]), ny = (int64_t)nearbyint(g[1]), nz = (int64_t)nearbyint(g[2]);
+            for (;;) { /* :217-222 */
+                if (nx < 0 || ny < 0 || nz < 0 || nx >= W || ny >= H || nz >= L) {
+                    *status = GDM_ERROR; *n_out = n; return ORC_REF_INDEXERROR;
+                }
+                if (!isinf(T[(ny * W + nx) * L + nz])) break;
+                --n;
+                if (n == 0) { *status = GDM_ERROR; *n_out = 0; return ORC_REF_INDEXERROR; }
+                const double *q = out + 3 * (n - 1);
+                nx = (int64_t)nearbyint(q[0]);
+                ny = (int64_t)nearbyint(q[1]);
+                nz = (int64_t)nearbyint(q[2]);
+            }
+            if (n > 0) { /* :223-227 */
+                while (norm3(out[3 * (n - 1)] - nx, out[3 * (n - 1) + 1] - ny, out[3 * (n - 1) + 2] - nz) < 1) {
+                    --n;
+                    if (n == 0) break;
+                }
+            }
+            PUSH3((double)nx, (double)ny, (double)nz); /* :229 */
+            double curT = T[(ny * W + nx) * L + nz];   /* :230 */
+            for (int q = 0; q < 6; ++q) {              /* :231-253 */
+                int64_t cx = nx + off[q][0], cy = ny + off[q][1], cz = nz + off[q][2];
+                if (cx < 0) cx += W; /* negative indices wrap (python) */
+                if (cy < 0) cy += H;
+                if (cz < 0) cz += L;
+                if (cx >= W || cy >= H || cz >= L) { *status = GDM_ERROR; *n_out = n; return ORC_REF_INDEXERROR; }
+                double tc = T[(cy * W + cx) * L + cz];
+                if (tc < curT) {
+                    curT = tc;
+                    dx = (double)(nx - (nx + off[q][0])) / tau;
+                    dy = (double)(ny - (ny + off[q][1])) / tau;
+                    dz = (double)(nz - (nz + off[q][2])) / tau;
+                }
+            }
+        }
+        g = out + 3 * (n - 1);
+        double nrm = sqrt(pow(dx, 2) + pow(dy, 2) + pow(dz, 2)); /* :255 */
+        double ax, ay, az;
+        if (nrm < 0.01) { /* :256-261 */
+            ax = g[0] - tau * (dx / nrm);
+            ay = g[1] - tau * (dy / nrm);
+            az = g[2] - tau * (dz / nrm);
+        } else { /* :262-264 (unnormalised) */
+            ax = g[0] - tau * dx;
+            ay = g[1] - tau * dy;
+            az = g[2] - tau * dz;
+        }
+        if (isnan(ax) || isnan(ay) || isnan(az)) { *status = GDM_ERROR; PUSH3(ax, ay, az); *n_out = n; return ORC_OK; }
+        PUSH3(ax, ay, az);
+        if (norm3(ax - end[0], ay - end[1], az - end[2]) < 1.5) break; /* :266-267 */
+    }
+    PUSH3(end[0], end[1], end[2]); /* :269 */
+    *n_out = n;
+    return ORC_OK;
+#undef PUSH3
+}
+
+/* ------------------------------------------------------------------ batch (baseline) */
+/* One map per call, many maps across threads: the CPU baseline for the 128-map config.  */
+int orc_fmm2d_batch(const double *cost, int64_t B, int64_t H, int64_t W, const int64_t *goals, double *T,
+                    int nthreads) {
+    int rc_all = ORC_OK;
+#ifdef _OPENMP
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 1)
+#endif
+    for (int64_t b = 0; b < B; ++b) {
+        int rc = orc_fmm2d(cost + b * H * W, H, W, goals[2 * b], goals[2 * b + 1], -1, -1, T + b * H * W, 0);
+        if (rc) rc_all = rc;
+    }
+    (void)nthreads;
+    return rc_all;
+}
