@@ -1,0 +1,145 @@
+/*
+ * eikonal.h -- C ABI of the MI355X-native Eikonal cost-to-go solver (libeikonal.so).
+ *
+ * The drop-in boundary for the hot path of esa-prl/planning-motion_planning:
+ *   src/FastMarching/FastMarching.py   (2D FMM + gradient-descent path)
+ *   src/FastMarching/FastMarching3D.py (3D FMM + path)
+ * reached from Python through ctypes (planning-motion_planning_amd/FastMarching/, same module
+ * and function names as the reference) and from C++ directly (include/MotionPlanning.hpp
+ * users, Rock components).  Plain C: pointers + sizes, no exceptions, no torch types.
+ *
+ * Conventions (identical to the reference):
+ *   - rasters are row-major [y][x] (3D: [y][x][z]); nodes are (x, y(, z));
+ *   - cost = +inf marks an impassable cell (FastMarching.py:93-94); costs must be >= 0;
+ *   - T = +inf marks an unreached cell;
+ *   - out-of-range neighbours read as +inf (the reference instead relies on an inf border,
+ *     Coupled_motion_planner.py:1213-1216, and wraps/raises without one).
+ * Every function returns an eik_status (0 = OK); on error eik_last_error() describes it.
+ * One context per host thread; a context owns its device buffers and HIP stream.
+ * Host-buffer entry points (eik_tmap*, eik_path*, eik_gradient*) are synchronous.
+ * Device entry points (eik_fim2d_*, eik_path2d_dev) take device pointers and a hipStream_t
+ * (passed as void*; NULL = the context's stream) and are asynchronous unless noted.
+ */
+#ifndef EIKONAL_H_
+#define EIKONAL_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    EIK_OK = 0,
+    EIK_ERR_ARG = -1,         /* bad argument (shape, index, negative cost, NULL pointer)     */
+    EIK_ERR_HIP = -2,         /* HIP runtime / launch failure                                  */
+    EIK_ERR_NOMEM = -3,       /* device or host allocation failed                               */
+    EIK_ERR_NOCONVERGE = -4,  /* iteration cap reached (e.g. negative cost on a device buffer)  */
+    EIK_ERR_UNREACHABLE = -5, /* bidirectional fronts never meet (reference: UnboundLocalError) */
+    EIK_ERR_NODEVICE = -6     /* no HIP device / library built without one                       */
+} eik_status;
+
+typedef enum { EIK_F32 = 0, EIK_F64 = 1 } eik_dtype;
+
+/* path status (eik_path2d / eik_path3d), mirrors the reference's exits */
+typedef enum {
+    EIK_PATH_DONE = 0,     /* stop radius (< 1.5 cells) or step budget hit; end appended (:231-234) */
+    EIK_PATH_FALLBACK = 1, /* NaN gradient: the reference's fallback returns a truncated path
+                              (numpy-2 behaviour of FastMarching.py:178-218)                       */
+    EIK_PATH_ERROR = 2     /* the reference raises out of getPathGDM (NaN point / out of range)     */
+} eik_path_status;
+
+typedef struct eik_ctx eik_ctx;
+typedef struct eik_fim2d eik_fim2d;
+
+typedef struct {
+    int64_t iterations;   /* outer FIM iterations (sweep launches) of the last solve           */
+    int64_t tile_visits;  /* 64x64 tile visits of the last solve                                */
+    int64_t host_syncs;   /* active-count read-backs                                            */
+    double solve_ms;      /* device time of the last solve (hipEvents, init..converged)         */
+    double sweep_ms;      /* summed device time of the sweep launches (timing option on)        */
+    double bytes_alg;     /* algorithmic bytes of the sweep launches (tile_visits x bytes/visit) */
+} eik_stats;
+
+/* options (eik_set_option) */
+typedef enum {
+    EIK_OPT_MAX_ROUNDS = 0,  /* sweep rounds per tile visit before re-enqueueing (default 1)   */
+    EIK_OPT_SYNC_EVERY = 1,  /* sweep launches between active-count read-backs (default 8)     */
+    EIK_OPT_TIMING = 2,      /* 1: time each sweep launch with hipEvents (for the roofline)     */
+    EIK_OPT_GRID = 3         /* workgroups per sweep launch (default 4 x CUs)                   */
+} eik_option;
+
+/* ---- context: replaces MotionPlanning::initPython / shutDownPython (MotionPlanning.cpp:5-29,
+ *      :93-100) as the owner of solver state; one per host thread -------------------------- */
+int eik_create(int device, eik_ctx** out);
+void eik_destroy(eik_ctx* ctx);
+const char* eik_last_error(const eik_ctx* ctx);
+int eik_set_option(eik_ctx* ctx, int option, double value);
+int eik_get_stats(const eik_ctx* ctx, eik_stats* out);
+const char* eik_version(void);
+
+/* ---- host-buffer drop-ins of FastMarching.py ------------------------------------------- */
+
+/* computeTmap(costMap, goal, start) FastMarching.py:92-112 -> full arrival field T (the
+ * reference raises at :107; this is its intended semantics with no early exit).
+ * cost, T: H*W row-major.  f32: fp32 compute; f64: fp64 compute. */
+int eik_tmap2d_f32(eik_ctx* ctx, const float* cost, int64_t H, int64_t W, int64_t gx, int64_t gy, float* T);
+int eik_tmap2d_f64(eik_ctx* ctx, const double* cost, int64_t H, int64_t W, int64_t gx, int64_t gy, double* T);
+
+/* biComputeTmap(costMap, goal, start) FastMarching.py:114-162 -> (TmapG, TmapS, nodeJoin).
+ * Both fields are FULL fields (fp64); nodeJoin is the first node popped by one front that the
+ * other front had already closed, evaluated on the device from the two fields' pop ranks. */
+int eik_tmap2d_bidir_f64(eik_ctx* ctx, const double* cost, int64_t H, int64_t W, int64_t gx, int64_t gy,
+                         int64_t sx, int64_t sy, double* TG, double* TS, uint32_t join[2]);
+
+/* B independent maps (goal sweep / terrain Monte-Carlo): cost, T: B*H*W; goals: B x (x, y). */
+int eik_tmap2d_batch_f32(eik_ctx* ctx, const float* cost, int64_t B, int64_t H, int64_t W, const int64_t* goals,
+                         float* T);
+
+/* getPathGDM(T, init, end, tau) FastMarching.py:164-236 on an fp64 field.
+ * out: cap x 2 (x, y) rows; *n_out rows written; *status an eik_path_status. */
+int eik_path2d_f64(eik_ctx* ctx, const double* T, int64_t H, int64_t W, const double init[2], const double end[2],
+                   double tau, double* out, int64_t cap, int64_t* n_out, int* status);
+
+/* computeGradient(T) FastMarching.py:242-300 (point = [] -> whole field): Gnx, Gny. */
+int eik_gradient2d_f64(eik_ctx* ctx, const double* T, int64_t H, int64_t W, double* gnx, double* gny);
+
+/* ---- device-resident solver (bench, multi-GPU domain decomposition, C++ hosts) ---------- */
+
+/* A solver for B maps of H x W in `dtype`; owns the active lists, marks and counters. */
+int eik_fim2d_create(eik_ctx* ctx, int64_t B, int64_t H, int64_t W, int dtype, eik_fim2d** out);
+void eik_fim2d_destroy(eik_fim2d* fim);
+
+/* Ghost strips for a subdomain of a decomposed raster (device pointers, NULL = +inf border):
+ * north/south length W, west/east length H.  Values are min-merged by eik_fim2d_merge_ghost. */
+int eik_fim2d_set_ghosts(eik_fim2d* fim, void* north, void* south, void* west, void* east);
+
+/* Bind device cost/T (B*H*W of dtype), set T = inf, T[goal] = 0, seed the goal tiles.
+ * goals: host array B x (x, y); a goal outside the map seeds nothing (subdomain w/o goal). */
+int eik_fim2d_start(eik_fim2d* fim, const void* d_cost, void* d_T, const int64_t* goals, void* stream);
+
+/* Run up to max_iters outer iterations (stops early when no tile is active); *active gets the
+ * number of tiles active for the next iteration (synchronises the stream). */
+int eik_fim2d_iterate(eik_fim2d* fim, int64_t max_iters, int64_t* active);
+
+/* start + iterate to convergence (synchronous). */
+int eik_fim2d_solve(eik_fim2d* fim, const void* d_cost, void* d_T, const int64_t* goals, void* stream);
+
+/* Halo exchange helpers (async on the bound stream): copy edge rows/columns of T into send
+ * strips; min-merge a received strip into ghost `side` (0 N, 1 S, 2 W, 3 E) and activate the
+ * edge tiles whose ghost decreased. */
+int eik_fim2d_pack_edges(eik_fim2d* fim, void* north, void* south, void* west, void* east);
+int eik_fim2d_merge_ghost(eik_fim2d* fim, int side, const void* recv);
+/* number of tiles active for the next iteration (synchronises the stream) */
+int eik_fim2d_active(eik_fim2d* fim, int64_t* active);
+int eik_fim2d_stats(const eik_fim2d* fim, eik_stats* out);
+
+/* getPathGDM on a device-resident field; out/n_out/status are device pointers. */
+int eik_path2d_dev(eik_ctx* ctx, const void* d_T, int dtype, int64_t H, int64_t W, const double init[2],
+                   const double end[2], double tau, double* d_out, int64_t cap, int64_t* d_n_out, int* d_status,
+                   void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EIKONAL_H_ */

@@ -1,0 +1,67 @@
+// eik_common.hpp -- shared device helpers for the MI355X Eikonal kernels (gfx950 / CDNA4).
+//
+// Grid convention follows the reference (FastMarching.py): rasters are row-major [y][x], nodes
+// are (x, y); +inf cost = impassable (closed, FastMarching.py:93-94); T = +inf = unreached.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace eik {
+
+constexpr int kTile = 64;          // tile side (cells); one wave64 lane per tile column
+constexpr int kThreads = 256;      // 4 waves per tile: one per quadrant sweep direction
+constexpr int kLds = kTile + 2;    // LDS row stride: tile + 1-cell halo on each side
+
+template <typename R> struct Real;
+template <> struct Real<float> {
+    using U = unsigned int;
+    static __host__ __device__ constexpr float inf() { return __builtin_inff(); }
+};
+template <> struct Real<double> {
+    using U = unsigned long long;
+    static __host__ __device__ constexpr double inf() { return __builtin_inf(); }
+};
+
+// 2D Godunov upwind update -- the three branches of getEikonal (FastMarching.py:17-29):
+//   both neighbours inf -> inf;  one inf -> other + c;  c < |a-b| -> min + c;
+//   else 0.5 * (a + b + sqrt(2c^2 - (a-b)^2)).
+// Branch-free: hi == inf covers the first two branches (lo + c, inf + c = inf).
+template <typename R>
+__device__ __forceinline__ R godunov2(R a, R b, R c) {
+    const R lo = a < b ? a : b;
+    const R hi = a < b ? b : a;
+    const R d = hi - lo;                     // NaN when both inf (never selected)
+    const R t1 = lo + c;
+    const R t2 = R(0.5) * (lo + hi + __builtin_sqrt(R(2) * (c * c) - d * d));
+    return (hi == Real<R>::inf() || c < d) ? t1 : t2;
+}
+template <>
+__device__ __forceinline__ float godunov2<float>(float a, float b, float c) {
+    const float lo = fminf(a, b), hi = fmaxf(a, b);
+    const float d = hi - lo;
+    const float t1 = lo + c;
+    const float t2 = 0.5f * (lo + hi + __builtin_sqrtf(2.f * (c * c) - d * d));
+    return (hi == Real<float>::inf() || c < d) ? t1 : t2;
+}
+
+// Whole-wave shift by one lane (lane i <- lane i-1) on the DPP path: v_mov_b32_dpp wave_shr:1.
+// Keeps the Gauss-Seidel dependency of the skewed sweep in registers (no LDS round trip).
+__device__ __forceinline__ float wave_shr1(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xF, 0xF, false));
+}
+__device__ __forceinline__ double wave_shr1(double v) {
+    const unsigned long long u = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(u & 0xffffffffu), 0x138, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), 0x138, 0xF, 0xF, false);
+    return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+// LDS atomic min on a non-negative float/double (IEEE order == unsigned-integer order for x >= 0).
+__device__ __forceinline__ void lds_min(float* p, float v) {
+    atomicMin(reinterpret_cast<unsigned int*>(p), __float_as_uint(v));
+}
+__device__ __forceinline__ void lds_min(double* p, double v) {
+    atomicMin(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v));
+}
+
+}  // namespace eik

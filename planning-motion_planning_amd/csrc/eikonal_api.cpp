@@ -1,0 +1,522 @@
+// eikonal_api.cpp -- C ABI (include/eikonal.h) over the HIP kernels: contexts, device buffers,
+// the outer FIM iteration driver and the synchronous host-buffer drop-ins.
+//
+// Every entry point fails loudly (status + eik_last_error) -- there is no CPU fallback: a
+// missing device is EIK_ERR_NODEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/eikonal.h"
+#include "eik_common.hpp"
+#include "eik_kernels.hpp"
+
+namespace eik {
+hipError_t bidir_join(const double* d_TG, const double* d_TS, int64_t n, void* d_work, size_t work_bytes,
+                      unsigned long long* d_best, hipStream_t st);
+size_t bidir_join_work_bytes(int64_t n);
+}  // namespace eik
+
+using namespace eik;
+
+namespace {
+
+thread_local std::string g_create_err;
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= bytes) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        hipError_t e = hipMalloc(&p, n);
+        if (e == hipSuccess) bytes = n;
+        return e;
+    }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+}  // namespace
+
+struct eik_ctx {
+    int device = 0;
+    int cu_count = 256;
+    hipStream_t stream = nullptr;
+    std::string err;
+    int max_rounds = 1;
+    int sync_every = 8;
+    int timing = 0;
+    int grid = 0;
+    eik_stats last{};
+    eik_fim2d* cached = nullptr;  // solver reused by the host-buffer entry points
+    DevBuf cost, T, T2, goals, work, misc;
+};
+
+struct eik_fim2d {
+    eik_ctx* ctx = nullptr;
+    int64_t B = 0, H = 0, W = 0;
+    bool f64 = false;
+    Fim2dArgs a{};
+    hipStream_t stream = nullptr;
+    DevBuf lists, counts, mark, visits, edge, goals;
+    int* h_counts = nullptr;             // pinned
+    unsigned long long* h_visits = nullptr;
+    int64_t iterations = 0, host_syncs = 0, max_iters = 0;
+    hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+    std::vector<hipEvent_t> ev_pool;     // per-launch timing pairs (timing option)
+    size_t ev_used = 0;
+    double sweep_ms = 0.0, solve_ms = 0.0;
+    bool started = false;
+};
+
+static int set_err(eik_ctx* c, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (c)
+        c->err = buf;
+    else
+        g_create_err = buf;
+    return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                          \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess)                                                                      \
+            return set_err((ctx), e_ == hipErrorOutOfMemory ? EIK_ERR_NOMEM : EIK_ERR_HIP, "%s: %s (%s:%d)", \
+                           #expr, hipGetErrorString(e_), __FILE__, __LINE__);                      \
+    } while (0)
+
+static int bytes_per_visit(bool f64) { return (f64 ? 8 : 4) * (3 * kTile * kTile + 4 * kTile); }
+
+extern "C" {
+
+const char* eik_version(void) { return "eikonal-mi355x 0.1 (gfx950 block-FIM, 64x64 tiles)"; }
+
+int eik_create(int device, eik_ctx** out) {
+    if (!out) return set_err(nullptr, EIK_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return set_err(nullptr, EIK_ERR_NODEVICE, "no HIP device visible (the Eikonal solver has no CPU path)");
+    if (device < 0 || device >= n) return set_err(nullptr, EIK_ERR_ARG, "device %d out of range [0,%d)", device, n);
+    if (hipSetDevice(device) != hipSuccess) return set_err(nullptr, EIK_ERR_HIP, "hipSetDevice(%d) failed", device);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess)
+        return set_err(nullptr, EIK_ERR_HIP, "hipGetDeviceProperties failed");
+    auto* c = new eik_ctx();
+    c->device = device;
+    c->cu_count = prop.multiProcessorCount;
+    c->grid = 4 * c->cu_count;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return set_err(nullptr, EIK_ERR_HIP, "hipStreamCreate failed");
+    }
+    *out = c;
+    return EIK_OK;
+}
+
+void eik_destroy(eik_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->cached) eik_fim2d_destroy(c->cached);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* eik_last_error(const eik_ctx* c) { return c ? c->err.c_str() : g_create_err.c_str(); }
+
+int eik_set_option(eik_ctx* c, int opt, double v) {
+    if (!c) return EIK_ERR_ARG;
+    switch (opt) {
+        case EIK_OPT_MAX_ROUNDS: c->max_rounds = std::max(1, (int)v); break;
+        case EIK_OPT_SYNC_EVERY: c->sync_every = std::max(1, (int)v); break;
+        case EIK_OPT_TIMING: c->timing = v != 0; break;
+        case EIK_OPT_GRID: c->grid = v > 0 ? (int)v : 4 * c->cu_count; break;
+        default: return set_err(c, EIK_ERR_ARG, "unknown option %d", opt);
+    }
+    return EIK_OK;
+}
+
+int eik_get_stats(const eik_ctx* c, eik_stats* out) {
+    if (!c || !out) return EIK_ERR_ARG;
+    *out = c->last;
+    return EIK_OK;
+}
+
+// ------------------------------------------------------------------------------ fim2d
+int eik_fim2d_create(eik_ctx* c, int64_t B, int64_t H, int64_t W, int dtype, eik_fim2d** out) {
+    if (!c || !out) return EIK_ERR_ARG;
+    *out = nullptr;
+    if (B < 1 || H < 1 || W < 1) return set_err(c, EIK_ERR_ARG, "bad shape B=%ld H=%ld W=%ld", (long)B, (long)H, (long)W);
+    if (dtype != EIK_F32 && dtype != EIK_F64) return set_err(c, EIK_ERR_ARG, "bad dtype %d", dtype);
+    const int64_t ntx = (W + kTile - 1) / kTile, nty = (H + kTile - 1) / kTile;
+    const int64_t tiles = B * ntx * nty;
+    if (tiles >= (1ll << 31) - 8) return set_err(c, EIK_ERR_ARG, "too many tiles");
+    HIPCHK(c, hipSetDevice(c->device));
+    auto* f = new eik_fim2d();
+    f->ctx = c;
+    f->B = B;
+    f->H = H;
+    f->W = W;
+    f->f64 = dtype == EIK_F64;
+    f->stream = c->stream;
+    Fim2dArgs& a = f->a;
+    a.H = H;
+    a.W = W;
+    a.ntx = (int)ntx;
+    a.nty = (int)nty;
+    a.tiles_per_map = (int)(ntx * nty);
+    a.capacity = (int)tiles;
+    for (auto& g : a.ghost) g = nullptr;
+    hipError_t e = hipSuccess;
+    if ((e = f->lists.ensure(sizeof(int) * 3 * tiles)) != hipSuccess ||
+        (e = f->counts.ensure(sizeof(int) * 64)) != hipSuccess || (e = f->mark.ensure(sizeof(unsigned) * tiles)) != hipSuccess ||
+        (e = f->visits.ensure(sizeof(unsigned long long))) != hipSuccess ||
+        (e = f->edge.ensure(sizeof(unsigned) * 4)) != hipSuccess || (e = f->goals.ensure(sizeof(int64_t) * 2 * B)) != hipSuccess ||
+        (e = hipHostMalloc((void**)&f->h_counts, sizeof(int) * 64)) != hipSuccess ||
+        (e = hipHostMalloc((void**)&f->h_visits, sizeof(unsigned long long))) != hipSuccess ||
+        (e = hipEventCreate(&f->ev_start)) != hipSuccess || (e = hipEventCreate(&f->ev_stop)) != hipSuccess) {
+        eik_fim2d_destroy(f);
+        return set_err(c, EIK_ERR_NOMEM, "fim2d allocation: %s", hipGetErrorString(e));
+    }
+    a.lists = (int*)f->lists.p;
+    a.counts = (int*)f->counts.p;
+    a.mark = (unsigned*)f->mark.p;
+    a.visits = (unsigned long long*)f->visits.p;
+    a.edge_dirty = nullptr;
+    // safety cap: a monotone solve visits each tile a bounded number of times; negative costs
+    // (invalid input on a device buffer) would otherwise iterate forever.
+    f->max_iters = 64 * (ntx + nty) + 8 * tiles / B + 4096;
+    *out = f;
+    return EIK_OK;
+}
+
+void eik_fim2d_destroy(eik_fim2d* f) {
+    if (!f) return;
+    if (f->h_counts) (void)hipHostFree(f->h_counts);
+    if (f->h_visits) (void)hipHostFree(f->h_visits);
+    if (f->ev_start) (void)hipEventDestroy(f->ev_start);
+    if (f->ev_stop) (void)hipEventDestroy(f->ev_stop);
+    for (auto ev : f->ev_pool) (void)hipEventDestroy(ev);
+    delete f;
+}
+
+int eik_fim2d_set_ghosts(eik_fim2d* f, void* n, void* s, void* w, void* e) {
+    if (!f) return EIK_ERR_ARG;
+    if (f->B != 1) return set_err(f->ctx, EIK_ERR_ARG, "ghost strips need B == 1");
+    f->a.ghost[0] = n;
+    f->a.ghost[1] = s;
+    f->a.ghost[2] = w;
+    f->a.ghost[3] = e;
+    f->a.edge_dirty = (n || s || w || e) ? (unsigned*)f->edge.p : nullptr;
+    return EIK_OK;
+}
+
+int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* goals, void* stream) {
+    if (!f || !d_cost || !d_T || !goals) return EIK_ERR_ARG;
+    eik_ctx* c = f->ctx;
+    HIPCHK(c, hipSetDevice(c->device));
+    f->stream = stream ? (hipStream_t)stream : c->stream;
+    f->a.cost = d_cost;
+    f->a.T = d_T;
+    f->a.iter = 0;
+    f->a.max_rounds = c->max_rounds;
+    f->iterations = 0;
+    f->host_syncs = 0;
+    f->sweep_ms = 0.0;
+    f->solve_ms = 0.0;
+    f->ev_used = 0;
+    HIPCHK(c, hipEventRecord(f->ev_start, f->stream));
+    HIPCHK(c, hipMemcpyAsync(f->goals.p, goals, sizeof(int64_t) * 2 * f->B, hipMemcpyHostToDevice, f->stream));
+    HIPCHK(c, hipMemsetAsync(f->visits.p, 0, sizeof(unsigned long long), f->stream));
+    HIPCHK(c, hipMemsetAsync(f->edge.p, 0, sizeof(unsigned) * 4, f->stream));
+    HIPCHK(c, fim2d_init(f->a, f->f64, (int)f->B, (const int64_t*)f->goals.p, f->stream));
+    f->started = true;
+    return EIK_OK;
+}
+
+static int drain_timing(eik_fim2d* f) {
+    // events were recorded in (start, stop) pairs; the stream has been synchronised
+    for (size_t i = 0; i + 1 < f->ev_used; i += 2) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, f->ev_pool[i], f->ev_pool[i + 1]) == hipSuccess) f->sweep_ms += ms;
+    }
+    f->ev_used = 0;
+    return EIK_OK;
+}
+
+int eik_fim2d_iterate(eik_fim2d* f, int64_t max_iters, int64_t* active) {
+    if (!f || !f->started) return EIK_ERR_ARG;
+    eik_ctx* c = f->ctx;
+    HIPCHK(c, hipSetDevice(c->device));
+    int64_t done = 0;
+    int h = 1;
+    const int grid = c->grid > 0 ? c->grid : 4 * c->cu_count;
+    while (done < max_iters) {
+        const int64_t K = std::min<int64_t>(c->sync_every, max_iters - done);
+        for (int64_t k = 0; k < K; ++k) {
+            f->a.iter = (unsigned)f->iterations;
+            if (c->timing) {
+                while (f->ev_pool.size() < f->ev_used + 2) {
+                    hipEvent_t ev;
+                    HIPCHK(c, hipEventCreate(&ev));
+                    f->ev_pool.push_back(ev);
+                }
+                HIPCHK(c, hipEventRecord(f->ev_pool[f->ev_used++], f->stream));
+            }
+            HIPCHK(c, fim2d_sweep(f->a, f->f64, grid, f->stream));
+            if (c->timing) HIPCHK(c, hipEventRecord(f->ev_pool[f->ev_used++], f->stream));
+            ++f->iterations;
+        }
+        done += K;
+        HIPCHK(c, hipMemcpyAsync(f->h_counts, (int*)f->counts.p + (f->iterations % 3), sizeof(int),
+                                 hipMemcpyDeviceToHost, f->stream));
+        HIPCHK(c, hipStreamSynchronize(f->stream));
+        ++f->host_syncs;
+        if (c->timing) drain_timing(f);
+        h = f->h_counts[0];
+        if (h == 0) break;
+    }
+    if (active) *active = h;
+    return EIK_OK;
+}
+
+int eik_fim2d_active(eik_fim2d* f, int64_t* active) {
+    if (!f || !active) return EIK_ERR_ARG;
+    eik_ctx* c = f->ctx;
+    HIPCHK(c, hipMemcpyAsync(f->h_counts, (int*)f->counts.p + (f->iterations % 3), sizeof(int), hipMemcpyDeviceToHost,
+                             f->stream));
+    HIPCHK(c, hipStreamSynchronize(f->stream));
+    *active = f->h_counts[0];
+    return EIK_OK;
+}
+
+static int finish_solve(eik_fim2d* f) {
+    eik_ctx* c = f->ctx;
+    HIPCHK(c, hipEventRecord(f->ev_stop, f->stream));
+    HIPCHK(c, hipMemcpyAsync(f->h_visits, f->visits.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, f->stream));
+    HIPCHK(c, hipStreamSynchronize(f->stream));
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, f->ev_start, f->ev_stop);
+    f->solve_ms = ms;
+    eik_fim2d_stats(f, &c->last);
+    return EIK_OK;
+}
+
+int eik_fim2d_solve(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* goals, void* stream) {
+    int rc = eik_fim2d_start(f, d_cost, d_T, goals, stream);
+    if (rc) return rc;
+    int64_t active = 0;
+    rc = eik_fim2d_iterate(f, f->max_iters, &active);
+    if (rc) return rc;
+    rc = finish_solve(f);
+    if (rc) return rc;
+    if (active != 0)
+        return set_err(f->ctx, EIK_ERR_NOCONVERGE, "no convergence after %ld iterations (negative costs?)",
+                       (long)f->iterations);
+    return EIK_OK;
+}
+
+int eik_fim2d_pack_edges(eik_fim2d* f, void* n, void* s, void* w, void* e) {
+    if (!f || !f->started) return EIK_ERR_ARG;
+    HIPCHK(f->ctx, fim2d_pack_edges(f->a, f->f64, n, s, w, e, f->stream));
+    return EIK_OK;
+}
+
+int eik_fim2d_merge_ghost(eik_fim2d* f, int side, const void* recv) {
+    if (!f || !f->started || side < 0 || side > 3 || !recv || !f->a.ghost[side]) return EIK_ERR_ARG;
+    f->a.iter = (unsigned)f->iterations;  // enqueue for the next sweep launch
+    HIPCHK(f->ctx, fim2d_merge_ghost(f->a, f->f64, side, recv, side < 2 ? f->W : f->H, f->stream));
+    return EIK_OK;
+}
+
+int eik_fim2d_stats(const eik_fim2d* f, eik_stats* out) {
+    if (!f || !out) return EIK_ERR_ARG;
+    out->iterations = f->iterations;
+    out->tile_visits = (int64_t)*f->h_visits;
+    out->host_syncs = f->host_syncs;
+    out->solve_ms = f->solve_ms;
+    out->sweep_ms = f->sweep_ms;
+    out->bytes_alg = (double)out->tile_visits * bytes_per_visit(f->f64) +
+                     (double)f->B * f->H * f->W * (f->f64 ? 8 : 4);
+    return EIK_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------- host-buffer drop-ins
+static int get_solver(eik_ctx* c, int64_t B, int64_t H, int64_t W, int dtype, eik_fim2d** out) {
+    eik_fim2d* f = c->cached;
+    if (f && f->B == B && f->H == H && f->W == W && (int)f->f64 == (dtype == EIK_F64)) {
+        *out = f;
+        return EIK_OK;
+    }
+    if (f) eik_fim2d_destroy(f);
+    c->cached = nullptr;
+    int rc = eik_fim2d_create(c, B, H, W, dtype, &f);
+    if (rc) return rc;
+    c->cached = f;
+    *out = f;
+    return EIK_OK;
+}
+
+template <typename R>
+static int check_cost(eik_ctx* c, const R* cost, int64_t n) {
+    for (int64_t i = 0; i < n; ++i) {
+        const R v = cost[i];
+        if (!(v >= R(0)))  // negative or NaN
+            return set_err(c, EIK_ERR_ARG, "cost[%ld] = %g: costs must be >= 0 or +inf", (long)i, (double)v);
+    }
+    return EIK_OK;
+}
+
+template <typename R>
+static int tmap_host(eik_ctx* c, const R* cost, int64_t B, int64_t H, int64_t W, const int64_t* goals, R* T) {
+    if (!c || !cost || !T || !goals || B < 1 || H < 1 || W < 1) return c ? set_err(c, EIK_ERR_ARG, "bad arguments") : EIK_ERR_ARG;
+    for (int64_t b = 0; b < B; ++b)
+        if (goals[2 * b] < 0 || goals[2 * b + 1] < 0 || goals[2 * b] >= W || goals[2 * b + 1] >= H)
+            return set_err(c, EIK_ERR_ARG, "goal (%ld, %ld) of map %ld outside %ldx%ld", (long)goals[2 * b],
+                           (long)goals[2 * b + 1], (long)b, (long)H, (long)W);
+    const int64_t n = B * H * W;
+    int rc = check_cost(c, cost, n);
+    if (rc) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    eik_fim2d* f = nullptr;
+    rc = get_solver(c, B, H, W, sizeof(R) == 8 ? EIK_F64 : EIK_F32, &f);
+    if (rc) return rc;
+    HIPCHK(c, c->cost.ensure(sizeof(R) * n));
+    HIPCHK(c, c->T.ensure(sizeof(R) * n));
+    HIPCHK(c, hipMemcpyAsync(c->cost.p, cost, sizeof(R) * n, hipMemcpyHostToDevice, c->stream));
+    rc = eik_fim2d_solve(f, c->cost.p, c->T.p, goals, c->stream);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(T, c->T.p, sizeof(R) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return EIK_OK;
+}
+
+extern "C" {
+
+int eik_tmap2d_f32(eik_ctx* c, const float* cost, int64_t H, int64_t W, int64_t gx, int64_t gy, float* T) {
+    const int64_t g[2] = {gx, gy};
+    return tmap_host<float>(c, cost, 1, H, W, g, T);
+}
+
+int eik_tmap2d_f64(eik_ctx* c, const double* cost, int64_t H, int64_t W, int64_t gx, int64_t gy, double* T) {
+    const int64_t g[2] = {gx, gy};
+    return tmap_host<double>(c, cost, 1, H, W, g, T);
+}
+
+int eik_tmap2d_batch_f32(eik_ctx* c, const float* cost, int64_t B, int64_t H, int64_t W, const int64_t* goals,
+                         float* T) {
+    return tmap_host<float>(c, cost, B, H, W, goals, T);
+}
+
+int eik_tmap2d_bidir_f64(eik_ctx* c, const double* cost, int64_t H, int64_t W, int64_t gx, int64_t gy, int64_t sx,
+                         int64_t sy, double* TG, double* TS, uint32_t join[2]) {
+    if (!c || !cost || !TG || !TS || !join) return c ? set_err(c, EIK_ERR_ARG, "NULL argument") : EIK_ERR_ARG;
+    const int64_t n = H * W;
+    if (n >= (1ll << 29)) return set_err(c, EIK_ERR_ARG, "bidirectional join supports < 2^29 cells");
+    // both fronts as one 2-map batch: map 0 from the goal, map 1 from the start
+    std::vector<double> cost2((size_t)(2 * n));
+    std::memcpy(cost2.data(), cost, sizeof(double) * n);
+    std::memcpy(cost2.data() + n, cost, sizeof(double) * n);
+    const int64_t goals[4] = {gx, gy, sx, sy};
+    std::vector<double> T2((size_t)(2 * n));
+    int rc = tmap_host<double>(c, cost2.data(), 2, H, W, goals, T2.data());
+    if (rc) return rc;
+    // join from the device-resident fields (c->T holds both maps back to back)
+    const size_t wb = bidir_join_work_bytes(n);
+    HIPCHK(c, c->work.ensure(wb));
+    HIPCHK(c, c->misc.ensure(64));
+    HIPCHK(c, bidir_join((const double*)c->T.p, (const double*)c->T.p + n, n, c->work.p, c->work.bytes,
+                         (unsigned long long*)c->misc.p, c->stream));
+    unsigned long long best = 0;
+    HIPCHK(c, hipMemcpyAsync(&best, c->misc.p, sizeof best, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::memcpy(TG, T2.data(), sizeof(double) * n);
+    std::memcpy(TS, T2.data() + n, sizeof(double) * n);
+    if (best == ~0ull) return set_err(c, EIK_ERR_UNREACHABLE, "goal and start are not connected");
+    const int64_t node = (int64_t)(best & ((1ull << 29) - 1));
+    join[0] = (uint32_t)(node % W);
+    join[1] = (uint32_t)(node / W);
+    return EIK_OK;
+}
+
+int eik_path2d_dev(eik_ctx* c, const void* d_T, int dtype, int64_t H, int64_t W, const double init[2],
+                   const double end[2], double tau, double* d_out, int64_t cap, int64_t* d_n_out, int* d_status,
+                   void* stream) {
+    if (!c || !d_T || !init || !end || !d_out || !d_n_out || !d_status || cap < 2 || H < 3 || W < 3 || !(tau > 0))
+        return c ? set_err(c, EIK_ERR_ARG, "bad path arguments") : EIK_ERR_ARG;
+    Gdm2dArgs a;
+    a.T = d_T;
+    a.H = H;
+    a.W = W;
+    a.ix = init[0];
+    a.iy = init[1];
+    a.ex = end[0];
+    a.ey = end[1];
+    a.tau = tau;
+    a.steps = (long)std::nearbyint(15000.0 / tau);  // round(15000/tau), FastMarching.py:173
+    a.out = d_out;
+    a.cap = cap;
+    a.n_out = d_n_out;
+    a.status = d_status;
+    HIPCHK(c, gdm2d(a, dtype == EIK_F64, stream ? (hipStream_t)stream : c->stream));
+    return EIK_OK;
+}
+
+int eik_path2d_f64(eik_ctx* c, const double* T, int64_t H, int64_t W, const double init[2], const double end[2],
+                   double tau, double* out, int64_t cap, int64_t* n_out, int* status) {
+    if (!c || !T || !out || !n_out || !status) return c ? set_err(c, EIK_ERR_ARG, "NULL argument") : EIK_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t n = H * W;
+    HIPCHK(c, c->T2.ensure(sizeof(double) * n));
+    HIPCHK(c, c->work.ensure(sizeof(double) * 2 * cap + 64));
+    HIPCHK(c, hipMemcpyAsync(c->T2.p, T, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    double* d_out = (double*)c->work.p;
+    int64_t* d_n = (int64_t*)(d_out + 2 * cap);
+    int* d_st = (int*)(d_n + 1);
+    int rc = eik_path2d_dev(c, c->T2.p, EIK_F64, H, W, init, end, tau, d_out, cap, d_n, d_st, c->stream);
+    if (rc) return rc;
+    int64_t nn = 0;
+    int st = 0;
+    HIPCHK(c, hipMemcpyAsync(&nn, d_n, sizeof nn, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&st, d_st, sizeof st, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (nn > cap) nn = cap;
+    HIPCHK(c, hipMemcpy(out, d_out, sizeof(double) * 2 * nn, hipMemcpyDeviceToHost));
+    *n_out = nn;
+    *status = st;
+    return EIK_OK;
+}
+
+int eik_gradient2d_f64(eik_ctx* c, const double* T, int64_t H, int64_t W, double* gnx, double* gny) {
+    if (!c || !T || !gnx || !gny || H < 2 || W < 2) return c ? set_err(c, EIK_ERR_ARG, "bad arguments") : EIK_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t n = H * W;
+    HIPCHK(c, c->T2.ensure(sizeof(double) * n));
+    HIPCHK(c, c->work.ensure(sizeof(double) * 2 * n));
+    HIPCHK(c, hipMemcpyAsync(c->T2.p, T, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    double* gx = (double*)c->work.p;
+    HIPCHK(c, gradient2d((const double*)c->T2.p, H, W, gx, gx + n, c->stream));
+    HIPCHK(c, hipMemcpyAsync(gnx, gx, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(gny, gx + n, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return EIK_OK;
+}
+
+}  // extern "C"

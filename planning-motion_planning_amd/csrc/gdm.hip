@@ -1,0 +1,170 @@
+// gdm.hip -- gradient-descent path extraction (getPathGDM, FastMarching.py:164-236) and the
+// inf-aware normalised gradient (computeGradient, FastMarching.py:242-300) on gfx950.
+//
+// The path is inherently sequential (<= round(15000/tau) dependent steps), so it runs as ONE
+// small kernel: a single wave whose lane 0 walks the field.  Per step the reference builds the
+// normalised gradient in a 6x6 window (allocating four full-size arrays, :255-258) but only ever
+// reads it at the four bilinear corners; the kernel evaluates the gradient at exactly those
+// four corners (bit-identical control flow, see oracle/eikonal_oracle.c grad_at/orc_gdm2d).
+//
+// Arithmetic is IEEE fp64 with contraction disabled.  The one deliberate difference: the
+// reference squares numpy scalars with `x**2`, which goes through glibc pow() and is not
+// always correctly rounded; the device uses the exact product x*x (<= 1 ulp per square,
+// tolerance stated in tests/test_gpu_parity.py).
+#include "eik_common.hpp"
+#include "eik_kernels.hpp"
+
+#pragma clang fp contract(off)
+
+namespace eik {
+
+template <typename R>
+__device__ __forceinline__ double tv(const R* __restrict__ T, int64_t W, int64_t j, int64_t i) {
+    return (double)T[j * W + i];
+}
+
+// computeGradient body at one (j, i), FastMarching.py:262-297
+template <typename R>
+__device__ void grad_at(const R* __restrict__ T, int64_t m, int64_t n, int64_t j, int64_t i, double& gnx, double& gny) {
+    double gy, gx;
+    if (j == 0)
+        gy = tv(T, n, 1, i) - tv(T, n, 0, i);
+    else if (j == m - 1)
+        gy = tv(T, n, j, i) - tv(T, n, j - 1, i);
+    else if (__builtin_isinf(tv(T, n, j + 1, i)))
+        gy = __builtin_isinf(tv(T, n, j - 1, i)) ? 0.0 : tv(T, n, j, i) - tv(T, n, j - 1, i);
+    else
+        gy = __builtin_isinf(tv(T, n, j - 1, i)) ? tv(T, n, j + 1, i) - tv(T, n, j, i)
+                                                 : (tv(T, n, j + 1, i) - tv(T, n, j - 1, i)) / 2;
+    if (i == 0)
+        gx = tv(T, n, j, 1) - tv(T, n, j, 0);
+    else if (i == n - 1)
+        gx = tv(T, n, j, i) - tv(T, n, j, i - 1);
+    else if (__builtin_isinf(tv(T, n, j, i + 1)))
+        gx = __builtin_isinf(tv(T, n, j, i - 1)) ? 0.0 : tv(T, n, j, i) - tv(T, n, j, i - 1);
+    else
+        gx = __builtin_isinf(tv(T, n, j, i - 1)) ? tv(T, n, j, i + 1) - tv(T, n, j, i)
+                                                 : (tv(T, n, j, i + 1) - tv(T, n, j, i - 1)) / 2;
+    const double den = __builtin_sqrt(gx * gx + gy * gy);
+    gnx = gx / den;
+    gny = gy / den;
+}
+
+// interpolatePoint FastMarching.py:305-338 on a 2x2 patch g[jj][ii]
+__device__ __forceinline__ double interp2_patch(double a, double b, const double (&g)[2][2]) {
+    const double a00 = g[0][0];
+    const double a10 = g[0][1] - g[0][0];
+    const double a01 = g[1][0] - g[0][0];
+    const double a11 = g[1][1] + g[0][0] - g[0][1] - g[1][0];
+    if (a == 0) return b == 0 ? a00 : a00 + a01 * b;
+    return b == 0 ? a00 + a10 * a : a00 + a10 * a + a01 * b + a11 * a * b;
+}
+
+__device__ __forceinline__ double norm2(double a, double b) { return __builtin_sqrt(a * a + b * b); }
+
+enum { kGdmDone = 0, kGdmFallback = 1, kGdmError = 2 };
+
+template <typename R>
+__global__ __launch_bounds__(64) void gdm2d_kernel(Gdm2dArgs a) {
+    if (threadIdx.x != 0) return;
+    const R* __restrict__ T = static_cast<const R*>(a.T);
+    const int64_t H = a.H, W = a.W;
+    double* out = a.out;
+    int64_t n = 0;
+    int status = kGdmDone;
+    out[0] = a.ix;
+    out[1] = a.iy;
+    n = 1;
+    const double tau = a.tau;
+    bool finished = false;
+    for (long k = 0; k < a.steps && !finished; ++k) {
+        const double px = out[2 * (n - 1)], py = out[2 * (n - 1) + 1];
+        if (__builtin_isnan(px) || __builtin_isnan(py)) { status = kGdmError; finished = true; break; }
+        const uint32_t i = (uint32_t)__builtin_trunc(px), j = (uint32_t)__builtin_trunc(py);
+        if (i + 1 >= (uint64_t)W || j + 1 >= (uint64_t)H) { status = kGdmError; finished = true; break; }
+        double gx[2][2], gy[2][2];
+        for (int jj = 0; jj < 2; ++jj)
+            for (int ii = 0; ii < 2; ++ii) grad_at<R>(T, H, W, j + jj, i + ii, gx[jj][ii], gy[jj][ii]);
+        const double fa = px - i, fb = py - j;
+        double dx = interp2_patch(fa, fb, gx);
+        double dy = interp2_patch(fa, fb, gy);
+        if (__builtin_isnan(dx) || __builtin_isnan(dy)) {
+            // NaN fallback (:178-218) as the reference behaves under numpy 2: the neighbour
+            // probe `np.uint32(nearN + [0,-1])` raises OverflowError, caught at :217.
+            int64_t nx = (int64_t)__builtin_rint(px), ny = (int64_t)__builtin_rint(py);
+            bool empty = false, oob = false;
+            for (;;) {
+                const int64_t wx = nx < 0 ? nx + W : nx, wy = ny < 0 ? ny + H : ny;
+                if (wx < 0 || wy < 0 || wx >= W || wy >= H) { oob = true; break; }
+                if (!__builtin_isinf(tv(T, W, wy, wx))) break;
+                --n;
+                if (n == 0) { empty = true; break; }
+                nx = (int64_t)__builtin_rint(out[2 * (n - 1)]);
+                ny = (int64_t)__builtin_rint(out[2 * (n - 1) + 1]);
+            }
+            if (!empty && !oob) {
+                while (n > 0 && norm2(out[2 * (n - 1)] - (double)nx, out[2 * (n - 1) + 1] - (double)ny) < 1) --n;
+                if (n < a.cap) {
+                    out[2 * n] = (double)nx;
+                    out[2 * n + 1] = (double)ny;
+                    ++n;
+                }
+            }
+            status = kGdmFallback;
+            finished = true;
+            break;
+        }
+        double sx, sy;
+        if (norm2(dx, dy) < 0.01) {  // :220-224
+            const double dnx = dx / __builtin_sqrt(dx * dx + dy * dy);
+            const double dny = dy / __builtin_sqrt(dx * dx + dy * dy);
+            sx = px - tau * dnx;
+            sy = py - tau * dny;
+        } else {  // :225-229 (dy normalised with the already-normalised dx)
+            dx = dx / __builtin_sqrt(dx * dx + dy * dy);
+            dy = dy / __builtin_sqrt(dx * dx + dy * dy);
+            sx = px - tau * dx;
+            sy = py - tau * dy;
+        }
+        if (n >= a.cap) { status = kGdmError; finished = true; break; }
+        out[2 * n] = sx;
+        out[2 * n + 1] = sy;
+        ++n;
+        if (norm2(sx - a.ex, sy - a.ey) < 1.5) break;  // :231-232
+    }
+    if (status == kGdmDone && n < a.cap) {  // :234
+        out[2 * n] = a.ex;
+        out[2 * n + 1] = a.ey;
+        ++n;
+    }
+    *a.n_out = n;
+    *a.status = status;
+}
+
+hipError_t gdm2d(const Gdm2dArgs& a, bool f64, hipStream_t st) {
+    if (f64)
+        hipLaunchKernelGGL(gdm2d_kernel<double>, dim3(1), dim3(64), 0, st, a);
+    else
+        hipLaunchKernelGGL(gdm2d_kernel<float>, dim3(1), dim3(64), 0, st, a);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- full-field gradient
+__global__ void gradient2d_kernel(const double* __restrict__ T, int64_t H, int64_t W, double* __restrict__ gnx,
+                                  double* __restrict__ gny) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= H * W) return;
+    const int64_t j = idx / W, i = idx - (idx / W) * W;
+    double a, b;
+    grad_at<double>(T, H, W, j, i, a, b);
+    gnx[idx] = a;
+    gny[idx] = b;
+}
+
+hipError_t gradient2d(const double* T, int64_t H, int64_t W, double* gnx, double* gny, hipStream_t st) {
+    const int64_t n = H * W;
+    hipLaunchKernelGGL(gradient2d_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, T, H, W, gnx, gny);
+    return hipGetLastError();
+}
+
+}  // namespace eik

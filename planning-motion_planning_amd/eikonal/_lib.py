@@ -1,0 +1,235 @@
+"""ctypes binding of libeikonal.so (include/eikonal.h), mirroring the C ABI one-to-one."""
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("EIKONAL_LIB", os.path.join(PKG_DIR, "lib", "libeikonal.so"))
+
+EIK_OK, EIK_ERR_ARG, EIK_ERR_HIP, EIK_ERR_NOMEM, EIK_ERR_NOCONVERGE, EIK_ERR_UNREACHABLE, EIK_ERR_NODEVICE = \
+    0, -1, -2, -3, -4, -5, -6
+EIK_F32, EIK_F64 = 0, 1
+PATH_DONE, PATH_FALLBACK, PATH_ERROR = 0, 1, 2
+OPT_MAX_ROUNDS, OPT_SYNC_EVERY, OPT_TIMING, OPT_GRID = 0, 1, 2, 3
+
+i64 = C.c_int64
+vp = C.c_void_p
+_f32p = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_i64p = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
+_u32p = np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS")
+
+
+class EikStats(C.Structure):
+    _fields_ = [("iterations", i64), ("tile_visits", i64), ("host_syncs", i64), ("solve_ms", C.c_double),
+                ("sweep_ms", C.c_double), ("bytes_alg", C.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class EikError(RuntimeError):
+    def __init__(self, code, msg):
+        self.code = code
+        super().__init__(f"eikonal error {code}: {msg}")
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib():
+    """Load libeikonal.so; raise (never fall back) when it is absent."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise EikError(EIK_ERR_NODEVICE, f"{LIB_PATH} not built (run __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        P = C.POINTER
+        L.eik_version.restype = C.c_char_p
+        L.eik_create.argtypes = [C.c_int, P(vp)]
+        L.eik_destroy.argtypes = [vp]
+        L.eik_destroy.restype = None
+        L.eik_last_error.argtypes = [vp]
+        L.eik_last_error.restype = C.c_char_p
+        L.eik_set_option.argtypes = [vp, C.c_int, C.c_double]
+        L.eik_get_stats.argtypes = [vp, P(EikStats)]
+        L.eik_tmap2d_f32.argtypes = [vp, _f32p, i64, i64, i64, i64, _f32p]
+        L.eik_tmap2d_f64.argtypes = [vp, _f64p, i64, i64, i64, i64, _f64p]
+        L.eik_tmap2d_bidir_f64.argtypes = [vp, _f64p, i64, i64, i64, i64, i64, i64, _f64p, _f64p, _u32p]
+        L.eik_tmap2d_batch_f32.argtypes = [vp, _f32p, i64, i64, i64, _i64p, _f32p]
+        L.eik_path2d_f64.argtypes = [vp, _f64p, i64, i64, _f64p, _f64p, C.c_double, _f64p, i64, P(i64), P(C.c_int)]
+        L.eik_gradient2d_f64.argtypes = [vp, _f64p, i64, i64, _f64p, _f64p]
+        L.eik_fim2d_create.argtypes = [vp, i64, i64, i64, C.c_int, P(vp)]
+        L.eik_fim2d_destroy.argtypes = [vp]
+        L.eik_fim2d_destroy.restype = None
+        L.eik_fim2d_set_ghosts.argtypes = [vp, vp, vp, vp, vp]
+        L.eik_fim2d_start.argtypes = [vp, vp, vp, _i64p, vp]
+        L.eik_fim2d_iterate.argtypes = [vp, i64, P(i64)]
+        L.eik_fim2d_solve.argtypes = [vp, vp, vp, _i64p, vp]
+        L.eik_fim2d_pack_edges.argtypes = [vp, vp, vp, vp, vp]
+        L.eik_fim2d_merge_ghost.argtypes = [vp, C.c_int, vp]
+        L.eik_fim2d_active.argtypes = [vp, P(i64)]
+        L.eik_fim2d_stats.argtypes = [vp, P(EikStats)]
+        L.eik_path2d_dev.argtypes = [vp, vp, C.c_int, i64, i64, _f64p, _f64p, C.c_double, vp, i64, vp, vp, vp]
+        _lib = L
+        return L
+
+
+EXPORTED = [
+    "eik_version", "eik_create", "eik_destroy", "eik_last_error", "eik_set_option", "eik_get_stats",
+    "eik_tmap2d_f32", "eik_tmap2d_f64", "eik_tmap2d_bidir_f64", "eik_tmap2d_batch_f32", "eik_path2d_f64",
+    "eik_gradient2d_f64", "eik_fim2d_create", "eik_fim2d_destroy", "eik_fim2d_set_ghosts", "eik_fim2d_start",
+    "eik_fim2d_iterate", "eik_fim2d_solve", "eik_fim2d_pack_edges", "eik_fim2d_merge_ghost", "eik_fim2d_active",
+    "eik_fim2d_stats", "eik_path2d_dev",
+]
+
+
+class Context:
+    """One eik_ctx (device state + HIP stream); use one per host thread."""
+
+    def __init__(self, device=0):
+        L = lib()
+        h = vp()
+        rc = L.eik_create(int(device), C.byref(h))
+        if rc != EIK_OK:
+            raise EikError(rc, L.eik_last_error(None).decode())
+        self._h = h
+        self.device = device
+
+    def _chk(self, rc):
+        if rc != EIK_OK:
+            raise EikError(rc, lib().eik_last_error(self._h).decode())
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().eik_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_option(self, opt, value):
+        self._chk(lib().eik_set_option(self._h, int(opt), float(value)))
+
+    def stats(self):
+        s = EikStats()
+        self._chk(lib().eik_get_stats(self._h, C.byref(s)))
+        return s.as_dict()
+
+    # -- host-buffer drop-ins -------------------------------------------------------------
+    def tmap2d(self, cost, goal, dtype=np.float64):
+        cost = np.ascontiguousarray(cost, dtype=dtype)
+        H, W = cost.shape
+        T = np.empty_like(cost)
+        fn = lib().eik_tmap2d_f64 if cost.dtype == np.float64 else lib().eik_tmap2d_f32
+        self._chk(fn(self._h, cost, H, W, int(goal[0]), int(goal[1]), T))
+        return T
+
+    def tmap2d_batch(self, costs, goals):
+        costs = np.ascontiguousarray(costs, dtype=np.float32)
+        B, H, W = costs.shape
+        T = np.empty_like(costs)
+        self._chk(lib().eik_tmap2d_batch_f32(self._h, costs, B, H, W, np.ascontiguousarray(goals, np.int64), T))
+        return T
+
+    def tmap2d_bidir(self, cost, goal, start):
+        cost = np.ascontiguousarray(cost, dtype=np.float64)
+        H, W = cost.shape
+        TG, TS = np.empty_like(cost), np.empty_like(cost)
+        join = np.zeros(2, np.uint32)
+        self._chk(lib().eik_tmap2d_bidir_f64(self._h, cost, H, W, int(goal[0]), int(goal[1]), int(start[0]),
+                                             int(start[1]), TG, TS, join))
+        return TG, TS, join
+
+    def path2d(self, T, init, end, tau=0.5):
+        T = np.ascontiguousarray(T, dtype=np.float64)
+        H, W = T.shape
+        cap = int(round(15000 / tau)) + 4
+        out = np.empty((cap, 2))
+        n, st = i64(0), C.c_int(0)
+        self._chk(lib().eik_path2d_f64(self._h, T, H, W, np.asarray(init, np.float64)[:2].copy(),
+                                       np.asarray(end, np.float64)[:2].copy(), float(tau), out, cap, C.byref(n),
+                                       C.byref(st)))
+        return out[: n.value].copy(), st.value
+
+    def gradient2d(self, T):
+        T = np.ascontiguousarray(T, dtype=np.float64)
+        H, W = T.shape
+        gx, gy = np.empty_like(T), np.empty_like(T)
+        self._chk(lib().eik_gradient2d_f64(self._h, T, H, W, gx, gy))
+        return gx, gy
+
+
+class Fim2d:
+    """Device-resident solver (eik_fim2d): device pointers in, async on a caller stream."""
+
+    def __init__(self, ctx, B, H, W, dtype=EIK_F32):
+        self.ctx = ctx
+        h = vp()
+        ctx._chk(lib().eik_fim2d_create(ctx._h, int(B), int(H), int(W), int(dtype), C.byref(h)))
+        self._h = h
+        self.B, self.H, self.W, self.dtype = B, H, W, dtype
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().eik_fim2d_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_ghosts(self, n, s, w, e):
+        self.ctx._chk(lib().eik_fim2d_set_ghosts(self._h, n, s, w, e))
+
+    def start(self, d_cost, d_T, goals, stream=None):
+        self.ctx._chk(lib().eik_fim2d_start(self._h, d_cost, d_T, np.ascontiguousarray(goals, np.int64).reshape(-1),
+                                            stream))
+
+    def iterate(self, max_iters):
+        a = i64(0)
+        self.ctx._chk(lib().eik_fim2d_iterate(self._h, int(max_iters), C.byref(a)))
+        return a.value
+
+    def solve(self, d_cost, d_T, goals, stream=None):
+        self.ctx._chk(lib().eik_fim2d_solve(self._h, d_cost, d_T, np.ascontiguousarray(goals, np.int64).reshape(-1),
+                                            stream))
+
+    def pack_edges(self, n, s, w, e):
+        self.ctx._chk(lib().eik_fim2d_pack_edges(self._h, n, s, w, e))
+
+    def merge_ghost(self, side, recv):
+        self.ctx._chk(lib().eik_fim2d_merge_ghost(self._h, int(side), recv))
+
+    def active(self):
+        a = i64(0)
+        self.ctx._chk(lib().eik_fim2d_active(self._h, C.byref(a)))
+        return a.value
+
+    def stats(self):
+        s = EikStats()
+        self.ctx._chk(lib().eik_fim2d_stats(self._h, C.byref(s)))
+        return s.as_dict()
+
+
+_default = {}
+
+
+def default_context(device=0):
+    """Per-thread default context used by the FastMarching drop-in."""
+    key = (threading.get_ident(), device)
+    c = _default.get(key)
+    if c is None:
+        c = Context(device)
+        _default[key] = c
+    return c

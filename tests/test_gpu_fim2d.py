@@ -1,0 +1,166 @@
+"""GPU parity of the HIP block-FIM (libeikonal, through the C ABI) against the oracle.
+
+Tolerances (BASELINE.md "Parity tolerance"):
+  * reachability masks (isfinite) identical, T[goal] == 0;
+  * fp32 field: max relative error <= 2e-5 over finite cells;
+  * fp64 field: max absolute error <= 1e-9.
+The golden fields were produced by the reference FastMarching.py itself (tests/golden/); larger
+maps are checked against the C oracle (bit-exact restatement of the reference, pinned by
+tests/test_oracle_golden.py).
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+RTOL32 = 2e-5
+ATOL64 = 1e-9
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import eikonal
+
+    c = eikonal.Context(0)
+    yield c
+    c.close()
+
+
+def check_field(T, R, goal, f64):
+    assert T.shape == R.shape
+    fin = np.isfinite(R)
+    assert np.array_equal(np.isfinite(T), fin), "reachability mask differs"
+    assert T[goal[1], goal[0]] == 0
+    if not fin.any():
+        return
+    err = np.abs(T[fin].astype(np.float64) - R[fin])
+    if f64:
+        assert err.max() <= ATOL64, err.max()
+    else:
+        rel = err / np.maximum(np.abs(R[fin]), 1e-30)
+        rel[R[fin] == 0] = err[R[fin] == 0]
+        assert rel.max() <= RTOL32, rel.max()
+
+
+def oracle_field(cost, goal):
+    O.set_strict(False)  # intended semantics (no StopIteration on tied decrease-keys)
+    try:
+        return O.fmm2d(np.asarray(cost, np.float64), goal)
+    finally:
+        O.set_strict(True)
+
+
+@pytest.mark.parametrize("i", range(13))
+@pytest.mark.parametrize("f64", [False, True])
+def test_golden_fields(ctx, golden, i, f64):
+    d = golden("fmm2d_fields")
+    p = f"c{i}_"
+    cost = d[p + "cost"].astype(np.float64)
+    goal = d[p + "goal"]
+    R = d[p + "T"] if not str(d[p + "err"]) else oracle_field(cost, goal)  # blobs_ties: ref raised
+    T = ctx.tmap2d(cost, goal, dtype=np.float64 if f64 else np.float32)
+    check_field(T, R, goal, f64)
+
+
+@pytest.mark.parametrize("shape,kind,seed", [
+    ((517, 1031), "obst", 1),      # ragged: neither side a multiple of the 64-cell tile
+    ((1024, 1024), "random", 2),
+    ((300, 70), "maze", 3),        # long winding front: many outer iterations
+    ((64, 64), "random", 4),       # exactly one tile
+    ((1, 200), "random", 5),       # degenerate strip
+    ((37, 1), "random", 6),
+    ((2048, 2048), "blobs", 7),
+])
+def test_vs_oracle(ctx, shape, kind, seed):
+    rng = np.random.default_rng(seed)
+    H, W = shape
+    c = rng.uniform(1, 10, shape)
+    if kind == "obst":
+        c[rng.random(shape) < 0.15] = np.inf
+    elif kind == "maze":
+        for x in range(4, W - 2, 8):  # walls with alternating gaps
+            c[:, x] = np.inf
+            gap = 2 if (x // 8) % 2 == 0 else H - 3
+            c[gap, x] = 3.0
+    elif kind == "blobs":
+        yy, xx = np.mgrid[0:H, 0:W]
+        for _ in range(40):
+            cy, cx, r = rng.integers(0, H), rng.integers(0, W), rng.integers(10, 80)
+            c[(yy - cy) ** 2 + (xx - cx) ** 2 <= r * r] = 300.0
+    c = c.astype(np.float32).astype(np.float64)
+    goal = [W // 3, H // 2] if W > 1 else [0, H // 2]
+    c[goal[1], goal[0]] = 1.0
+    R = oracle_field(c, goal)
+    check_field(ctx.tmap2d(c, goal, dtype=np.float32), R, goal, False)
+    if H * W <= 1 << 20:
+        check_field(ctx.tmap2d(c, goal, dtype=np.float64), R, goal, True)
+
+
+def test_enclosed_goal_and_unreachable(ctx):
+    c = np.full((90, 130), 2.0)
+    c[40:50, 60] = c[40:50, 70] = np.inf
+    c[40, 60:71] = c[49, 60:71] = np.inf  # goal boxed in
+    goal = [65, 45]
+    T = ctx.tmap2d(c, goal, dtype=np.float32)
+    R = oracle_field(c, goal)
+    check_field(T, R, goal, False)
+    assert np.isfinite(T).sum() == np.isfinite(R).sum() == 8 * 9
+
+
+def test_non_inf_border_matches_oob_as_inf(ctx):
+    rng = np.random.default_rng(11)
+    c = rng.uniform(0.5, 3, (150, 160))  # no inf border: out-of-range reads as +inf
+    check_field(ctx.tmap2d(c, [0, 0], dtype=np.float32), oracle_field(c, [0, 0]), [0, 0], False)
+
+
+def test_zero_cost_cells(ctx):
+    c = np.ones((80, 80))
+    c[30:50, 30:50] = 0.0  # free region: T constant across it
+    check_field(ctx.tmap2d(c, [40, 40], dtype=np.float64), oracle_field(c, [40, 40]), [40, 40], True)
+
+
+def test_bad_inputs_raise(ctx):
+    import eikonal
+
+    c = np.ones((10, 10))
+    with pytest.raises(eikonal.EikError):
+        ctx.tmap2d(c, [10, 3])  # goal outside
+    c[3, 3] = -1.0
+    with pytest.raises(eikonal.EikError):
+        ctx.tmap2d(c, [1, 1])  # negative cost rejected (reference semantics undefined)
+    c[3, 3] = np.nan
+    with pytest.raises(eikonal.EikError):
+        ctx.tmap2d(c, [1, 1])
+
+
+def test_batch_matches_single(ctx):
+    rng = np.random.default_rng(5)
+    B, H, W = 6, 190, 260
+    costs = rng.uniform(1, 8, (B, H, W)).astype(np.float32)
+    costs[:, rng.random((H, W)) < 0.1] = np.inf
+    goals = np.array([[rng.integers(0, W), rng.integers(0, H)] for _ in range(B)], np.int64)
+    for b in range(B):
+        costs[b, goals[b, 1], goals[b, 0]] = 1.0
+    T = ctx.tmap2d_batch(costs, goals)
+    for b in range(B):
+        check_field(T[b], oracle_field(costs[b], goals[b]), goals[b], False)
+
+
+def test_repeatable(ctx):
+    """Monotone min-updates: racing sweeps may differ only in the last bits between runs."""
+    rng = np.random.default_rng(9)
+    c = rng.uniform(1, 10, (700, 900)).astype(np.float32)
+    a = ctx.tmap2d(c, [450, 350], dtype=np.float32)
+    b = ctx.tmap2d(c, [450, 350], dtype=np.float32)
+    fin = np.isfinite(a)
+    assert np.array_equal(fin, np.isfinite(b))
+    assert (np.abs(a[fin] - b[fin]) / np.maximum(a[fin], 1e-30)).max() <= 1e-5
+
+
+def test_stats_count_visits(ctx):
+    c = np.ones((512, 512), np.float32)
+    ctx.tmap2d(c, [256, 256], dtype=np.float32)
+    s = ctx.stats()
+    assert s["tile_visits"] >= 64 and s["iterations"] >= 8 and s["solve_ms"] > 0
