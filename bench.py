@@ -1,0 +1,231 @@
+"""Benchmark: Eikonal cost-to-go on MI355X (BASELINE.json metric), one JSON line on rank 0.
+
+  python bench.py [--gpus N --steps K --warmup W]                   # N = 1 here
+  torchrun --nproc-per-node N bench.py --gpus N ...                 # driver, N > 1
+
+Workload (BASELINE.json configs): N = 1 -> config[1], a 4096 x 4096 DEM-derived cost raster
+(terrain.py: fractal DEM seed 42 + the planner's cost recipe), single goal at the centre, fp32
+block-FIM.  N > 1 -> weak scaling: every rank owns a 4096 x 4096 block of ONE global raster
+(px x py = 2x1, 2x2, 4x2 -> 8192 x 4096, 8192^2, 16384 x 8192), single goal at the global
+centre, halo exchange over RCCL (eikonal/dd.py).  A "step" = one full solve of the whole raster
+(T init -> converged), inputs resident in HBM.  value = cells of the global raster x steps /
+max-over-ranks wall time (Gcells/s).
+
+Also reported: roofline of the dominant kernel (fim2d_sweep_kernel: per-launch hipEvents on the
+solver stream over the timed region, algorithmic bytes = tile visits x 50176 B), ms-to-path
+(host cost -> host path, N = 1), and the CPU baseline (oracle C heap FMM, 1 thread, N = 1).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "planning-motion_planning_amd"))
+
+import eikonal  # noqa: E402
+from eikonal import dd, terrain  # noqa: E402
+from eikonal import _lib as L  # noqa: E402
+
+METRIC = "Eikonal Gcells/s + ms-to-path, 4k² & 16k² costmap at 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+BYTES_PER_VISIT = 4 * (3 * 64 * 64 + 4 * 64)  # fp32: cost read + T read + T write + halo read
+
+
+def env_int(k, d):
+    return int(os.environ.get(k, d))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--block", type=int, default=4096, help="per-rank block side (cells)")
+    ap.add_argument("--exchange-every", type=int, default=8)
+    ap.add_argument("--sync-every", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-path", action="store_true")
+    ap.add_argument("--no-timing", action="store_true", help="skip per-launch events (roofline)")
+    ap.add_argument("--pmc-traffic", type=str, default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    args = ap.parse_args()
+
+    world = env_int("WORLD_SIZE", 1)
+    rank = env_int("RANK", 0)
+    local_rank = env_int("LOCAL_RANK", 0)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    px, py = dd.SPLITS[world]
+    H, W = args.block * py, args.block * px
+    blk = dd.Block(H, W, px, py, rank)
+    goal_g = (W // 2, H // 2)
+
+    cost = terrain.cost_block(blk.y0, blk.x0, blk.h, blk.w, H, W, seed=42, device=dev).contiguous()
+    T = torch.empty_like(cost)
+    stream = torch.cuda.current_stream(dev)
+    ctx = eikonal.Context(local_rank)
+    ctx.set_option(L.OPT_SYNC_EVERY, args.sync_every)
+    fim = eikonal.Fim2d(ctx, 1, blk.h, blk.w, L.EIK_F32)
+    lgoal = blk.local_goal(*goal_g)
+
+    if world > 1:
+        send, recv, ghost = dd.make_strips(blk, torch.float32, dev, float("inf"))
+        local = dd.GpuLocal(fim, ghost)
+
+        def step():
+            local.start(cost, T, lgoal, stream.cuda_stream)
+            dd.solve(local, blk, send, recv, exchange_every=args.exchange_every)
+    else:
+        def step():
+            fim.solve(cost.data_ptr(), T.data_ptr(), [lgoal], stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    if not args.no_timing:
+        ctx.set_option(L.OPT_TIMING, 1)
+    visits = 0
+    sweep_ms = 0.0
+    iters = 0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        s = fim.stats()
+        visits += s["tile_visits"]
+        sweep_ms += s["sweep_ms"]
+        iters += s["iterations"]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    ctx.set_option(L.OPT_TIMING, 0)
+    el = t1 - t0
+    if world > 1:
+        tt = torch.tensor([el], device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = tt.item()
+        agg = torch.tensor([visits, iters], dtype=torch.float64, device=dev)
+        dist.all_reduce(agg)
+        visits_all, iters_all = agg.tolist()
+    else:
+        visits_all, iters_all = visits, iters
+
+    value = H * W * args.steps / el / 1e9
+    ms_per_step = el / args.steps * 1e3
+
+    # roofline of the dominant kernel (rank-local: this rank's launches and its event time)
+    launches = iters
+    achieved = (visits * BYTES_PER_VISIT / (sweep_ms * 1e-3) / 1e9) if sweep_ms > 0 else None
+    traffic = None
+    if os.path.exists(args.pmc_traffic):
+        try:
+            traffic = json.load(open(args.pmc_traffic)).get("bytes_per_launch")
+        except Exception:
+            traffic = None
+    roof = {
+        "bound": "hbm",
+        "kernel": "fim2d_sweep_kernel<float>",
+        "achieved": round(achieved, 2) if achieved else None,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+        "traffic": traffic,
+        "alg_bytes_per_launch": round(visits * BYTES_PER_VISIT / max(launches, 1)),
+        "avg_launch_us": round(sweep_ms * 1e3 / max(launches, 1), 2),
+        "launches_per_solve": round(launches / args.steps, 1),
+        "tile_visits_per_solve": round(visits / args.steps, 1),
+    }
+
+    out = {
+        "metric": METRIC,
+        "value": round(value, 4),
+        "unit": "Gcells/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (fractal DEM seed 42 -> planner cost recipe, eikonal/terrain.py)",
+        "config": {
+            "workload": ("C2: 4096x4096 DEM-derived cost raster, single goal, FIM on 1 MI355X" if world == 1 else
+                         f"C4-weak: {H}x{W} DEM-derived raster, {px}x{py} blocks of {args.block}^2 with RCCL halo"),
+            "H": H, "W": W, "split": f"{px}x{py}", "goal": list(goal_g), "tile": 64,
+            "parallelism": "single-gpu" if world == 1 else f"domain-decomposition {px}x{py}",
+        },
+        "roofline": roof,
+    }
+
+    if rank == 0 and world == 1 and not args.no_path:
+        out.update(ms_to_path(cost, ctx, fim, dev, stream, goal_g))
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(cost, goal_g)
+
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def ms_to_path(cost, ctx, fim, dev, stream, goal, start=(256, 256), reps=3):
+    """host cost (pageable numpy) -> H2D -> solve -> path kernel -> D2H path."""
+    host_cost = cost.cpu().numpy()
+    cap = 30004
+    out_d = torch.empty((cap, 2), dtype=torch.float64, device=dev)
+    n_d = torch.zeros(1, dtype=torch.int64, device=dev)
+    st_d = torch.zeros(1, dtype=torch.int32, device=dev)
+    H, W = host_cost.shape
+    tot, devs, lens = [], [], []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        c = torch.from_numpy(host_cost).to(dev)
+        T = torch.empty_like(c)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        fim.solve(c.data_ptr(), T.data_ptr(), [goal], stream.cuda_stream)
+        ctx._chk(L.lib().eik_path2d_dev(ctx._h, T.data_ptr(), L.EIK_F32, H, W, np.array(start, np.float64),
+                                        np.array(goal, np.float64), 0.5, out_d.data_ptr(), cap, n_d.data_ptr(),
+                                        st_d.data_ptr(), stream.cuda_stream))
+        e1.record(stream)
+        n = int(n_d.item())
+        path = out_d[:n].cpu().numpy()
+        t1 = time.perf_counter()
+        tot.append((t1 - t0) * 1e3)
+        devs.append(e0.elapsed_time(e1))
+        lens.append(n)
+    return {"ms_to_path": round(float(np.median(tot)), 3), "ms_to_path_device": round(float(np.median(devs)), 3),
+            "path_points": int(lens[0]), "path_status": int(st_d.item()), "path_from": list(start)}
+
+
+def cpu_baseline(cost, goal):
+    """Oracle C heap FMM (bit-exact restatement of the reference), 1 host thread."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    c = cost.double().cpu().numpy()
+    O.set_strict(False)
+    t0 = time.perf_counter()
+    O.fmm2d(c, goal)
+    el = time.perf_counter() - t0
+    O.set_strict(True)
+    return {"value": round(c.size / el / 1e9, 6), "unit": "Gcells/s", "cores": 1, "kind": "port",
+            "sample": f"one full-field solve of the same {c.shape[0]}x{c.shape[1]} raster in fp64 "
+                      f"({el:.2f} s, oracle/eikonal_oracle.c heap FMM)",
+            "seconds": round(el, 3)}
+
+
+if __name__ == "__main__":
+    main()

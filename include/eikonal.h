@@ -132,7 +132,8 @@ int eik_fim2d_pack_edges(eik_fim2d* fim, void* north, void* south, void* west, v
 int eik_fim2d_merge_ghost(eik_fim2d* fim, int side, const void* recv);
 /* number of tiles active for the next iteration (synchronises the stream) */
 int eik_fim2d_active(eik_fim2d* fim, int64_t* active);
-int eik_fim2d_stats(const eik_fim2d* fim, eik_stats* out);
+/* statistics of the current/last solve (synchronises the stream to read the visit counter) */
+int eik_fim2d_stats(eik_fim2d* fim, eik_stats* out);
 
 /* getPathGDM on a device-resident field; out/n_out/status are device pointers. */
 int eik_path2d_dev(eik_ctx* ctx, const void* d_T, int dtype, int64_t H, int64_t W, const double init[2],

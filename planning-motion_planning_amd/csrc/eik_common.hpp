@@ -40,7 +40,11 @@ __device__ __forceinline__ float godunov2<float>(float a, float b, float c) {
     const float lo = fminf(a, b), hi = fmaxf(a, b);
     const float d = hi - lo;
     const float t1 = lo + c;
+#ifdef EIK_IEEE_SQRT
     const float t2 = 0.5f * (lo + hi + __builtin_sqrtf(2.f * (c * c) - d * d));
+#else
+    const float t2 = 0.5f * (lo + hi + __builtin_amdgcn_sqrtf(2.f * (c * c) - d * d));  // v_sqrt_f32, <= 1 ulp
+#endif
     return (hi == Real<float>::inf() || c < d) ? t1 : t2;
 }
 

@@ -344,8 +344,14 @@ int eik_fim2d_merge_ghost(eik_fim2d* f, int side, const void* recv) {
     return EIK_OK;
 }
 
-int eik_fim2d_stats(const eik_fim2d* f, eik_stats* out) {
+int eik_fim2d_stats(eik_fim2d* f, eik_stats* out) {
     if (!f || !out) return EIK_ERR_ARG;
+    if (f->started) {
+        eik_ctx* c = f->ctx;
+        HIPCHK(c, hipMemcpyAsync(f->h_visits, f->visits.p, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                 f->stream));
+        HIPCHK(c, hipStreamSynchronize(f->stream));
+    }
     out->iterations = f->iterations;
     out->tile_visits = (int64_t)*f->h_visits;
     out->host_syncs = f->host_syncs;

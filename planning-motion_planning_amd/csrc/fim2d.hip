@@ -44,6 +44,8 @@ __device__ __forceinline__ void enqueue(const Fim2dArgs& a, int tile, int list, 
 }
 
 // One quadrant sweep of the staged tile.  DX/DY = +-1: direction of propagation.
+// Branch-free: lanes outside the tile (skew prologue/epilogue) compute on clamped addresses and
+// merge +inf (a no-op ds_min).
 template <typename R, int DX, int DY>
 __device__ __forceinline__ bool sweep_quadrant(R* __restrict__ Ts, const R* __restrict__ Cs, int lane) {
     constexpr R INF = Real<R>::inf();
@@ -52,45 +54,38 @@ __device__ __forceinline__ bool sweep_quadrant(R* __restrict__ Ts, const R* __re
     bool changed = false;
     R cur = INF;
 
-    // values one step ahead (prefetched before the previous step's LDS atomic is issued)
     R p_old, p_dnx, p_dny, p_upx, p_c;
-    auto fetch = [&](int s, R& o, R& dx, R& dy, R& ux, R& c) {
-        const int r = s - lane;
-        const int rc = r < -1 ? -1 : (r > kTile - 1 ? kTile - 1 : r);
-        const int y = DY > 0 ? rc : kTile - 1 - rc;  // -1..64 (halo rows at r == -1)
-        const int lr = y + 1;
-        int lry = lr + DY;
-        lry = lry < 0 ? 0 : (lry > kLds - 1 ? kLds - 1 : lry);
-        const int yc = y < 0 ? 0 : (y > kTile - 1 ? kTile - 1 : y);
-        o = Ts[lr * kLds + col];
-        dx = Ts[lr * kLds + col + DX];
-        dy = Ts[lry * kLds + col];
-        ux = Ts[lr * kLds + col - DX];  // used by lane 0 only (halo column)
+    int p_o;
+    auto fetch = [&](int s, int& o, R& old, R& dx, R& dy, R& ux, R& c) {
+        int r = s - lane;
+        r = r < -1 ? -1 : (r > kTile - 1 ? kTile - 1 : r);
+        const int lr = DY > 0 ? r + 1 : kTile - r;  // LDS row: 0..65 (halo rows at r == -1)
+        o = lr * kLds + col;
+        old = Ts[o];
+        dx = Ts[o + DX];
+        dy = Ts[o + DY * kLds];
+        ux = Ts[o - DX];  // halo column, used by lane 0 only
+        // clamp: an out-of-array index would be UB, and the compiler then assumes r >= 0 and
+        // drops the +inf masking of the halo-row step
+        const int yc = lr < 1 ? 0 : (lr > kTile ? kTile - 1 : lr - 1);
         c = Cs[yc * kTile + x];
     };
-    fetch(-1, p_old, p_dnx, p_dny, p_upx, p_c);
+    fetch(-1, p_o, p_old, p_dnx, p_dny, p_upx, p_c);
 #pragma unroll 2
     for (int s = -1; s < 2 * kTile - 1; ++s) {
         const R old = p_old, dnx = p_dnx, dny = p_dny, uxh = p_upx, c = p_c;
-        fetch(s + 1, p_old, p_dnx, p_dny, p_upx, p_c);
+        const int o = p_o;
+        fetch(s + 1, p_o, p_old, p_dnx, p_dny, p_upx, p_c);  // issued before this step's ds_min
         const int r = s - lane;
         R upx = wave_shr1(cur);
-        if (lane == 0) upx = uxh;
+        upx = lane == 0 ? uxh : upx;
         const R a = upx < dnx ? upx : dnx;
         const R b = cur < dny ? cur : dny;
         const R nv = godunov2<R>(a, b, c);
-        if (r >= 0 && r < kTile) {
-            if (nv < old) {
-                const int y = DY > 0 ? r : kTile - 1 - r;
-                lds_min(&Ts[(y + 1) * kLds + col], nv);
-                cur = nv;
-                changed = true;
-            } else {
-                cur = old;
-            }
-        } else if (r == -1) {
-            cur = old;  // upstream halo row
-        }
+        const R w = (unsigned)r < (unsigned)kTile ? nv : INF;
+        lds_min(&Ts[o], w);
+        changed |= w < old;
+        cur = w < old ? w : old;  // r == -1: the upstream halo row value
     }
     return changed;
 }
@@ -199,12 +194,23 @@ __global__ __launch_bounds__(kThreads) void fim2d_sweep_kernel(Fim2dArgs a) {
                 const bool chg = nv[e] < told[4 * k + e];
                 any |= chg;
                 if (chg) {
-                    const int64_t gx = x0 + cx + e;
-                    if (ry == 0 || gy == 0) fl |= 1u;                          // north edge
-                    if (ry == kTile - 1 || gy == a.H - 1) fl |= 2u;            // south edge
-                    if (cx + e == 0 || gx == 0) fl |= 4u;                      // west edge
-                    if (cx + e == kTile - 1 || gx == a.W - 1) fl |= 8u;        // east edge
-                    fl |= 16u;
+                    // A neighbour can only improve if this edge value undercuts the neighbour's
+                    // adjacent cell (the halo value, stale => larger => conservative).
+                    const int lx = cx + e + 1, ly = ry + 1;
+#ifdef EIK_NO_FILTER
+                    if (ry == 0) fl |= 1u;
+                    if (ry == kTile - 1) fl |= 2u;
+                    if (cx + e == 0) fl |= 4u;
+                    if (cx + e == kTile - 1) fl |= 8u;
+#else
+                    if (ry == 0 && nv[e] < Ts[lx]) fl |= 1u;                                   // north
+                    if (ry == kTile - 1 && nv[e] < Ts[(kLds - 1) * kLds + lx]) fl |= 2u;     // south
+                    if (cx + e == 0 && nv[e] < Ts[ly * kLds]) fl |= 4u;                       // west
+                    if (cx + e == kTile - 1 && nv[e] < Ts[ly * kLds + kLds - 1]) fl |= 8u;    // east
+#endif
+                    const int64_t gx = x0 + cx + e;                     // subdomain edges (DD)
+                    if (gy == a.H - 1 && ry != kTile - 1) fl |= 32u;
+                    if (gx == a.W - 1 && cx + e != kTile - 1) fl |= 64u;
                 }
             }
             if (any) {
@@ -237,9 +243,9 @@ __global__ __launch_bounds__(kThreads) void fim2d_sweep_kernel(Fim2dArgs a) {
             if (a.edge_dirty) {  // subdomain edges (domain decomposition)
                 unsigned e = 0;
                 if ((f & 1u) && ty == 0) e |= 1u;
-                if ((f & 2u) && ty + 1 == a.nty) e |= 2u;
+                if (((f & 2u) || (f & 32u)) && ty + 1 == a.nty) e |= 2u;
                 if ((f & 4u) && tx == 0) e |= 4u;
-                if ((f & 8u) && tx + 1 == a.ntx) e |= 8u;
+                if (((f & 8u) || (f & 64u)) && tx + 1 == a.ntx) e |= 8u;
                 if (e) atomicOr(a.edge_dirty, e);
             }
             if (a.visits) atomicAdd(a.visits, 1ull);
