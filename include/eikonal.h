@@ -18,7 +18,8 @@
  * One context per host thread; a context owns its device buffers and HIP stream.
  * Host-buffer entry points (eik_tmap*, eik_path*, eik_gradient*) are synchronous.
  * Device entry points (eik_fim2d_*, eik_path2d_dev) take device pointers and a hipStream_t
- * (passed as void*; NULL = the context's stream) and are asynchronous unless noted.
+ * (passed as void*, used as given: NULL is the default null stream, as in HIP) and are
+ * asynchronous unless noted.
  */
 #ifndef EIKONAL_H_
 #define EIKONAL_H_
@@ -104,6 +105,19 @@ int eik_path2d_f64(eik_ctx* ctx, const double* T, int64_t H, int64_t W, const do
 /* computeGradient(T) FastMarching.py:242-300 (point = [] -> whole field): Gnx, Gny. */
 int eik_gradient2d_f64(eik_ctx* ctx, const double* T, int64_t H, int64_t W, double* gnx, double* gny);
 
+/* ---- host-buffer drop-ins of FastMarching3D.py ----------------------------------------- */
+
+/* FastMarching3D.computeTmap(costMap, goal, start) :126-145 -> full field T (the reference
+ * stops once `start` is popped; every value it closes is identical here).  cost, T: H*W*L
+ * row-major [y][x][z]; goal = (x, y, z). */
+int eik_tmap3d_f32(eik_ctx* ctx, const float* cost, int64_t H, int64_t W, int64_t L, const int64_t goal[3], float* T);
+int eik_tmap3d_f64(eik_ctx* ctx, const double* cost, int64_t H, int64_t W, int64_t L, const int64_t goal[3],
+                   double* T);
+
+/* FastMarching3D.getPathGDM(T, init, end, tau) :198-271 on an fp64 field: out cap x 3 rows. */
+int eik_path3d_f64(eik_ctx* ctx, const double* T, int64_t H, int64_t W, int64_t L, const double init[3],
+                   const double end[3], double tau, double* out, int64_t cap, int64_t* n_out, int* status);
+
 /* ---- device-resident solver (bench, multi-GPU domain decomposition, C++ hosts) ---------- */
 
 /* A solver for B maps of H x W in `dtype`; owns the active lists, marks and counters. */
@@ -138,6 +152,16 @@ int eik_fim2d_stats(eik_fim2d* fim, eik_stats* out);
 /* getPathGDM on a device-resident field; out/n_out/status are device pointers. */
 int eik_path2d_dev(eik_ctx* ctx, const void* d_T, int dtype, int64_t H, int64_t W, const double init[2],
                    const double end[2], double tau, double* d_out, int64_t cap, int64_t* d_n_out, int* d_status,
+                   void* stream);
+
+/* 3D solve on device buffers (synchronous: returns after convergence; stats via
+ * eik_get_stats). */
+int eik_fim3d_solve(eik_ctx* ctx, const void* d_cost, void* d_T, int64_t H, int64_t W, int64_t L, int dtype,
+                    const int64_t goal[3], void* stream);
+
+/* FastMarching3D.getPathGDM on a device-resident field. */
+int eik_path3d_dev(eik_ctx* ctx, const void* d_T, int dtype, int64_t H, int64_t W, int64_t L, const double init[3],
+                   const double end[3], double tau, double* d_out, int64_t cap, int64_t* d_n_out, int* d_status,
                    void* stream);
 
 #ifdef __cplusplus

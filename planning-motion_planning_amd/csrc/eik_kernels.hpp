@@ -27,6 +27,25 @@ hipError_t fim2d_sweep(const Fim2dArgs& a, bool f64, int grid, hipStream_t st);
 hipError_t fim2d_merge_ghost(const Fim2dArgs& a, bool f64, int side, const void* recv, int64_t len, hipStream_t st);
 hipError_t fim2d_pack_edges(const Fim2dArgs& a, bool f64, void* n, void* s, void* w, void* e, hipStream_t st);
 
+// 3D FIM over one H x W x L volume ([y][x][z], FastMarching3D.py layout).
+struct Fim3dArgs {
+    const void* cost;
+    void* T;
+    int64_t H, W, L;
+    int tx, ty, tz;        // tile shape
+    int ntx, nty, ntz;
+    int* lists;
+    int* counts;
+    unsigned* mark;
+    int capacity;
+    unsigned iter;
+    int max_passes;        // relaxation passes per tile visit
+    unsigned long long* visits;
+};
+hipError_t fim3d_init(const Fim3dArgs& a, bool f64, int64_t gx, int64_t gy, int64_t gz, hipStream_t st);
+hipError_t fim3d_sweep(const Fim3dArgs& a, bool f64, int grid, hipStream_t st);
+void fim3d_tile_shape(int64_t L, int* tx, int* ty, int* tz);
+
 // Gradient-descent path extraction (getPathGDM, FastMarching.py:164-236), one wave.
 struct Gdm2dArgs {
     const void* T;         // [H][W] field (R), device
@@ -39,6 +58,20 @@ struct Gdm2dArgs {
     int* status;           // device
 };
 hipError_t gdm2d(const Gdm2dArgs& a, bool f64, hipStream_t st);
+
+// FastMarching3D.getPathGDM (:198-271): np.gradient field, trilinear (a7 as in :290), integer
+// 6-neighbour fallback, unnormalised step.
+struct Gdm3dArgs {
+    const void* T;         // [H][W][L] field (R), device
+    int64_t H, W, L;
+    double init[3], end[3], tau;
+    long steps;
+    double* out;           // [cap][3]
+    int64_t cap;
+    int64_t* n_out;
+    int* status;
+};
+hipError_t gdm3d(const Gdm3dArgs& a, bool f64, hipStream_t st);
 
 // Full-field inf-aware normalised gradient (computeGradient(T, point=[]), FastMarching.py:242-300)
 hipError_t gradient2d(const double* T, int64_t H, int64_t W, double* gnx, double* gny, hipStream_t st);

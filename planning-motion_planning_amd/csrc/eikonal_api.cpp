@@ -60,6 +60,8 @@ struct eik_ctx {
     eik_stats last{};
     eik_fim2d* cached = nullptr;  // solver reused by the host-buffer entry points
     DevBuf cost, T, T2, goals, work, misc;
+    DevBuf l3, c3, m3, v3;             // 3D solver scratch (lists, counts, marks, visits)
+    int max_passes3 = 24;
 };
 
 struct eik_fim2d {
@@ -230,7 +232,7 @@ int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
     if (!f || !d_cost || !d_T || !goals) return EIK_ERR_ARG;
     eik_ctx* c = f->ctx;
     HIPCHK(c, hipSetDevice(c->device));
-    f->stream = stream ? (hipStream_t)stream : c->stream;
+    f->stream = (hipStream_t)stream;  // as given: NULL is the default (null) stream
     f->a.cost = d_cost;
     f->a.T = d_T;
     f->a.iter = 0;
@@ -481,7 +483,7 @@ int eik_path2d_dev(eik_ctx* c, const void* d_T, int dtype, int64_t H, int64_t W,
     a.cap = cap;
     a.n_out = d_n_out;
     a.status = d_status;
-    HIPCHK(c, gdm2d(a, dtype == EIK_F64, stream ? (hipStream_t)stream : c->stream));
+    HIPCHK(c, gdm2d(a, dtype == EIK_F64, (hipStream_t)stream));
     return EIK_OK;
 }
 
@@ -505,6 +507,161 @@ int eik_path2d_f64(eik_ctx* c, const double* T, int64_t H, int64_t W, const doub
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (nn > cap) nn = cap;
     HIPCHK(c, hipMemcpy(out, d_out, sizeof(double) * 2 * nn, hipMemcpyDeviceToHost));
+    *n_out = nn;
+    *status = st;
+    return EIK_OK;
+}
+
+// ------------------------------------------------------------------------------ 3D
+int eik_fim3d_solve(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, int64_t W, int64_t L, int dtype,
+                    const int64_t goal[3], void* stream) {
+    if (!c || !d_cost || !d_T || !goal || H < 1 || W < 1 || L < 1)
+        return c ? set_err(c, EIK_ERR_ARG, "bad 3D arguments") : EIK_ERR_ARG;
+    if (goal[0] < 0 || goal[1] < 0 || goal[2] < 0 || goal[0] >= W || goal[1] >= H || goal[2] >= L)
+        return set_err(c, EIK_ERR_ARG, "goal (%ld,%ld,%ld) outside %ldx%ldx%ld", (long)goal[0], (long)goal[1],
+                       (long)goal[2], (long)H, (long)W, (long)L);
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t st = (hipStream_t)stream;
+    Fim3dArgs a{};
+    a.cost = d_cost;
+    a.T = d_T;
+    a.H = H;
+    a.W = W;
+    a.L = L;
+    fim3d_tile_shape(L, &a.tx, &a.ty, &a.tz);
+    a.ntx = (int)((W + a.tx - 1) / a.tx);
+    a.nty = (int)((H + a.ty - 1) / a.ty);
+    a.ntz = (int)((L + a.tz - 1) / a.tz);
+    const int64_t tiles = (int64_t)a.ntx * a.nty * a.ntz;
+    if (tiles >= (1ll << 31) - 8) return set_err(c, EIK_ERR_ARG, "too many 3D tiles");
+    a.capacity = (int)tiles;
+    a.max_passes = c->max_passes3;
+    HIPCHK(c, c->l3.ensure(sizeof(int) * 3 * tiles));
+    HIPCHK(c, c->c3.ensure(sizeof(int) * 64));
+    HIPCHK(c, c->m3.ensure(sizeof(unsigned) * tiles));
+    HIPCHK(c, c->v3.ensure(sizeof(unsigned long long)));
+    a.lists = (int*)c->l3.p;
+    a.counts = (int*)c->c3.p;
+    a.mark = (unsigned*)c->m3.p;
+    a.visits = (unsigned long long*)c->v3.p;
+    hipEvent_t e0, e1;
+    HIPCHK(c, hipEventCreate(&e0));
+    HIPCHK(c, hipEventCreate(&e1));
+    HIPCHK(c, hipEventRecord(e0, st));
+    HIPCHK(c, hipMemsetAsync(c->v3.p, 0, sizeof(unsigned long long), st));
+    HIPCHK(c, fim3d_init(a, dtype == EIK_F64, goal[0], goal[1], goal[2], st));
+    int* h = nullptr;
+    HIPCHK(c, hipHostMalloc((void**)&h, sizeof(int) * 2 + sizeof(unsigned long long)));
+    const int grid = c->grid > 0 ? c->grid : 4 * c->cu_count;
+    const int64_t max_iters = 64 * ((int64_t)a.ntx + a.nty + a.ntz) + 8 * tiles + 4096;
+    int64_t it = 0;
+    int rc = EIK_OK;
+    for (;;) {
+        for (int k = 0; k < c->sync_every; ++k, ++it) {
+            a.iter = (unsigned)it;
+            hipError_t e = fim3d_sweep(a, dtype == EIK_F64, grid, st);
+            if (e != hipSuccess) { rc = set_err(c, EIK_ERR_HIP, "fim3d_sweep: %s", hipGetErrorString(e)); break; }
+        }
+        if (rc) break;
+        hipError_t e = hipMemcpyAsync(h, (int*)c->c3.p + (it % 3), sizeof(int), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) { rc = set_err(c, EIK_ERR_HIP, "fim3d sync: %s", hipGetErrorString(e)); break; }
+        if (h[0] == 0) break;
+        if (it >= max_iters) { rc = set_err(c, EIK_ERR_NOCONVERGE, "3D solve did not converge"); break; }
+    }
+    if (rc == EIK_OK) {
+        unsigned long long* hv = (unsigned long long*)(h + 2);
+        (void)hipEventRecord(e1, st);
+        (void)hipMemcpyAsync(hv, c->v3.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, st);
+        (void)hipStreamSynchronize(st);
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        c->last = eik_stats{};
+        c->last.iterations = it;
+        c->last.tile_visits = (int64_t)*hv;
+        c->last.solve_ms = ms;
+        c->last.bytes_alg = (double)*hv * (dtype == EIK_F64 ? 8 : 4) * 3.0 * a.tx * a.ty * a.tz;
+    }
+    (void)hipHostFree(h);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return rc;
+}
+
+}  // extern "C"
+
+template <typename R>
+static int tmap3d_host(eik_ctx* c, const R* cost, int64_t H, int64_t W, int64_t L, const int64_t goal[3], R* T) {
+    if (!c || !cost || !T || !goal) return c ? set_err(c, EIK_ERR_ARG, "NULL argument") : EIK_ERR_ARG;
+    const int64_t n = H * W * L;
+    int rc = check_cost(c, cost, n);
+    if (rc) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, c->cost.ensure(sizeof(R) * n));
+    HIPCHK(c, c->T.ensure(sizeof(R) * n));
+    HIPCHK(c, hipMemcpyAsync(c->cost.p, cost, sizeof(R) * n, hipMemcpyHostToDevice, c->stream));
+    rc = eik_fim3d_solve(c, c->cost.p, c->T.p, H, W, L, sizeof(R) == 8 ? EIK_F64 : EIK_F32, goal, c->stream);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(T, c->T.p, sizeof(R) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return EIK_OK;
+}
+
+extern "C" {
+
+int eik_tmap3d_f32(eik_ctx* c, const float* cost, int64_t H, int64_t W, int64_t L, const int64_t goal[3], float* T) {
+    return tmap3d_host<float>(c, cost, H, W, L, goal, T);
+}
+
+int eik_tmap3d_f64(eik_ctx* c, const double* cost, int64_t H, int64_t W, int64_t L, const int64_t goal[3],
+                   double* T) {
+    return tmap3d_host<double>(c, cost, H, W, L, goal, T);
+}
+
+int eik_path3d_dev(eik_ctx* c, const void* d_T, int dtype, int64_t H, int64_t W, int64_t L, const double init[3],
+                   const double end[3], double tau, double* d_out, int64_t cap, int64_t* d_n_out, int* d_status,
+                   void* stream) {
+    if (!c || !d_T || !init || !end || !d_out || !d_n_out || !d_status || cap < 2 || !(tau > 0))
+        return c ? set_err(c, EIK_ERR_ARG, "bad 3D path arguments") : EIK_ERR_ARG;
+    Gdm3dArgs a;
+    a.T = d_T;
+    a.H = H;
+    a.W = W;
+    a.L = L;
+    for (int i = 0; i < 3; ++i) {
+        a.init[i] = init[i];
+        a.end[i] = end[i];
+    }
+    a.tau = tau;
+    a.steps = (long)std::nearbyint(15000.0 / tau);  // int(round(15000/tau)), FastMarching3D.py:207
+    a.out = d_out;
+    a.cap = cap;
+    a.n_out = d_n_out;
+    a.status = d_status;
+    HIPCHK(c, gdm3d(a, dtype == EIK_F64, (hipStream_t)stream));
+    return EIK_OK;
+}
+
+int eik_path3d_f64(eik_ctx* c, const double* T, int64_t H, int64_t W, int64_t L, const double init[3],
+                   const double end[3], double tau, double* out, int64_t cap, int64_t* n_out, int* status) {
+    if (!c || !T || !out || !n_out || !status) return c ? set_err(c, EIK_ERR_ARG, "NULL argument") : EIK_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t n = H * W * L;
+    HIPCHK(c, c->T2.ensure(sizeof(double) * n));
+    HIPCHK(c, c->work.ensure(sizeof(double) * 3 * cap + 64));
+    HIPCHK(c, hipMemcpyAsync(c->T2.p, T, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    double* d_out = (double*)c->work.p;
+    int64_t* d_n = (int64_t*)(d_out + 3 * cap);
+    int* d_st = (int*)(d_n + 1);
+    int rc = eik_path3d_dev(c, c->T2.p, EIK_F64, H, W, L, init, end, tau, d_out, cap, d_n, d_st, c->stream);
+    if (rc) return rc;
+    int64_t nn = 0;
+    int st = 0;
+    HIPCHK(c, hipMemcpyAsync(&nn, d_n, sizeof nn, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&st, d_st, sizeof st, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (nn > cap) nn = cap;
+    HIPCHK(c, hipMemcpy(out, d_out, sizeof(double) * 3 * nn, hipMemcpyDeviceToHost));
     *n_out = nn;
     *status = st;
     return EIK_OK;

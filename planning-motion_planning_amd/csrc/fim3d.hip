@@ -1,0 +1,229 @@
+// fim3d.hip -- block FIM for the 3D (x, y, z) Eikonal of FastMarching3D.py on gfx950.
+//
+// Reference: FastMarching3D.py:19-145 (updateNode with the 6-neighbour "drop the largest"
+// n-D Godunov solve, :59-75; sorted-list narrow band; computeTmap driver).  Layout follows the
+// reference: cost[y][x][z] row-major (z fastest), nodes (x, y, z).
+//
+// Tiles are TX x TY x TZ boxes of <= 1024 cells chosen per volume (16x16xL for the planner's
+// thin layered volumes, 8x16x8 for cubes).  A 256-thread workgroup stages the box + a 1-cell
+// halo in LDS and relaxes it in place (every thread owns up to 4 cells; chaotic relaxation is
+// monotone, so it converges to the same fixed point) until a pass changes nothing or the pass
+// budget runs out, then writes back and activates the face neighbours whose halo its new face
+// values undercut -- the same active-list / mark machinery as fim2d.hip.
+#include "eik_common.hpp"
+#include "eik_kernels.hpp"
+
+namespace eik {
+
+// FastMarching3D.py:59-75: try all three axes, drop the largest while the n-axis solution does
+// not exceed it (C^2 > sum (Tmax - Ti)^2 is the reference's acceptance test).
+template <typename R>
+__device__ __forceinline__ R godunov3(R a, R b, R c, R C) {
+    // sort ascending
+    R t;
+    if (a > b) { t = a; a = b; b = t; }
+    if (b > c) { t = b; b = c; c = t; }
+    if (a > b) { t = a; a = b; b = t; }
+    // Solutions written relative to the smallest neighbour (b' = b - a, c' = c - a):
+    // (S + sqrt(nC^2 + S^2 - nQ)) / n of the reference equals a + (S' + sqrt(nC^2 - (nQ' - S'^2)))/n
+    // with nQ' - S'^2 = 2(b'^2 + c'^2 - b'c') for n = 3 -- no cancellation of the large T values
+    // (the reference's form loses ~1e-4 relative in fp32 at T ~ 300).
+    const R C2 = C * C;
+    const R bp = b - a, cp = c - a;
+    if (c != Real<R>::inf() && C2 > cp * cp + (c - b) * (c - b)) {
+        return a + (bp + cp + __builtin_sqrt(R(3) * C2 - R(2) * (bp * bp + cp * cp - bp * cp))) / R(3);
+    }
+    if (b != Real<R>::inf() && C2 > bp * bp) {
+        return a + (bp + __builtin_sqrt(R(2) * C2 - bp * bp)) / R(2);
+    }
+    return a + C;
+}
+
+__device__ __forceinline__ void enqueue3(const Fim3dArgs& a, int tile, int list, unsigned stamp) {
+    if (atomicMax(&a.mark[tile], stamp) < stamp) {
+        const int pos = atomicAdd(&a.counts[list], 1);
+        a.lists[(int64_t)list * a.capacity + pos] = tile;
+    }
+}
+
+template <typename R>
+__global__ __launch_bounds__(256) void fim3d_sweep_kernel(Fim3dArgs a) {
+    constexpr R INF = Real<R>::inf();
+    constexpr int kMaxCells = 1024;
+    constexpr int kMaxHalo = 18 * 18 * 10;  // (TX+2)(TY+2)(TZ+2) bound for the tile shapes used
+    __shared__ R Ts[kMaxHalo];
+    __shared__ R Cs[kMaxCells];
+    __shared__ unsigned s_flags;
+    __shared__ int s_changed[2];  // double-buffered by pass parity (no reset/read race)
+
+    const int tid = threadIdx.x;
+    const int cur = a.iter % 3, nxt = (a.iter + 1) % 3, rst = (a.iter + 2) % 3;
+    const int cnt = a.counts[cur];
+    if (blockIdx.x == 0 && tid == 0) a.counts[rst] = 0;
+    const unsigned stamp = a.iter + 2;
+    const int TX = a.tx, TY = a.ty, TZ = a.tz;
+    const int HX = TX + 2, HY = TY + 2, HZ = TZ + 2;  // halo box, index ((y*HX)+x)*HZ+z
+    const int ncell = TX * TY * TZ;
+
+    for (int it = blockIdx.x; it < cnt; it += gridDim.x) {
+        const int tile = a.lists[(int64_t)cur * a.capacity + it];
+        const int bz = tile % a.ntz, bxy = tile / a.ntz, bx = bxy % a.ntx, by = bxy / a.ntx;
+        const int64_t x0 = (int64_t)bx * TX, y0 = (int64_t)by * TY, z0 = (int64_t)bz * TZ;
+        const R* __restrict__ cost = static_cast<const R*>(a.cost);
+        R* __restrict__ T = static_cast<R*>(a.T);
+        if (tid == 0) {
+            s_flags = 0;
+            s_changed[0] = 0;
+            s_changed[1] = 0;
+        }
+        // stage the halo box (cells outside the volume read +inf)
+        const int nh = HX * HY * HZ;
+        for (int i = tid; i < nh; i += 256) {
+            const int hz = i % HZ, hxy = i / HZ, hx = hxy % HX, hy = hxy / HX;
+            const int64_t gz = z0 + hz - 1, gx = x0 + hx - 1, gy = y0 + hy - 1;
+            const bool in = gz >= 0 && gz < a.L && gx >= 0 && gx < a.W && gy >= 0 && gy < a.H;
+            Ts[i] = in ? T[(gy * a.W + gx) * a.L + gz] : INF;
+        }
+        R told[4], cst[4];
+        int hidx[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int c = tid + 256 * k;
+            hidx[k] = -1;
+            cst[k] = INF;
+            if (c < ncell) {
+                const int cz = c % TZ, cxy = c / TZ, cx = cxy % TX, cy = cxy / TX;
+                hidx[k] = ((cy + 1) * HX + (cx + 1)) * HZ + (cz + 1);
+                const int64_t gz = z0 + cz, gx = x0 + cx, gy = y0 + cy;
+                const bool in = gz < a.L && gx < a.W && gy < a.H;
+                cst[k] = in ? cost[(gy * a.W + gx) * a.L + gz] : INF;
+                Cs[c] = cst[k];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 4; ++k) told[k] = hidx[k] >= 0 ? Ts[hidx[k]] : INF;
+
+        // in-place relaxation passes
+        bool last = false;
+        const int sx = HZ, sy = HX * HZ;
+        for (int pass = 0; pass < a.max_passes; ++pass) {
+            const int slot = pass & 1;
+            bool ch = false;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (hidx[k] < 0) continue;
+                const int h = hidx[k];
+                const R v = Ts[h];
+                const R tx_ = fmin(Ts[h - sx], Ts[h + sx]);
+                const R ty_ = fmin(Ts[h - sy], Ts[h + sy]);
+                const R tz_ = fmin(Ts[h - 1], Ts[h + 1]);
+                const R nv = cst[k] == INF ? INF : godunov3<R>(tx_, ty_, tz_, cst[k]);
+                if (nv < v) {
+                    Ts[h] = nv;  // owner-only write; concurrent readers see old or new (both bounds)
+                    ch = true;
+                }
+            }
+            if (ch) s_changed[slot] = 1;
+            if (tid == 0) s_changed[slot ^ 1] = 0;  // next pass's flag: last read two passes ago
+            __syncthreads();
+            last = s_changed[slot] != 0;
+            if (!last) break;
+        }
+
+        // write back and collect face flags (bit f: face f's neighbour can improve)
+        unsigned fl = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (hidx[k] < 0) continue;
+            const int h = hidx[k];
+            const R nv = Ts[h];
+            if (!(nv < told[k])) continue;
+            const int c = tid + 256 * k;
+            const int cz = c % TZ, cxy = c / TZ, cx = cxy % TX, cy = cxy / TX;
+            const int64_t gz = z0 + cz, gx = x0 + cx, gy = y0 + cy;
+            if (gz < a.L && gx < a.W && gy < a.H) T[(gy * a.W + gx) * a.L + gz] = nv;
+            if (cx == 0 && nv < Ts[h - sx]) fl |= 1u;
+            if (cx == TX - 1 && nv < Ts[h + sx]) fl |= 2u;
+            if (cy == 0 && nv < Ts[h - sy]) fl |= 4u;
+            if (cy == TY - 1 && nv < Ts[h + sy]) fl |= 8u;
+            if (cz == 0 && nv < Ts[h - 1]) fl |= 16u;
+            if (cz == TZ - 1 && nv < Ts[h + 1]) fl |= 32u;
+        }
+        if (fl) atomicOr(&s_flags, fl);
+        __syncthreads();
+        if (tid == 0) {
+            const unsigned f = s_flags;
+            const int base = bxy * a.ntz;
+            if (last) enqueue3(a, tile, nxt, stamp);
+            if ((f & 1u) && bx > 0) enqueue3(a, tile - a.ntz, nxt, stamp);
+            if ((f & 2u) && bx + 1 < a.ntx) enqueue3(a, tile + a.ntz, nxt, stamp);
+            if ((f & 4u) && by > 0) enqueue3(a, tile - a.ntx * a.ntz, nxt, stamp);
+            if ((f & 8u) && by + 1 < a.nty) enqueue3(a, tile + a.ntx * a.ntz, nxt, stamp);
+            if ((f & 16u) && bz > 0) enqueue3(a, base + bz - 1, nxt, stamp);
+            if ((f & 32u) && bz + 1 < a.ntz) enqueue3(a, base + bz + 1, nxt, stamp);
+            if (a.visits) atomicAdd(a.visits, 1ull);
+        }
+        __syncthreads();
+    }
+}
+
+template <typename R>
+__global__ void fim3d_init_kernel(R* __restrict__ T, int64_t n, unsigned* __restrict__ mark, int64_t ntiles) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) T[i] = Real<R>::inf();
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ntiles; i += stride) mark[i] = 0;
+}
+
+template <typename R>
+__global__ void fim3d_seed_kernel(Fim3dArgs a, int64_t gx, int64_t gy, int64_t gz) {
+    a.counts[1] = 0;
+    a.counts[2] = 0;
+    static_cast<R*>(a.T)[(gy * a.W + gx) * a.L + gz] = R(0);
+    const int tile = ((int)(gy / a.ty) * a.ntx + (int)(gx / a.tx)) * a.ntz + (int)(gz / a.tz);
+    a.mark[tile] = 1;
+    a.lists[0] = tile;
+    a.counts[0] = 1;
+}
+
+hipError_t fim3d_init(const Fim3dArgs& a, bool f64, int64_t gx, int64_t gy, int64_t gz, hipStream_t st) {
+    const int64_t n = a.H * a.W * a.L;
+    const int grid = (int)std::min<int64_t>(4096, (n + 255) / 256);
+    if (f64) {
+        hipLaunchKernelGGL(fim3d_init_kernel<double>, dim3(grid), dim3(256), 0, st, static_cast<double*>(a.T), n,
+                           a.mark, (int64_t)a.capacity);
+        hipLaunchKernelGGL(fim3d_seed_kernel<double>, dim3(1), dim3(1), 0, st, a, gx, gy, gz);
+    } else {
+        hipLaunchKernelGGL(fim3d_init_kernel<float>, dim3(grid), dim3(256), 0, st, static_cast<float*>(a.T), n,
+                           a.mark, (int64_t)a.capacity);
+        hipLaunchKernelGGL(fim3d_seed_kernel<float>, dim3(1), dim3(1), 0, st, a, gx, gy, gz);
+    }
+    return hipGetLastError();
+}
+
+hipError_t fim3d_sweep(const Fim3dArgs& a, bool f64, int grid, hipStream_t st) {
+    if (f64)
+        hipLaunchKernelGGL(fim3d_sweep_kernel<double>, dim3(grid), dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL(fim3d_sweep_kernel<float>, dim3(grid), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+// tile shape for a volume with L layers: <= 1024 cells, halo box <= 18 x 18 x 10
+void fim3d_tile_shape(int64_t L, int* tx, int* ty, int* tz) {
+    if (L <= 4) {
+        *tz = (int)L;
+        *tx = 16;
+        *ty = 16;
+    } else if (L <= 8) {
+        *tz = (int)L;
+        *tx = 16;
+        *ty = 8;
+    } else {
+        *tz = 8;
+        *tx = 16;
+        *ty = 8;
+    }
+}
+
+}  // namespace eik

@@ -149,6 +149,141 @@ hipError_t gdm2d(const Gdm2dArgs& a, bool f64, hipStream_t st) {
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- 3D path (FM3D)
+// np.gradient(T) along `axis` (0 y, 1 x, 2 z) at (j, i, k): central differences / 2 inside,
+// one-sided at the ends (numpy's edge_order=1), no inf awareness (FastMarching3D.py:200).
+template <typename R>
+__device__ __forceinline__ double npgrad(const R* __restrict__ T, int64_t H, int64_t W, int64_t L, int axis,
+                                         int64_t j, int64_t i, int64_t k) {
+    const int64_t len = axis == 0 ? H : axis == 1 ? W : L;
+    const int64_t p = axis == 0 ? j : axis == 1 ? i : k;
+    const int64_t st = axis == 0 ? W * L : axis == 1 ? L : 1;
+    const R* c = T + (j * W + i) * L + k;
+    if (p == 0) return ((double)c[st] - (double)c[0]) / 1.0;
+    if (p == len - 1) return ((double)c[0] - (double)c[-st]) / 1.0;
+    return ((double)c[st] - (double)c[-st]) / 2.0;
+}
+
+// FastMarching3D.interpolatePoint :275-314, interior branch (a7 coefficient as written, :290)
+template <typename R>
+__device__ double interp3(const R* __restrict__ T, int64_t H, int64_t W, int64_t L, int axis, double px, double py,
+                          double pz, bool& oob) {
+    const uint32_t i = (uint32_t)__builtin_trunc(px), j = (uint32_t)__builtin_trunc(py), k = (uint32_t)__builtin_trunc(pz);
+    oob = i + 1 >= (uint64_t)W || j + 1 >= (uint64_t)H || k + 1 >= (uint64_t)L;
+    if (oob) return 0.0;
+    const double a = px - i, b = py - j, c = pz - k;
+    const double m000 = npgrad(T, H, W, L, axis, j, i, k), m010 = npgrad(T, H, W, L, axis, j, i + 1, k);
+    const double m100 = npgrad(T, H, W, L, axis, j + 1, i, k), m001 = npgrad(T, H, W, L, axis, j, i, k + 1);
+    const double m110 = npgrad(T, H, W, L, axis, j + 1, i + 1, k), m011 = npgrad(T, H, W, L, axis, j, i + 1, k + 1);
+    const double m101 = npgrad(T, H, W, L, axis, j + 1, i, k + 1), m111 = npgrad(T, H, W, L, axis, j + 1, i + 1, k + 1);
+    const double a0 = m000;
+    const double a1 = m010 - m000;
+    const double a2 = m100 - m000;
+    const double a3 = m001 - m000;
+    const double a4 = m110 + m000 - m010 - m100;
+    const double a5 = m011 + m000 - m010 - m001;
+    const double a6 = m101 + m000 - m100 - m001;
+    const double a7 = m111 + m000 - m100 - m001 - m010;
+    return a0 + a1 * a + a2 * b + a3 * c + a4 * a * b + a5 * a * c + a6 * b * c + a7 * a * b * c;
+}
+
+__device__ __forceinline__ double norm3(double a, double b, double c) { return __builtin_sqrt(a * a + b * b + c * c); }
+
+template <typename R>
+__global__ __launch_bounds__(64) void gdm3d_kernel(Gdm3dArgs a) {
+    if (threadIdx.x != 0) return;
+    const R* __restrict__ T = static_cast<const R*>(a.T);
+    const int64_t H = a.H, W = a.W, L = a.L;
+    double* out = a.out;
+    int64_t n = 1;
+    int status = kGdmDone;
+    out[0] = a.init[0];
+    out[1] = a.init[1];
+    out[2] = a.init[2];
+    const double tau = a.tau;
+    const int off[6][3] = {{0, -1, 0}, {0, 1, 0}, {-1, 0, 0}, {1, 0, 0}, {0, 0, -1}, {0, 0, 1}};
+    for (long k = 0; k < a.steps; ++k) {
+        const double* g = out + 3 * (n - 1);
+        bool o1, o2, o3;
+        double dx = interp3<R>(T, H, W, L, 1, g[0], g[1], g[2], o1);
+        double dy = interp3<R>(T, H, W, L, 0, g[0], g[1], g[2], o2);
+        double dz = interp3<R>(T, H, W, L, 2, g[0], g[1], g[2], o3);
+        if (o1 || o2 || o3) { status = kGdmError; break; }
+        if (__builtin_isnan(dx) || __builtin_isnan(dy) || __builtin_isnan(dz)) {  // :212-253
+            int64_t nx = (int64_t)__builtin_rint(g[0]), ny = (int64_t)__builtin_rint(g[1]), nz = (int64_t)__builtin_rint(g[2]);
+            bool err = false;
+            for (;;) {
+                if (nx < 0 || ny < 0 || nz < 0 || nx >= W || ny >= H || nz >= L) { err = true; break; }
+                if (!__builtin_isinf((double)T[(ny * W + nx) * L + nz])) break;
+                --n;
+                if (n == 0) { err = true; break; }
+                const double* q = out + 3 * (n - 1);
+                nx = (int64_t)__builtin_rint(q[0]);
+                ny = (int64_t)__builtin_rint(q[1]);
+                nz = (int64_t)__builtin_rint(q[2]);
+            }
+            if (err) { status = kGdmError; break; }
+            while (n > 0 && norm3(out[3 * (n - 1)] - nx, out[3 * (n - 1) + 1] - ny, out[3 * (n - 1) + 2] - nz) < 1) --n;
+            if (n >= a.cap) { status = kGdmError; break; }
+            out[3 * n] = (double)nx;
+            out[3 * n + 1] = (double)ny;
+            out[3 * n + 2] = (double)nz;
+            ++n;
+            double curT = (double)T[(ny * W + nx) * L + nz];
+            for (int q = 0; q < 6; ++q) {
+                int64_t cx = nx + off[q][0], cy = ny + off[q][1], cz = nz + off[q][2];
+                if (cx < 0) cx += W;  // python negative indices wrap
+                if (cy < 0) cy += H;
+                if (cz < 0) cz += L;
+                if (cx >= W || cy >= H || cz >= L) { err = true; break; }
+                const double tc = (double)T[(cy * W + cx) * L + cz];
+                if (tc < curT) {
+                    curT = tc;
+                    dx = (double)(-off[q][0]) / tau;
+                    dy = (double)(-off[q][1]) / tau;
+                    dz = (double)(-off[q][2]) / tau;
+                }
+            }
+            if (err) { status = kGdmError; break; }
+        }
+        g = out + 3 * (n - 1);
+        const double nrm = __builtin_sqrt(dx * dx + dy * dy + dz * dz);  // :255
+        double ax, ay, az;
+        if (nrm < 0.01) {
+            ax = g[0] - tau * (dx / nrm);
+            ay = g[1] - tau * (dy / nrm);
+            az = g[2] - tau * (dz / nrm);
+        } else {  // unnormalised step (:262-264)
+            ax = g[0] - tau * dx;
+            ay = g[1] - tau * dy;
+            az = g[2] - tau * dz;
+        }
+        if (n >= a.cap) { status = kGdmError; break; }
+        out[3 * n] = ax;
+        out[3 * n + 1] = ay;
+        out[3 * n + 2] = az;
+        ++n;
+        if (__builtin_isnan(ax) || __builtin_isnan(ay) || __builtin_isnan(az)) { status = kGdmError; break; }
+        if (norm3(ax - a.end[0], ay - a.end[1], az - a.end[2]) < 1.5) break;  // :266-267
+    }
+    if (status == kGdmDone && n < a.cap) {  // :269
+        out[3 * n] = a.end[0];
+        out[3 * n + 1] = a.end[1];
+        out[3 * n + 2] = a.end[2];
+        ++n;
+    }
+    *a.n_out = n;
+    *a.status = status;
+}
+
+hipError_t gdm3d(const Gdm3dArgs& a, bool f64, hipStream_t st) {
+    if (f64)
+        hipLaunchKernelGGL(gdm3d_kernel<double>, dim3(1), dim3(64), 0, st, a);
+    else
+        hipLaunchKernelGGL(gdm3d_kernel<float>, dim3(1), dim3(64), 0, st, a);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- full-field gradient
 __global__ void gradient2d_kernel(const double* __restrict__ T, int64_t H, int64_t W, double* __restrict__ gnx,
                                   double* __restrict__ gny) {

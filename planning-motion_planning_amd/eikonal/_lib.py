@@ -40,6 +40,24 @@ _lib = None
 _lock = threading.Lock()
 
 
+def _share_hip_runtime():
+    """Use ONE HIP runtime per process.  PyTorch-ROCm ships its own libamdhip64 (requested by
+    its libraries as "libamdhip64.so", soname libamdhip64.so.7); libeikonal asks for
+    "libamdhip64.so.7".  Whichever loads first, the other would otherwise map a second copy of
+    the runtime (and of HSA) into the process.  When torch is installed, pre-load the very file
+    torch uses so both resolve to it (the loader de-duplicates by soname and by file)."""
+    import importlib.util
+
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return
+    libdir = os.path.join(list(spec.submodule_search_locations)[0], "lib")
+    for name in ("libhsa-runtime64.so", "libamdhip64.so"):
+        p = os.path.join(libdir, name)
+        if os.path.exists(p):
+            C.CDLL(p, mode=C.RTLD_GLOBAL)
+
+
 def lib():
     """Load libeikonal.so; raise (never fall back) when it is absent."""
     global _lib
@@ -48,6 +66,7 @@ def lib():
             return _lib
         if not os.path.exists(LIB_PATH):
             raise EikError(EIK_ERR_NODEVICE, f"{LIB_PATH} not built (run __graft_entry__.build())")
+        _share_hip_runtime()
         L = C.CDLL(LIB_PATH)
         P = C.POINTER
         L.eik_version.restype = C.c_char_p
@@ -76,6 +95,12 @@ def lib():
         L.eik_fim2d_active.argtypes = [vp, P(i64)]
         L.eik_fim2d_stats.argtypes = [vp, P(EikStats)]
         L.eik_path2d_dev.argtypes = [vp, vp, C.c_int, i64, i64, _f64p, _f64p, C.c_double, vp, i64, vp, vp, vp]
+        L.eik_tmap3d_f32.argtypes = [vp, _f32p, i64, i64, i64, _i64p, _f32p]
+        L.eik_tmap3d_f64.argtypes = [vp, _f64p, i64, i64, i64, _i64p, _f64p]
+        L.eik_path3d_f64.argtypes = [vp, _f64p, i64, i64, i64, _f64p, _f64p, C.c_double, _f64p, i64, P(i64),
+                                     P(C.c_int)]
+        L.eik_fim3d_solve.argtypes = [vp, vp, vp, i64, i64, i64, C.c_int, _i64p, vp]
+        L.eik_path3d_dev.argtypes = [vp, vp, C.c_int, i64, i64, i64, _f64p, _f64p, C.c_double, vp, i64, vp, vp, vp]
         _lib = L
         return L
 
@@ -85,7 +110,8 @@ EXPORTED = [
     "eik_tmap2d_f32", "eik_tmap2d_f64", "eik_tmap2d_bidir_f64", "eik_tmap2d_batch_f32", "eik_path2d_f64",
     "eik_gradient2d_f64", "eik_fim2d_create", "eik_fim2d_destroy", "eik_fim2d_set_ghosts", "eik_fim2d_start",
     "eik_fim2d_iterate", "eik_fim2d_solve", "eik_fim2d_pack_edges", "eik_fim2d_merge_ghost", "eik_fim2d_active",
-    "eik_fim2d_stats", "eik_path2d_dev",
+    "eik_fim2d_stats", "eik_path2d_dev", "eik_tmap3d_f32", "eik_tmap3d_f64", "eik_path3d_f64", "eik_fim3d_solve",
+    "eik_path3d_dev",
 ]
 
 
@@ -157,6 +183,25 @@ class Context:
         n, st = i64(0), C.c_int(0)
         self._chk(lib().eik_path2d_f64(self._h, T, H, W, np.asarray(init, np.float64)[:2].copy(),
                                        np.asarray(end, np.float64)[:2].copy(), float(tau), out, cap, C.byref(n),
+                                       C.byref(st)))
+        return out[: n.value].copy(), st.value
+
+    def tmap3d(self, cost, goal, dtype=np.float64):
+        cost = np.ascontiguousarray(cost, dtype=dtype)
+        H, W, Lz = cost.shape
+        T = np.empty_like(cost)
+        fn = lib().eik_tmap3d_f64 if cost.dtype == np.float64 else lib().eik_tmap3d_f32
+        self._chk(fn(self._h, cost, H, W, Lz, np.ascontiguousarray(np.asarray(goal)[:3], np.int64), T))
+        return T
+
+    def path3d(self, T, init, end, tau=0.5):
+        T = np.ascontiguousarray(T, dtype=np.float64)
+        H, W, Lz = T.shape
+        cap = int(round(15000 / tau)) + 4
+        out = np.empty((cap, 3))
+        n, st = i64(0), C.c_int(0)
+        self._chk(lib().eik_path3d_f64(self._h, T, H, W, Lz, np.asarray(init, np.float64)[:3].copy(),
+                                       np.asarray(end, np.float64)[:3].copy(), float(tau), out, cap, C.byref(n),
                                        C.byref(st)))
         return out[: n.value].copy(), st.value
 

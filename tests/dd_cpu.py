@@ -1,0 +1,72 @@
+"""CPU local solver for the domain-decomposition tests (TEST INFRASTRUCTURE, numpy).
+
+Implements the duck-typed local-solver protocol of eikonal/dd.py (start / iterate /
+pack_edges / merge_ghost / active) with a vectorised Jacobi Godunov iteration on one block
+plus its ghost strips, so the rank-exchange logic of dd.solve can be exercised with the gloo
+backend on CPU.  The GPU path plugs eikonal.Fim2d into the same driver (dd.GpuLocal).
+"""
+import numpy as np
+import torch
+
+
+def godunov(a, b, c):
+    lo, hi = np.minimum(a, b), np.maximum(a, b)
+    with np.errstate(invalid="ignore"):
+        d = hi - lo
+        t2 = 0.5 * (lo + hi + np.sqrt(np.maximum(2 * c * c - d * d, 0.0)))
+    return np.where((hi == np.inf) | (c < d), lo + c, t2)
+
+
+class CpuLocal:
+    def __init__(self, cost, ghosts):
+        self.cost = np.asarray(cost, np.float64)
+        self.ghosts = ghosts  # torch tensors or None, order N S W E
+        self.T = None
+        self.dirty = False
+
+    def start(self, goal):
+        self.T = np.full(self.cost.shape, np.inf)
+        for g in self.ghosts:
+            if g is not None:
+                g.fill_(float("inf"))
+        if goal[0] >= 0:
+            self.T[goal[1], goal[0]] = 0.0
+        self.dirty = True
+
+    def _padded(self):
+        h, w = self.T.shape
+        P = np.full((h + 2, w + 2), np.inf)
+        P[1:-1, 1:-1] = self.T
+        for side, sl in ((0, (0, slice(1, -1))), (1, (-1, slice(1, -1))), (2, (slice(1, -1), 0)),
+                         (3, (slice(1, -1), -1))):
+            if self.ghosts[side] is not None:
+                P[sl] = self.ghosts[side].numpy()
+        return P
+
+    def iterate(self, k):
+        if not self.dirty:
+            return
+        while True:
+            P = self._padded()
+            a = np.minimum(P[1:-1, :-2], P[1:-1, 2:])
+            b = np.minimum(P[:-2, 1:-1], P[2:, 1:-1])
+            nv = np.minimum(self.T, godunov(a, b, self.cost))
+            if np.array_equal(nv, self.T):
+                break
+            self.T = nv
+        self.dirty = False
+
+    def pack_edges(self, n, s, w, e):
+        for t, v in ((n, self.T[0]), (s, self.T[-1]), (w, self.T[:, 0]), (e, self.T[:, -1])):
+            if t is not None:
+                t.copy_(torch.from_numpy(np.ascontiguousarray(v)))
+
+    def merge_ghost(self, side, recv):
+        g = self.ghosts[side]
+        m = torch.minimum(g, recv)
+        if bool((m < g).any()):
+            self.dirty = True
+        g.copy_(m)
+
+    def active(self):
+        return int(self.dirty)

@@ -1,0 +1,94 @@
+"""Multi-rank domain decomposition on CPU (gloo): the halo-exchange driver eikonal/dd.py, run
+with 2 and 4 ranks on blocks of one raster, must converge to the single-domain solution (the
+oracle FMM field, <= 1e-9 abs: same Godunov fixed point).  The GPU bench plugs the HIP solver
+into the same driver over RCCL."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle as O
+from eikonal import dd
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _cost(H, W, seed):
+    rng = np.random.default_rng(seed)
+    c = rng.uniform(1, 6, (H, W))
+    c[rng.random((H, W)) < 0.12] = np.inf
+    c[0, :] = c[-1, :] = c[:, 0] = c[:, -1] = np.inf
+    return c
+
+
+def _worker(rank, world, port, H, W, goal, seed, q):
+    from dd_cpu import CpuLocal
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    px, py = dd.SPLITS[world]
+    blk = dd.Block(H, W, px, py, rank)
+    cost = _cost(H, W, seed)[blk.y0:blk.y1, blk.x0:blk.x1]
+    send, recv, ghost = dd.make_strips(blk, torch.float64, "cpu", float("inf"))
+    loc = CpuLocal(cost, ghost)
+    loc.start(blk.local_goal(*goal))
+    rounds = dd.solve(loc, blk, send, recv, exchange_every=4)
+    q.put((rank, blk.y0, blk.y1, blk.x0, blk.x1, loc.T, rounds))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_dd_matches_single_domain(world):
+    H, W, seed = 48, 70, 3
+    goal = (9, 30)
+    c = _cost(H, W, seed)
+    c[goal[1], goal[0]] = 2.0
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, H, W, goal, seed, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    parts = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    T = np.full((H, W), np.nan)
+    for _, y0, y1, x0, x1, Tb, rounds in parts:
+        T[y0:y1, x0:x1] = Tb
+        assert rounds >= 2  # the front crossed at least one rank boundary
+    O.set_strict(False)
+    try:
+        cc = c.copy()
+        R = O.fmm2d(cc, goal)
+    finally:
+        O.set_strict(True)
+    fin = np.isfinite(R)
+    assert np.array_equal(np.isfinite(T), fin)
+    assert np.abs(T[fin] - R[fin]).max() <= 1e-9
+
+
+def test_block_partition_covers_raster():
+    for world, (px, py) in dd.SPLITS.items():
+        H, W = 100, 130
+        cov = np.zeros((H, W), int)
+        for r in range(world):
+            b = dd.Block(H, W, px, py, r)
+            cov[b.y0:b.y1, b.x0:b.x1] += 1
+            for s, nb in enumerate(b.nb):
+                if nb is not None:  # neighbour relation is symmetric
+                    opp = {0: 1, 1: 0, 2: 3, 3: 2}[s]
+                    assert dd.Block(H, W, px, py, nb).nb[opp] == r
+        assert (cov == 1).all()

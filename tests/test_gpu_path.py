@@ -95,3 +95,33 @@ def test_bidirectional(ctx, golden, i):
     rover = np.vstack((np.flipud(ps), pg[1:]))
     ref = np.vstack((np.flipud(d[p + "pathS"]), d[p + "pathG"][1:]))
     assert hausdorff(rover, ref) <= 3.0
+
+
+def test_path_device_fp32_field(ctx):
+    """eik_path2d_dev on a device-resident fp32 field (the bench's ms-to-path route)."""
+    import ctypes
+    import torch
+
+    import eikonal
+    from eikonal import _lib as L
+
+    rng = np.random.default_rng(4)
+    cost = rng.uniform(1, 3, (300, 340)).astype(np.float32)
+    cost[0, :] = cost[-1, :] = cost[:, 0] = cost[:, -1] = np.inf
+    goal, start = (250, 200), (30, 40)
+    T64 = ctx.tmap2d(cost.astype(np.float64), goal, dtype=np.float64)
+    ref, rst = ctx.path2d(T64, start, goal)
+    dev = torch.device("cuda", 0)
+    T = torch.from_numpy(T64.astype(np.float32)).to(dev)
+    cap = 30004
+    out = torch.empty((cap, 2), dtype=torch.float64, device=dev)
+    n = torch.zeros(1, dtype=torch.int64, device=dev)
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream(dev)
+    ctx._chk(L.lib().eik_path2d_dev(ctx._h, T.data_ptr(), L.EIK_F32, 300, 340, np.array(start, np.float64),
+                                    np.array(goal, np.float64), 0.5, out.data_ptr(), cap, n.data_ptr(),
+                                    st.data_ptr(), s.cuda_stream))
+    k = int(n.item())
+    path = out[:k].cpu().numpy()
+    assert k == len(ref) and int(st.item()) == rst
+    assert np.abs(path - ref).max() < 1e-3  # fp32 field vs fp64 field (BASELINE.md path tolerance)
