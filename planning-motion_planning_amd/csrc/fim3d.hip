@@ -54,7 +54,7 @@ __global__ __launch_bounds__(256) void fim3d_sweep_kernel(Fim3dArgs a) {
     __shared__ R Ts[kMaxHalo];
     __shared__ R Cs[kMaxCells];
     __shared__ unsigned s_flags;
-    __shared__ int s_changed[2];  // double-buffered by pass parity (no reset/read race)
+    __shared__ int s_changed[3];  // triple-buffered by pass: reset two barriers after the last read
 
     const int tid = threadIdx.x;
     const int cur = a.iter % 3, nxt = (a.iter + 1) % 3, rst = (a.iter + 2) % 3;
@@ -75,6 +75,7 @@ __global__ __launch_bounds__(256) void fim3d_sweep_kernel(Fim3dArgs a) {
             s_flags = 0;
             s_changed[0] = 0;
             s_changed[1] = 0;
+            s_changed[2] = 0;
         }
         // stage the halo box (cells outside the volume read +inf)
         const int nh = HX * HY * HZ;
@@ -108,7 +109,7 @@ __global__ __launch_bounds__(256) void fim3d_sweep_kernel(Fim3dArgs a) {
         bool last = false;
         const int sx = HZ, sy = HX * HZ;
         for (int pass = 0; pass < a.max_passes; ++pass) {
-            const int slot = pass & 1;
+            const int slot = pass % 3;
             bool ch = false;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -125,7 +126,7 @@ __global__ __launch_bounds__(256) void fim3d_sweep_kernel(Fim3dArgs a) {
                 }
             }
             if (ch) s_changed[slot] = 1;
-            if (tid == 0) s_changed[slot ^ 1] = 0;  // next pass's flag: last read two passes ago
+            if (tid == 0) s_changed[(pass + 1) % 3] = 0;  // read at pass-2, all past barrier pass-1
             __syncthreads();
             last = s_changed[slot] != 0;
             if (!last) break;
