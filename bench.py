@@ -88,36 +88,37 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    if not args.no_timing:
-        ctx.set_option(L.OPT_TIMING, 1)
-    visits = 0
-    sweep_ms = 0.0
-    iters = 0
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        s = fim.stats()
-        visits += s["tile_visits"]
-        sweep_ms += s["sweep_ms"]
-        iters += s["iterations"]
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    ctx.set_option(L.OPT_TIMING, 0)
-    el = t1 - t0
-    if world > 1:
-        tt = torch.tensor([el], device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = tt.item()
-        agg = torch.tensor([visits, iters], dtype=torch.float64, device=dev)
-        dist.all_reduce(agg)
-        visits_all, iters_all = agg.tolist()
-    else:
-        visits_all, iters_all = visits, iters
+
+    def timed(instrument):
+        """K steps between barrier + synchronize; returns (max-over-ranks seconds, visits, sweep_ms, iters)."""
+        ctx.set_option(L.OPT_TIMING, 1 if instrument else 0)
+        visits, sweep_ms, iters = 0, 0.0, 0
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+            if instrument:
+                s = fim.stats()
+                visits += s["tile_visits"]
+                sweep_ms += s["sweep_ms"]
+                iters += s["iterations"]
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        ctx.set_option(L.OPT_TIMING, 0)
+        if world > 1:
+            tt = torch.tensor([el], device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = tt.item()
+        return el, visits, sweep_ms, iters
+
+    # 1) the measurement: no per-launch instrumentation inside the timed region
+    el, _, _, _ = timed(False)
+    # 2) the same K steps again with a hipEvent pair around every sweep launch (roofline)
+    el_i, visits, sweep_ms, iters = (0.0, 0, 0.0, 0) if args.no_timing else timed(True)
 
     value = H * W * args.steps / el / 1e9
     ms_per_step = el / args.steps * 1e3
@@ -141,6 +142,7 @@ def main():
         "traffic": traffic,
         "alg_bytes_per_launch": round(visits * BYTES_PER_VISIT / max(launches, 1)),
         "avg_launch_us": round(sweep_ms * 1e3 / max(launches, 1), 2),
+        "instrumented_ms_per_step": round(el_i / args.steps * 1e3, 4),
         "launches_per_solve": round(launches / args.steps, 1),
         "tile_visits_per_solve": round(visits / args.steps, 1),
     }

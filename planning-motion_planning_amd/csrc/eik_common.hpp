@@ -40,18 +40,60 @@ __device__ __forceinline__ float godunov2<float>(float a, float b, float c) {
     const float lo = fminf(a, b), hi = fmaxf(a, b);
     const float d = hi - lo;
     const float t1 = lo + c;
-#ifdef EIK_IEEE_SQRT
-    const float t2 = 0.5f * (lo + hi + __builtin_sqrtf(2.f * (c * c) - d * d));
-#else
     const float t2 = 0.5f * (lo + hi + __builtin_amdgcn_sqrtf(2.f * (c * c) - d * d));  // v_sqrt_f32, <= 1 ulp
-#endif
     return (hi == Real<float>::inf() || c < d) ? t1 : t2;
+}
+
+// min / max of non-negative floats (and +inf, and NaN, which sorts above +inf) on the bit
+// patterns: v_min_u32 / v_max_u32, no NaN canonicalisation as fminf/fmaxf need.
+__device__ __forceinline__ float umin(float a, float b) {
+    return __uint_as_float(min(__float_as_uint(a), __float_as_uint(b)));
+}
+__device__ __forceinline__ float umax(float a, float b) {
+    return __uint_as_float(max(__float_as_uint(a), __float_as_uint(b)));
+}
+__device__ __forceinline__ double umin(double a, double b) {
+    const unsigned long long x = __double_as_longlong(a), y = __double_as_longlong(b);
+    return __longlong_as_double(x < y ? x : y);
+}
+__device__ __forceinline__ double umax(double a, double b) {
+    const unsigned long long x = __double_as_longlong(a), y = __double_as_longlong(b);
+    return __longlong_as_double(x < y ? y : x);
+}
+
+// Sweep-step form: the one-inf case is folded into c < d (d = inf), and the both-inf case
+// yields NaN, which the caller's unsigned min / ds_min / `<` tests all treat as "no update"
+// -- shorter than godunov2.  Inputs are non-negative, +inf, never NaN.
+__device__ __forceinline__ float godunov2_step(float a, float b, float c) {
+    const float lo = umin(a, b), hi = umax(a, b);
+    const float d = hi - lo;
+    // 0.5 (a + b + sqrt(2c^2 - d^2)) written as lo + 0.5 (d + sqrt(.)): ONE rounding at the
+    // magnitude of T instead of three -- the fp32 error then stays within 2e-5 on 4096^2 fields
+    // with costs up to 300 (T ~ 1e5), where the direct form drifts past it.
+    const float t2 = lo + 0.5f * (d + __builtin_amdgcn_sqrtf(2.f * (c * c) - d * d));
+    return c < d ? lo + c : t2;
+}
+__device__ __forceinline__ double godunov2_step(double a, double b, double c) {
+    const double lo = umin(a, b), hi = umax(a, b);
+    const double d = hi - lo;
+    const double t2 = lo + 0.5 * (d + __builtin_sqrt(2.0 * (c * c) - d * d));
+    return c < d ? lo + c : t2;
 }
 
 // Whole-wave shift by one lane (lane i <- lane i-1) on the DPP path: v_mov_b32_dpp wave_shr:1.
 // Keeps the Gauss-Seidel dependency of the skewed sweep in registers (no LDS round trip).
 __device__ __forceinline__ float wave_shr1(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xF, 0xF, false));
+}
+// Same, lane 0 receives `lane0` (bound_ctrl off: an out-of-range source keeps the old value).
+__device__ __forceinline__ float wave_shr1(float v, float lane0) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(lane0), __float_as_int(v), 0x138, 0xF, 0xF, false));
+}
+__device__ __forceinline__ double wave_shr1(double v, double lane0) {
+    const unsigned long long u = __double_as_longlong(v), o = __double_as_longlong(lane0);
+    const int lo = __builtin_amdgcn_update_dpp((int)(o & 0xffffffffu), (int)(u & 0xffffffffu), 0x138, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(u >> 32), 0x138, 0xF, 0xF, false);
+    return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 __device__ __forceinline__ double wave_shr1(double v) {
     const unsigned long long u = __double_as_longlong(v);

@@ -18,6 +18,7 @@ struct Fim2dArgs {
     int capacity;          // B * tiles_per_map
     unsigned iter;         // outer iteration index of this launch
     int max_rounds;        // sweep rounds per tile visit
+    float keep;            // 1 - tol: a change counts for (re)activation only if new < old * keep
     unsigned long long* visits;  // tile-visit counter (stats / roofline bytes)
     unsigned* edge_dirty;  // DD: bit per subdomain side whose edge row/column changed
 };

@@ -54,6 +54,7 @@ struct eik_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     int max_rounds = 1;
+    double tol = 0.0;
     int sync_every = 8;
     int timing = 0;
     int grid = 0;
@@ -148,6 +149,7 @@ int eik_set_option(eik_ctx* c, int opt, double v) {
         case EIK_OPT_SYNC_EVERY: c->sync_every = std::max(1, (int)v); break;
         case EIK_OPT_TIMING: c->timing = v != 0; break;
         case EIK_OPT_GRID: c->grid = v > 0 ? (int)v : 4 * c->cu_count; break;
+        case EIK_OPT_TOL: c->tol = v > 0 ? v : 0.0; break;
         default: return set_err(c, EIK_ERR_ARG, "unknown option %d", opt);
     }
     return EIK_OK;
@@ -237,6 +239,7 @@ int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
     f->a.T = d_T;
     f->a.iter = 0;
     f->a.max_rounds = c->max_rounds;
+    f->a.keep = (float)(1.0 - c->tol);
     f->iterations = 0;
     f->host_syncs = 0;
     f->sweep_ms = 0.0;

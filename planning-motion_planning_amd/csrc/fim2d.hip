@@ -44,48 +44,44 @@ __device__ __forceinline__ void enqueue(const Fim2dArgs& a, int tile, int list, 
 }
 
 // One quadrant sweep of the staged tile.  DX/DY = +-1: direction of propagation.
-// Branch-free: lanes outside the tile (skew prologue/epilogue) compute on clamped addresses and
-// merge +inf (a no-op ds_min).
+// Lane l owns column x; at step s it updates row r = s - l (skewed Gauss-Seidel), so its
+// upstream x neighbour is lane l-1's previous result (DPP) and its upstream y neighbour its own.
+// Branch- and select-free: r is clamped to [-1, 64]; rows -1 and 64 are the halo rows, whose
+// cost is +inf in Cs (same 66-stride layout as Ts), so a lane outside the tile computes +inf or
+// NaN and its ds_min / min / `<` are no-ops.  Every LDS access of a step shares one address.
 template <typename R, int DX, int DY>
-__device__ __forceinline__ bool sweep_quadrant(R* __restrict__ Ts, const R* __restrict__ Cs, int lane) {
-    constexpr R INF = Real<R>::inf();
+__device__ __forceinline__ bool sweep_quadrant(R* __restrict__ Ts, const R* __restrict__ Cs, int lane, R keep) {
     const int x = DX > 0 ? lane : kTile - 1 - lane;
     const int col = x + 1;
     bool changed = false;
-    R cur = INF;
 
-    R p_old, p_dnx, p_dny, p_upx, p_c;
-    int p_o;
-    auto fetch = [&](int s, int& o, R& old, R& dx, R& dy, R& ux, R& c) {
+    auto addr = [&](int s) {
         int r = s - lane;
-        r = r < -1 ? -1 : (r > kTile - 1 ? kTile - 1 : r);
-        const int lr = DY > 0 ? r + 1 : kTile - r;  // LDS row: 0..65 (halo rows at r == -1)
-        o = lr * kLds + col;
-        old = Ts[o];
-        dx = Ts[o + DX];
-        dy = Ts[o + DY * kLds];
-        ux = Ts[o - DX];  // halo column, used by lane 0 only
-        // clamp: an out-of-array index would be UB, and the compiler then assumes r >= 0 and
-        // drops the +inf masking of the halo-row step
-        const int yc = lr < 1 ? 0 : (lr > kTile ? kTile - 1 : lr - 1);
-        c = Cs[yc * kTile + x];
+        r = r < -1 ? -1 : (r > kTile ? kTile : r);
+        const int lr = DY > 0 ? r + 1 : kTile - r;  // LDS row 0..65
+        return lr * kLds + col;
     };
-    fetch(-1, p_o, p_old, p_dnx, p_dny, p_upx, p_c);
-#pragma unroll 2
-    for (int s = -1; s < 2 * kTile - 1; ++s) {
+    // the upstream halo row value is the lane's "previous row" result before it starts
+    R cur = Ts[(DY > 0 ? 0 : kLds - 1) * kLds + col];
+    int o = addr(0);
+    R p_old = Ts[o], p_dnx = Ts[o + DX], p_dny = Ts[o + DY * kLds], p_upx = Ts[o - DX], p_c = Cs[o];
+#pragma clang loop unroll_count(2)
+    for (int s = 0; s < 2 * kTile; ++s) {
         const R old = p_old, dnx = p_dnx, dny = p_dny, uxh = p_upx, c = p_c;
-        const int o = p_o;
-        fetch(s + 1, p_o, p_old, p_dnx, p_dny, p_upx, p_c);  // issued before this step's ds_min
-        const int r = s - lane;
-        R upx = wave_shr1(cur);
-        upx = lane == 0 ? uxh : upx;
-        const R a = upx < dnx ? upx : dnx;
-        const R b = cur < dny ? cur : dny;
-        const R nv = godunov2<R>(a, b, c);
-        const R w = (unsigned)r < (unsigned)kTile ? nv : INF;
-        lds_min(&Ts[o], w);
-        changed |= w < old;
-        cur = w < old ? w : old;  // r == -1: the upstream halo row value
+        const int oc = o;
+        o = addr(s + 1);  // next step's loads issue before this step's ds_min (no intra-wave RAW)
+        p_old = Ts[o];
+        p_dnx = Ts[o + DX];
+        p_dny = Ts[o + DY * kLds];
+        p_upx = Ts[o - DX];
+        p_c = Cs[o];
+        const R upx = wave_shr1(cur, uxh);  // lane 0: halo column
+        const R a = umin(upx, dnx);
+        const R b = umin(cur, dny);
+        const R w = godunov2_step(a, b, c);
+        lds_min(&Ts[oc], w);
+        changed |= w < old * keep;
+        cur = umin(w, old);  // NaN (both-inf case) sorts above every value: keeps old
     }
     return changed;
 }
@@ -93,15 +89,23 @@ __device__ __forceinline__ bool sweep_quadrant(R* __restrict__ Ts, const R* __re
 template <typename R>
 __global__ __launch_bounds__(kThreads) void fim2d_sweep_kernel(Fim2dArgs a) {
     constexpr R INF = Real<R>::inf();
-    __shared__ R Ts[kLds * kLds];
-    __shared__ R Cs[kTile * kTile];
+    // Ts: tile + halo ring, plus one guard row above and below (the clamped r = -1 / 64 steps
+    // read one row beyond the halo: in-bounds, +inf, and masked by the +inf halo cost anyway)
+    __shared__ R Tbuf[(kLds + 2) * kLds];
+    __shared__ R Cs[kLds * kLds];  // same layout as Ts; halo ring = +inf
+    R* const Ts = Tbuf + kLds;
     __shared__ unsigned s_round, s_flags;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid < kLds) {
+        Tbuf[tid] = INF;
+        Tbuf[(kLds + 1) * kLds + tid] = INF;
+    }
     const int cur = a.iter % 3, nxt = (a.iter + 1) % 3, rst = (a.iter + 2) % 3;
     const int cnt = a.counts[cur];
     if (blockIdx.x == 0 && tid == 0) a.counts[rst] = 0;
     const unsigned stamp = a.iter + 2;  // "enqueued for iteration iter+1"
+    const R keep = (R)a.keep;
 
     for (int it = blockIdx.x; it < cnt; it += gridDim.x) {
         const int tile = a.lists[(int64_t)cur * a.capacity + it];
@@ -129,16 +133,16 @@ __global__ __launch_bounds__(kThreads) void fim2d_sweep_kernel(Fim2dArgs a) {
                     const float4 t4 = *reinterpret_cast<const float4*>(&T[gy * a.W + x0 + cx]);
                     const float4 c4 = *reinterpret_cast<const float4*>(&cost[gy * a.W + x0 + cx]);
                     told[4 * k + 0] = t4.x; told[4 * k + 1] = t4.y; told[4 * k + 2] = t4.z; told[4 * k + 3] = t4.w;
-                    Cs[ry * kTile + cx + 0] = c4.x; Cs[ry * kTile + cx + 1] = c4.y;
-                    Cs[ry * kTile + cx + 2] = c4.z; Cs[ry * kTile + cx + 3] = c4.w;
+                    R* cr = &Cs[(ry + 1) * kLds + cx + 1];
+                    cr[0] = c4.x; cr[1] = c4.y; cr[2] = c4.z; cr[3] = c4.w;
                 } else {
                     const double2 t0 = *reinterpret_cast<const double2*>(&T[gy * a.W + x0 + cx]);
                     const double2 t1 = *reinterpret_cast<const double2*>(&T[gy * a.W + x0 + cx + 2]);
                     const double2 c0 = *reinterpret_cast<const double2*>(&cost[gy * a.W + x0 + cx]);
                     const double2 c1 = *reinterpret_cast<const double2*>(&cost[gy * a.W + x0 + cx + 2]);
                     told[4 * k + 0] = t0.x; told[4 * k + 1] = t0.y; told[4 * k + 2] = t1.x; told[4 * k + 3] = t1.y;
-                    Cs[ry * kTile + cx + 0] = c0.x; Cs[ry * kTile + cx + 1] = c0.y;
-                    Cs[ry * kTile + cx + 2] = c1.x; Cs[ry * kTile + cx + 3] = c1.y;
+                    R* cr = &Cs[(ry + 1) * kLds + cx + 1];
+                    cr[0] = c0.x; cr[1] = c0.y; cr[2] = c1.x; cr[3] = c1.y;
                 }
             } else {
 #pragma unroll
@@ -146,7 +150,7 @@ __global__ __launch_bounds__(kThreads) void fim2d_sweep_kernel(Fim2dArgs a) {
                     const int64_t gx = x0 + cx + e;
                     const bool in = gy < a.H && gx < a.W;
                     told[4 * k + e] = load_T<R>(a, T, gy, gx);  // ghost cells land in padding
-                    Cs[ry * kTile + cx + e] = in ? cost[gy * a.W + gx] : INF;
+                    Cs[(ry + 1) * kLds + cx + e + 1] = in ? cost[gy * a.W + gx] : INF;
                 }
             }
 #pragma unroll
@@ -159,10 +163,14 @@ __global__ __launch_bounds__(kThreads) void fim2d_sweep_kernel(Fim2dArgs a) {
             else if (wave == 1) v = load_T<R>(a, T, y0 + kTile, x0 + lane);
             else if (wave == 2) v = load_T<R>(a, T, y0 + lane, x0 - 1);
             else                v = load_T<R>(a, T, y0 + lane, x0 + kTile);
-            if (wave == 0)      Ts[0 * kLds + lane + 1] = v;
-            else if (wave == 1) Ts[(kLds - 1) * kLds + lane + 1] = v;
-            else if (wave == 2) Ts[(lane + 1) * kLds + 0] = v;
-            else                Ts[(lane + 1) * kLds + kLds - 1] = v;
+            int h;
+            if (wave == 0)      h = 0 * kLds + lane + 1;
+            else if (wave == 1) h = (kLds - 1) * kLds + lane + 1;
+            else if (wave == 2) h = (lane + 1) * kLds + 0;
+            else                h = (lane + 1) * kLds + kLds - 1;
+            Ts[h] = v;
+            Cs[h] = INF;
+            if (lane < 4) Cs[(lane >> 1) * (kLds - 1) * kLds + (lane & 1) * (kLds - 1)] = INF;  // corners
         }
         __syncthreads();
 
@@ -170,10 +178,10 @@ __global__ __launch_bounds__(kThreads) void fim2d_sweep_kernel(Fim2dArgs a) {
         bool last_changed = false;
         for (int round = 0;; ++round) {
             bool ch;
-            if (wave == 0)      ch = sweep_quadrant<R, +1, +1>(Ts, Cs, lane);
-            else if (wave == 1) ch = sweep_quadrant<R, -1, +1>(Ts, Cs, lane);
-            else if (wave == 2) ch = sweep_quadrant<R, +1, -1>(Ts, Cs, lane);
-            else                ch = sweep_quadrant<R, -1, -1>(Ts, Cs, lane);
+            if (wave == 0)      ch = sweep_quadrant<R, +1, +1>(Ts, Cs, lane, keep);
+            else if (wave == 1) ch = sweep_quadrant<R, -1, +1>(Ts, Cs, lane, keep);
+            else if (wave == 2) ch = sweep_quadrant<R, +1, -1>(Ts, Cs, lane, keep);
+            else                ch = sweep_quadrant<R, -1, -1>(Ts, Cs, lane, keep);
             if (__any(ch) && lane == 0) atomicOr(&s_round, 1u << (round & 31));
             __syncthreads();
             last_changed = (s_round >> (round & 31)) & 1u;
@@ -193,7 +201,7 @@ __global__ __launch_bounds__(kThreads) void fim2d_sweep_kernel(Fim2dArgs a) {
                 nv[e] = Ts[(ry + 1) * kLds + cx + e + 1];
                 const bool chg = nv[e] < told[4 * k + e];
                 any |= chg;
-                if (chg) {
+                if (nv[e] < told[4 * k + e] * keep) {
                     // A neighbour can only improve if this edge value undercuts the neighbour's
                     // adjacent cell (the halo value, stale => larger => conservative).
                     const int lx = cx + e + 1, ly = ry + 1;
@@ -232,15 +240,15 @@ __global__ __launch_bounds__(kThreads) void fim2d_sweep_kernel(Fim2dArgs a) {
         }
         if (fl) atomicOr(&s_flags, fl);
         __syncthreads();
-        if (tid == 0) {
+        if (tid < 5) {  // up to 5 enqueues, one per lane, so their atomics overlap
             const unsigned f = s_flags;
             const int base = map * a.tiles_per_map;
-            if (last_changed) enqueue(a, tile, nxt, stamp);
-            if ((f & 1u) && ty > 0) enqueue(a, base + rem - a.ntx, nxt, stamp);
-            if ((f & 2u) && ty + 1 < a.nty) enqueue(a, base + rem + a.ntx, nxt, stamp);
-            if ((f & 4u) && tx > 0) enqueue(a, base + rem - 1, nxt, stamp);
-            if ((f & 8u) && tx + 1 < a.ntx) enqueue(a, base + rem + 1, nxt, stamp);
-            if (a.edge_dirty) {  // subdomain edges (domain decomposition)
+            if (tid == 0 && last_changed) enqueue(a, tile, nxt, stamp);
+            if (tid == 1 && (f & 1u) && ty > 0) enqueue(a, base + rem - a.ntx, nxt, stamp);
+            if (tid == 2 && (f & 2u) && ty + 1 < a.nty) enqueue(a, base + rem + a.ntx, nxt, stamp);
+            if (tid == 3 && (f & 4u) && tx > 0) enqueue(a, base + rem - 1, nxt, stamp);
+            if (tid == 4 && (f & 8u) && tx + 1 < a.ntx) enqueue(a, base + rem + 1, nxt, stamp);
+            if (tid == 0 && a.edge_dirty) {  // subdomain edges (domain decomposition)
                 unsigned e = 0;
                 if ((f & 1u) && ty == 0) e |= 1u;
                 if (((f & 2u) || (f & 32u)) && ty + 1 == a.nty) e |= 2u;
@@ -248,7 +256,7 @@ __global__ __launch_bounds__(kThreads) void fim2d_sweep_kernel(Fim2dArgs a) {
                 if (((f & 8u) || (f & 64u)) && tx + 1 == a.ntx) e |= 8u;
                 if (e) atomicOr(a.edge_dirty, e);
             }
-            if (a.visits) atomicAdd(a.visits, 1ull);
+            if (tid == 0 && a.visits) atomicAdd(a.visits, 1ull);
         }
         __syncthreads();  // LDS reuse by the next tile of this workgroup
     }

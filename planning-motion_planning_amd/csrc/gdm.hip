@@ -64,54 +64,128 @@ __device__ __forceinline__ double norm2(double a, double b) { return __builtin_s
 
 enum { kGdmDone = 0, kGdmFallback = 1, kGdmError = 2 };
 
+// LDS window around the walker: the inf-aware normalised gradient (Gnx, Gny) of a 32 x 32 node
+// block is computed by all 64 lanes when the walker's 2 x 2 interpolation corners leave the
+// block (every ~30 steps at tau = 0.5); each step then reads 8 values from LDS.  The gradient at
+// a node depends on T only, so precomputing it is exactly the reference's per-step
+// computeGradient evaluated earlier.
+constexpr int kG = 32;  // gradient block side (nodes)
+
+struct Win {
+    double gx[kG][kG + 1], gy[kG][kG + 1];
+    double t[kG + 2][kG + 3];  // T on the block + 1-node margin
+    int64_t x0, y0;
+};
+
+// computeGradient body at (j, i) reading the T window (FastMarching.py:262-297)
+__device__ void grad_win(const Win& w, int64_t m, int64_t n, int64_t j, int64_t i, double& gnx, double& gny) {
+#define TW(J, I) w.t[(J) - w.y0 + 1][(I) - w.x0 + 1]
+    double gy, gx;
+    if (j == 0)
+        gy = TW(1, i) - TW(0, i);
+    else if (j == m - 1)
+        gy = TW(j, i) - TW(j - 1, i);
+    else if (__builtin_isinf(TW(j + 1, i)))
+        gy = __builtin_isinf(TW(j - 1, i)) ? 0.0 : TW(j, i) - TW(j - 1, i);
+    else
+        gy = __builtin_isinf(TW(j - 1, i)) ? TW(j + 1, i) - TW(j, i) : (TW(j + 1, i) - TW(j - 1, i)) / 2;
+    if (i == 0)
+        gx = TW(j, 1) - TW(j, 0);
+    else if (i == n - 1)
+        gx = TW(j, i) - TW(j, i - 1);
+    else if (__builtin_isinf(TW(j, i + 1)))
+        gx = __builtin_isinf(TW(j, i - 1)) ? 0.0 : TW(j, i) - TW(j, i - 1);
+    else
+        gx = __builtin_isinf(TW(j, i - 1)) ? TW(j, i + 1) - TW(j, i) : (TW(j, i + 1) - TW(j, i - 1)) / 2;
+#undef TW
+    const double den = __builtin_sqrt(gx * gx + gy * gy);
+    gnx = gx / den;
+    gny = gy / den;
+}
+
+template <typename R>
+__device__ void win_load(Win& w, const R* __restrict__ T, int64_t H, int64_t W, int64_t i, int64_t j) {
+    int64_t x0 = i - kG / 2, y0 = j - kG / 2;
+    x0 = x0 + kG > W ? W - kG : x0;
+    y0 = y0 + kG > H ? H - kG : y0;
+    x0 = x0 < 0 ? 0 : x0;
+    y0 = y0 < 0 ? 0 : y0;
+    __syncthreads();
+    const int lane = threadIdx.x;
+    if (lane == 0) {
+        w.x0 = x0;
+        w.y0 = y0;
+    }
+    for (int e = lane; e < (kG + 2) * (kG + 2); e += 64) {
+        const int r = e / (kG + 2), c = e - r * (kG + 2);
+        const int64_t gy = y0 - 1 + r, gx = x0 - 1 + c;
+        w.t[r][c] = (gy >= 0 && gy < H && gx >= 0 && gx < W) ? (double)T[gy * W + gx] : 0.0;
+    }
+    __syncthreads();
+    for (int e = lane; e < kG * kG; e += 64) {
+        const int r = e / kG, c = e - r * kG;
+        const int64_t gy = y0 + r, gx = x0 + c;
+        if (gy < H && gx < W) grad_win(w, H, W, gy, gx, w.gx[r][c], w.gy[r][c]);
+    }
+    __syncthreads();
+}
+
 template <typename R>
 __global__ __launch_bounds__(64) void gdm2d_kernel(Gdm2dArgs a) {
-    if (threadIdx.x != 0) return;
+    __shared__ Win w;
     const R* __restrict__ T = static_cast<const R*>(a.T);
     const int64_t H = a.H, W = a.W;
+    const bool lead = threadIdx.x == 0;
     double* out = a.out;
-    int64_t n = 0;
     int status = kGdmDone;
-    out[0] = a.ix;
-    out[1] = a.iy;
-    n = 1;
+    double px = a.ix, py = a.iy;  // gamma[-1], kept in registers (all lanes)
+    if (lead) {
+        out[0] = px;
+        out[1] = py;
+    }
+    int64_t n = 1;
     const double tau = a.tau;
-    bool finished = false;
-    for (long k = 0; k < a.steps && !finished; ++k) {
-        const double px = out[2 * (n - 1)], py = out[2 * (n - 1) + 1];
-        if (__builtin_isnan(px) || __builtin_isnan(py)) { status = kGdmError; finished = true; break; }
+    w.x0 = -((int64_t)1 << 40);
+    w.y0 = -((int64_t)1 << 40);
+    __syncthreads();
+    for (long k = 0; k < a.steps; ++k) {
+        if (__builtin_isnan(px) || __builtin_isnan(py)) { status = kGdmError; break; }
         const uint32_t i = (uint32_t)__builtin_trunc(px), j = (uint32_t)__builtin_trunc(py);
-        if (i + 1 >= (uint64_t)W || j + 1 >= (uint64_t)H) { status = kGdmError; finished = true; break; }
-        double gx[2][2], gy[2][2];
-        for (int jj = 0; jj < 2; ++jj)
-            for (int ii = 0; ii < 2; ++ii) grad_at<R>(T, H, W, j + jj, i + ii, gx[jj][ii], gy[jj][ii]);
+        if (i + 1 >= (uint64_t)W || j + 1 >= (uint64_t)H) { status = kGdmError; break; }
+        // the 2 x 2 interpolation corners must lie in the gradient block
+        if ((int64_t)i < w.x0 || (int64_t)j < w.y0 || (int64_t)i + 1 >= w.x0 + kG || (int64_t)j + 1 >= w.y0 + kG)
+            win_load<R>(w, T, H, W, i, j);
+        const int li = (int)(i - w.x0), lj = (int)(j - w.y0);
+        const double gx[2][2] = {{w.gx[lj][li], w.gx[lj][li + 1]}, {w.gx[lj + 1][li], w.gx[lj + 1][li + 1]}};
+        const double gy[2][2] = {{w.gy[lj][li], w.gy[lj][li + 1]}, {w.gy[lj + 1][li], w.gy[lj + 1][li + 1]}};
         const double fa = px - i, fb = py - j;
         double dx = interp2_patch(fa, fb, gx);
         double dy = interp2_patch(fa, fb, gy);
         if (__builtin_isnan(dx) || __builtin_isnan(dy)) {
             // NaN fallback (:178-218) as the reference behaves under numpy 2: the neighbour
             // probe `np.uint32(nearN + [0,-1])` raises OverflowError, caught at :217.
-            int64_t nx = (int64_t)__builtin_rint(px), ny = (int64_t)__builtin_rint(py);
-            bool empty = false, oob = false;
-            for (;;) {
-                const int64_t wx = nx < 0 ? nx + W : nx, wy = ny < 0 ? ny + H : ny;
-                if (wx < 0 || wy < 0 || wx >= W || wy >= H) { oob = true; break; }
-                if (!__builtin_isinf(tv(T, W, wy, wx))) break;
-                --n;
-                if (n == 0) { empty = true; break; }
-                nx = (int64_t)__builtin_rint(out[2 * (n - 1)]);
-                ny = (int64_t)__builtin_rint(out[2 * (n - 1) + 1]);
-            }
-            if (!empty && !oob) {
-                while (n > 0 && norm2(out[2 * (n - 1)] - (double)nx, out[2 * (n - 1) + 1] - (double)ny) < 1) --n;
-                if (n < a.cap) {
-                    out[2 * n] = (double)nx;
-                    out[2 * n + 1] = (double)ny;
-                    ++n;
+            if (lead) {
+                int64_t nx = (int64_t)__builtin_rint(px), ny = (int64_t)__builtin_rint(py);
+                bool empty = false, oob = false;
+                for (;;) {
+                    const int64_t wx = nx < 0 ? nx + W : nx, wy = ny < 0 ? ny + H : ny;
+                    if (wx < 0 || wy < 0 || wx >= W || wy >= H) { oob = true; break; }
+                    if (!__builtin_isinf(tv(T, W, wy, wx))) break;
+                    --n;
+                    if (n == 0) { empty = true; break; }
+                    nx = (int64_t)__builtin_rint(out[2 * (n - 1)]);
+                    ny = (int64_t)__builtin_rint(out[2 * (n - 1) + 1]);
+                }
+                if (!empty && !oob) {
+                    while (n > 0 && norm2(out[2 * (n - 1)] - (double)nx, out[2 * (n - 1) + 1] - (double)ny) < 1) --n;
+                    if (n < a.cap) {
+                        out[2 * n] = (double)nx;
+                        out[2 * n + 1] = (double)ny;
+                        ++n;
+                    }
                 }
             }
             status = kGdmFallback;
-            finished = true;
             break;
         }
         double sx, sy;
@@ -126,19 +200,25 @@ __global__ __launch_bounds__(64) void gdm2d_kernel(Gdm2dArgs a) {
             sx = px - tau * dx;
             sy = py - tau * dy;
         }
-        if (n >= a.cap) { status = kGdmError; finished = true; break; }
-        out[2 * n] = sx;
-        out[2 * n + 1] = sy;
+        if (n >= a.cap) { status = kGdmError; break; }
+        if (lead) {
+            out[2 * n] = sx;
+            out[2 * n + 1] = sy;
+        }
         ++n;
+        px = sx;
+        py = sy;
         if (norm2(sx - a.ex, sy - a.ey) < 1.5) break;  // :231-232
     }
-    if (status == kGdmDone && n < a.cap) {  // :234
-        out[2 * n] = a.ex;
-        out[2 * n + 1] = a.ey;
-        ++n;
+    if (lead) {
+        if (status == kGdmDone && n < a.cap) {  // :234
+            out[2 * n] = a.ex;
+            out[2 * n + 1] = a.ey;
+            ++n;
+        }
+        *a.n_out = n;
+        *a.status = status;
     }
-    *a.n_out = n;
-    *a.status = status;
 }
 
 hipError_t gdm2d(const Gdm2dArgs& a, bool f64, hipStream_t st) {
