@@ -68,7 +68,9 @@ typedef enum {
     EIK_OPT_SYNC_EVERY = 1,  /* sweep launches between active-count read-backs (default 8)     */
     EIK_OPT_TIMING = 2,      /* 1: time each sweep launch with hipEvents (for the roofline)     */
     EIK_OPT_GRID = 3,        /* workgroups per sweep launch (default 4 x CUs)                   */
-    EIK_OPT_TOL = 4          /* relative change below which a cell does not (re)activate tiles  */
+    EIK_OPT_TOL = 4,         /* relative change below which a cell does not (re)activate tiles  */
+    EIK_OPT_DELTA = 5        /* ordered mode: per launch, only tiles whose entering T is within
+                                delta of the smallest pending one are swept (0: off)           */
 } eik_option;
 
 /* ---- context: replaces MotionPlanning::initPython / shutDownPython (MotionPlanning.cpp:5-29,

@@ -19,6 +19,9 @@ struct Fim2dArgs {
     unsigned iter;         // outer iteration index of this launch
     int max_rounds;        // sweep rounds per tile visit
     float keep;            // 1 - tol: a change counts for (re)activation only if new < old * keep
+    unsigned* key;         // per tile: smallest T entering it since its last visit (f32 bits)
+    unsigned* minkey;      // [3] per list: min key of the tiles enqueued in it (f32 bits)
+    float delta;           // process a listed tile only if key <= minkey + delta (inf: always)
     unsigned long long* visits;  // tile-visit counter (stats / roofline bytes)
     unsigned* edge_dirty;  // DD: bit per subdomain side whose edge row/column changed
 };

@@ -55,6 +55,7 @@ struct eik_ctx {
     std::string err;
     int max_rounds = 1;
     double tol = 0.0;
+    double delta = 0.0;  // 0: unordered FIM
     int sync_every = 8;
     int timing = 0;
     int grid = 0;
@@ -71,7 +72,7 @@ struct eik_fim2d {
     bool f64 = false;
     Fim2dArgs a{};
     hipStream_t stream = nullptr;
-    DevBuf lists, counts, mark, visits, edge, goals;
+    DevBuf lists, counts, mark, visits, edge, goals, key;
     int* h_counts = nullptr;             // pinned
     unsigned long long* h_visits = nullptr;
     int64_t iterations = 0, host_syncs = 0, max_iters = 0;
@@ -150,6 +151,7 @@ int eik_set_option(eik_ctx* c, int opt, double v) {
         case EIK_OPT_TIMING: c->timing = v != 0; break;
         case EIK_OPT_GRID: c->grid = v > 0 ? (int)v : 4 * c->cu_count; break;
         case EIK_OPT_TOL: c->tol = v > 0 ? v : 0.0; break;
+        case EIK_OPT_DELTA: c->delta = v > 0 ? v : 0.0; break;
         default: return set_err(c, EIK_ERR_ARG, "unknown option %d", opt);
     }
     return EIK_OK;
@@ -189,6 +191,7 @@ int eik_fim2d_create(eik_ctx* c, int64_t B, int64_t H, int64_t W, int dtype, eik
     hipError_t e = hipSuccess;
     if ((e = f->lists.ensure(sizeof(int) * 3 * tiles)) != hipSuccess ||
         (e = f->counts.ensure(sizeof(int) * 64)) != hipSuccess || (e = f->mark.ensure(sizeof(unsigned) * tiles)) != hipSuccess ||
+        (e = f->key.ensure(sizeof(unsigned) * tiles)) != hipSuccess ||
         (e = f->visits.ensure(sizeof(unsigned long long))) != hipSuccess ||
         (e = f->edge.ensure(sizeof(unsigned) * 4)) != hipSuccess || (e = f->goals.ensure(sizeof(int64_t) * 2 * B)) != hipSuccess ||
         (e = hipHostMalloc((void**)&f->h_counts, sizeof(int) * 64)) != hipSuccess ||
@@ -200,6 +203,8 @@ int eik_fim2d_create(eik_ctx* c, int64_t B, int64_t H, int64_t W, int dtype, eik
     a.lists = (int*)f->lists.p;
     a.counts = (int*)f->counts.p;
     a.mark = (unsigned*)f->mark.p;
+    a.key = (unsigned*)f->key.p;
+    a.minkey = (unsigned*)f->counts.p + 16;
     a.visits = (unsigned long long*)f->visits.p;
     a.edge_dirty = nullptr;
     // safety cap: a monotone solve visits each tile a bounded number of times; negative costs
@@ -240,6 +245,7 @@ int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
     f->a.iter = 0;
     f->a.max_rounds = c->max_rounds;
     f->a.keep = (float)(1.0 - c->tol);
+    f->a.delta = c->delta > 0 ? (float)c->delta : __builtin_inff();
     f->iterations = 0;
     f->host_syncs = 0;
     f->sweep_ms = 0.0;

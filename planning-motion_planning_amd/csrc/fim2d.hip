@@ -36,7 +36,14 @@ __device__ __forceinline__ R load_T(const Fim2dArgs& a, const R* __restrict__ T,
     return INF;
 }
 
-__device__ __forceinline__ void enqueue(const Fim2dArgs& a, int tile, int list, unsigned stamp) {
+__device__ __forceinline__ void enqueue(const Fim2dArgs& a, int tile, int list, unsigned stamp, float key) {
+    if (a.delta < __builtin_inff()) {  // ordered mode only: keep the entering-T keys
+        const unsigned kb = __float_as_uint(key);  // non-negative: float order == unsigned order
+        atomicMin(&a.key[tile], kb);
+        // one shared word per list: read first, so only a new minimum pays the contended atomic
+        if (kb < __hip_atomic_load(&a.minkey[list], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            atomicMin(&a.minkey[list], kb);
+    }
     if (atomicMax(&a.mark[tile], stamp) < stamp) {
         const int pos = atomicAdd(&a.counts[list], 1);
         a.lists[(int64_t)list * a.capacity + pos] = tile;
@@ -95,6 +102,8 @@ __global__ __launch_bounds__(kThreads) void fim2d_sweep_kernel(Fim2dArgs a) {
     __shared__ R Cs[kLds * kLds];  // same layout as Ts; halo ring = +inf
     R* const Ts = Tbuf + kLds;
     __shared__ unsigned s_round, s_flags;
+    __shared__ unsigned s_key[5];  // min new value: self, N, S, W, E (f32 bits)
+    __shared__ int s_defer;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid < kLds) {
@@ -103,12 +112,28 @@ __global__ __launch_bounds__(kThreads) void fim2d_sweep_kernel(Fim2dArgs a) {
     }
     const int cur = a.iter % 3, nxt = (a.iter + 1) % 3, rst = (a.iter + 2) % 3;
     const int cnt = a.counts[cur];
-    if (blockIdx.x == 0 && tid == 0) a.counts[rst] = 0;
+    if (blockIdx.x == 0 && tid == 0) {
+        a.counts[rst] = 0;
+        a.minkey[rst] = 0x7f800000u;
+    }
     const unsigned stamp = a.iter + 2;  // "enqueued for iteration iter+1"
+    const float thr = __uint_as_float(a.minkey[cur]) + a.delta;  // ordering window of this launch
     const R keep = (R)a.keep;
 
     for (int it = blockIdx.x; it < cnt; it += gridDim.x) {
         const int tile = a.lists[(int64_t)cur * a.capacity + it];
+        if (a.delta < INF) {  // ordered mode: defer tiles whose entering T is beyond the window
+            if (tid == 0) {
+                const float k = __uint_as_float(atomicOr(&a.key[tile], 0u));
+                s_defer = k > thr;
+                if (k > thr) enqueue(a, tile, nxt, stamp, k);
+                else atomicExch(&a.key[tile], 0x7f800000u);  // entering values count afresh
+            }
+            __syncthreads();
+            const bool defer = s_defer;
+            __syncthreads();
+            if (defer) continue;  // uniform across the workgroup
+        }
         const int map = tile / a.tiles_per_map;
         const int rem = tile - map * a.tiles_per_map;
         const int ty = rem / a.ntx, tx = rem - (rem / a.ntx) * a.ntx;
@@ -121,6 +146,7 @@ __global__ __launch_bounds__(kThreads) void fim2d_sweep_kernel(Fim2dArgs a) {
             s_round = 0;
             s_flags = 0;
         }
+        if (tid < 5) s_key[tid] = 0x7f800000u;
         // ---- stage the tile: 16 cells per thread (4 rows x 4 consecutive columns)
         R told[16];
         const int cx = (tid & 15) * 4;
@@ -188,8 +214,9 @@ __global__ __launch_bounds__(kThreads) void fim2d_sweep_kernel(Fim2dArgs a) {
             if (!last_changed || round + 1 >= a.max_rounds) break;
         }
 
-        // ---- write back changed cells, collect side flags
+        // ---- write back changed cells, collect side flags and the smallest entering values
         unsigned fl = 0;
+        R kmin_self = INF, kmin[4] = {INF, INF, INF, INF};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int ry = (tid >> 4) + 16 * k;
@@ -202,6 +229,7 @@ __global__ __launch_bounds__(kThreads) void fim2d_sweep_kernel(Fim2dArgs a) {
                 const bool chg = nv[e] < told[4 * k + e];
                 any |= chg;
                 if (nv[e] < told[4 * k + e] * keep) {
+                    kmin_self = umin(kmin_self, nv[e]);
                     // A neighbour can only improve if this edge value undercuts the neighbour's
                     // adjacent cell (the halo value, stale => larger => conservative).
                     const int lx = cx + e + 1, ly = ry + 1;
@@ -211,10 +239,10 @@ __global__ __launch_bounds__(kThreads) void fim2d_sweep_kernel(Fim2dArgs a) {
                     if (cx + e == 0) fl |= 4u;
                     if (cx + e == kTile - 1) fl |= 8u;
 #else
-                    if (ry == 0 && nv[e] < Ts[lx]) fl |= 1u;                                   // north
-                    if (ry == kTile - 1 && nv[e] < Ts[(kLds - 1) * kLds + lx]) fl |= 2u;     // south
-                    if (cx + e == 0 && nv[e] < Ts[ly * kLds]) fl |= 4u;                       // west
-                    if (cx + e == kTile - 1 && nv[e] < Ts[ly * kLds + kLds - 1]) fl |= 8u;    // east
+                    if (ry == 0 && nv[e] < Ts[lx]) { fl |= 1u; kmin[0] = umin(kmin[0], nv[e]); }
+                    if (ry == kTile - 1 && nv[e] < Ts[(kLds - 1) * kLds + lx]) { fl |= 2u; kmin[1] = umin(kmin[1], nv[e]); }
+                    if (cx + e == 0 && nv[e] < Ts[ly * kLds]) { fl |= 4u; kmin[2] = umin(kmin[2], nv[e]); }
+                    if (cx + e == kTile - 1 && nv[e] < Ts[ly * kLds + kLds - 1]) { fl |= 8u; kmin[3] = umin(kmin[3], nv[e]); }
 #endif
                     const int64_t gx = x0 + cx + e;                     // subdomain edges (DD)
                     if (gy == a.H - 1 && ry != kTile - 1) fl |= 32u;
@@ -239,15 +267,20 @@ __global__ __launch_bounds__(kThreads) void fim2d_sweep_kernel(Fim2dArgs a) {
             }
         }
         if (fl) atomicOr(&s_flags, fl);
+        if (kmin_self < INF) atomicMin(&s_key[0], __float_as_uint((float)kmin_self));
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (kmin[q] < INF) atomicMin(&s_key[q + 1], __float_as_uint((float)kmin[q]));
         __syncthreads();
         if (tid < 5) {  // up to 5 enqueues, one per lane, so their atomics overlap
             const unsigned f = s_flags;
             const int base = map * a.tiles_per_map;
-            if (tid == 0 && last_changed) enqueue(a, tile, nxt, stamp);
-            if (tid == 1 && (f & 1u) && ty > 0) enqueue(a, base + rem - a.ntx, nxt, stamp);
-            if (tid == 2 && (f & 2u) && ty + 1 < a.nty) enqueue(a, base + rem + a.ntx, nxt, stamp);
-            if (tid == 3 && (f & 4u) && tx > 0) enqueue(a, base + rem - 1, nxt, stamp);
-            if (tid == 4 && (f & 8u) && tx + 1 < a.ntx) enqueue(a, base + rem + 1, nxt, stamp);
+            const float kk = __uint_as_float(s_key[tid]);
+            if (tid == 0 && last_changed) enqueue(a, tile, nxt, stamp, kk);
+            if (tid == 1 && (f & 1u) && ty > 0) enqueue(a, base + rem - a.ntx, nxt, stamp, kk);
+            if (tid == 2 && (f & 2u) && ty + 1 < a.nty) enqueue(a, base + rem + a.ntx, nxt, stamp, kk);
+            if (tid == 3 && (f & 4u) && tx > 0) enqueue(a, base + rem - 1, nxt, stamp, kk);
+            if (tid == 4 && (f & 8u) && tx + 1 < a.ntx) enqueue(a, base + rem + 1, nxt, stamp, kk);
             if (tid == 0 && a.edge_dirty) {  // subdomain edges (domain decomposition)
                 unsigned e = 0;
                 if ((f & 1u) && ty == 0) e |= 1u;
@@ -264,10 +297,15 @@ __global__ __launch_bounds__(kThreads) void fim2d_sweep_kernel(Fim2dArgs a) {
 
 // T = inf everywhere; T[goal] = 0; marks cleared.  Goals: one per map (gx < 0: none).
 template <typename R>
-__global__ void fim2d_init_kernel(R* __restrict__ T, int64_t n, unsigned* __restrict__ mark, int64_t ntiles) {
+__global__ void fim2d_init_kernel(R* __restrict__ T, int64_t n, unsigned* __restrict__ mark, int64_t ntiles,
+                                  unsigned* __restrict__ key, unsigned* __restrict__ minkey) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) T[i] = Real<R>::inf();
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ntiles; i += stride) mark[i] = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ntiles; i += stride) {
+        mark[i] = 0;
+        key[i] = 0x7f800000u;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < 3) minkey[threadIdx.x] = threadIdx.x == 0 ? 0u : 0x7f800000u;
 }
 
 template <typename R>
@@ -283,6 +321,7 @@ __global__ void fim2d_seed_kernel(Fim2dArgs a, const int64_t* __restrict__ goals
     static_cast<R*>(a.T)[(int64_t)m * a.H * a.W + gy * a.W + gx] = R(0);
     const int tile = m * a.tiles_per_map + (int)(gy / kTile) * a.ntx + (int)(gx / kTile);
     a.mark[tile] = 1;  // enqueued for iteration 0
+    a.key[tile] = 0u;  // T = 0 enters at the goal
     const int pos = atomicAdd(&a.counts[0], 1);
     a.lists[pos] = tile;
 }
@@ -305,7 +344,7 @@ __global__ void fim2d_merge_ghost_kernel(Fim2dArgs a, int side, const R* __restr
             ty = (int)(i / kTile);
             tx = side == 2 ? 0 : a.ntx - 1;
         }
-        enqueue(a, ty * a.ntx + tx, a.iter % 3, a.iter + 1);
+        enqueue(a, ty * a.ntx + tx, a.iter % 3, a.iter + 1, (float)v);
     }
 }
 
@@ -344,11 +383,11 @@ hipError_t fim2d_init(const Fim2dArgs& a, bool f64, int nmaps, const int64_t* d_
     if (e0 != hipSuccess) return e0;
     if (f64) {
         hipLaunchKernelGGL(fim2d_init_kernel<double>, dim3(grid), dim3(256), 0, st, static_cast<double*>(a.T), n,
-                           a.mark, ntiles);
+                           a.mark, ntiles, a.key, a.minkey);
         hipLaunchKernelGGL(fim2d_seed_kernel<double>, dim3((nmaps + 255) / 256), dim3(256), 0, st, a, d_goals, nmaps);
     } else {
         hipLaunchKernelGGL(fim2d_init_kernel<float>, dim3(grid), dim3(256), 0, st, static_cast<float*>(a.T), n,
-                           a.mark, ntiles);
+                           a.mark, ntiles, a.key, a.minkey);
         hipLaunchKernelGGL(fim2d_seed_kernel<float>, dim3((nmaps + 255) / 256), dim3(256), 0, st, a, d_goals, nmaps);
     }
     return hipGetLastError();
