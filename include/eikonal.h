@@ -54,7 +54,7 @@ typedef struct eik_ctx eik_ctx;
 typedef struct eik_fim2d eik_fim2d;
 
 typedef struct {
-    int64_t iterations;   /* outer FIM iterations (sweep launches) of the last solve           */
+    int64_t iterations;   /* solver launches of the last solve (list mode: outer iterations) */
     int64_t tile_visits;  /* 64x64 tile visits of the last solve                                */
     int64_t host_syncs;   /* active-count read-backs                                            */
     double solve_ms;      /* device time of the last solve (hipEvents, init..converged)         */
@@ -69,9 +69,18 @@ typedef enum {
     EIK_OPT_TIMING = 2,      /* 1: time each sweep launch with hipEvents (for the roofline)     */
     EIK_OPT_GRID = 3,        /* workgroups per sweep launch (default 4 x CUs)                   */
     EIK_OPT_TOL = 4,         /* relative change below which a cell does not (re)activate tiles  */
-    EIK_OPT_DELTA = 5        /* ordered mode: per launch, only tiles whose entering T is within
-                                delta of the smallest pending one are swept (0: off)           */
+    EIK_OPT_DELTA = 5,       /* ordered mode: per launch, only tiles whose entering T is within
+                                delta of the smallest pending one are swept (0: off; > 0 forces
+                                EIK_MODE_LIST)                                                  */
+    EIK_OPT_MODE = 6,        /* EIK_MODE_PERSISTENT (default): one launch per solve over a device
+                                FIFO of tiles; EIK_MODE_LIST: one launch per outer iteration   */
+    EIK_OPT_QTIMEOUT = 7,    /* persistent mode: seconds a workgroup may wait on the FIFO before
+                                the solve fails with EIK_ERR_HIP instead of hanging (default 30) */
+    EIK_OPT_MAX_VISITS = 8   /* persistent mode: tile visits after which a solve fails with
+                                EIK_ERR_NOCONVERGE (0: default 1024 x tiles + 2^20)            */
 } eik_option;
+
+typedef enum { EIK_MODE_LIST = 0, EIK_MODE_PERSISTENT = 1 } eik_mode;
 
 /* ---- context: replaces MotionPlanning::initPython / shutDownPython (MotionPlanning.cpp:5-29,
  *      :93-100) as the owner of solver state; one per host thread -------------------------- */

@@ -24,10 +24,25 @@ struct Fim2dArgs {
     float delta;           // process a listed tile only if key <= minkey + delta (inf: always)
     unsigned long long* visits;  // tile-visit counter (stats / roofline bytes)
     unsigned* edge_dirty;  // DD: bit per subdomain side whose edge row/column changed
+    // persistent mode (one launch per solve, device FIFO of tiles)
+    int mode;              // kModeList / kModePersistent
+    unsigned long long* qhead;  // ticket counter (consumers)      -- qctl + 0
+    unsigned long long* qtail;  // append counter (producers)      -- qctl + 64
+    int* qactive;          // tiles pending or busy               -- qctl + 128
+    unsigned* qerror;      // nonzero: a spin timed out           -- qctl + 192
+    unsigned* qslot;       // [qmask + 1] FIFO slots: tile + 1, 0 = empty
+    unsigned qmask;        // power of two >= tiles, minus one
+    unsigned* qstate;      // per tile: kPending | kBusy
+    unsigned long long qtimeout;  // spin limit, s_memrealtime ticks (100 MHz)
+    unsigned long long qbudget;   // tile-visit cap (negative costs never converge)
 };
+constexpr int kModeList = 0, kModePersistent = 1;
+constexpr size_t kQueueCtlBytes = 256;
 
 hipError_t fim2d_init(const Fim2dArgs& a, bool f64, int nmaps, const int64_t* d_goals, hipStream_t st);
 hipError_t fim2d_sweep(const Fim2dArgs& a, bool f64, int grid, hipStream_t st);
+hipError_t fim2d_persist(const Fim2dArgs& a, bool f64, int grid, hipStream_t st);
+int fim2d_persist_resident(bool f64, int cus);
 hipError_t fim2d_merge_ghost(const Fim2dArgs& a, bool f64, int side, const void* recv, int64_t len, hipStream_t st);
 hipError_t fim2d_pack_edges(const Fim2dArgs& a, bool f64, void* n, void* s, void* w, void* e, hipStream_t st);
 

@@ -57,6 +57,9 @@ struct eik_ctx {
     double tol = 0.0;
     double delta = 0.0;  // 0: unordered FIM
     int sync_every = 8;
+    int mode = kModePersistent;  // EIK_OPT_MODE
+    double qtimeout_s = 30.0;    // EIK_OPT_QTIMEOUT: persistent-mode spin limit
+    unsigned long long max_visits = 0;  // EIK_OPT_MAX_VISITS (0: per-solver default)
     int timing = 0;
     int grid = 0;
     eik_stats last{};
@@ -73,7 +76,9 @@ struct eik_fim2d {
     Fim2dArgs a{};
     hipStream_t stream = nullptr;
     DevBuf lists, counts, mark, visits, edge, goals, key;
+    DevBuf qctl, qslot, qstate;          // persistent-mode FIFO
     int* h_counts = nullptr;             // pinned
+    unsigned* h_q = nullptr;             // pinned copy of qctl
     unsigned long long* h_visits = nullptr;
     int64_t iterations = 0, host_syncs = 0, max_iters = 0;
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
@@ -81,6 +86,7 @@ struct eik_fim2d {
     size_t ev_used = 0;
     double sweep_ms = 0.0, solve_ms = 0.0;
     bool started = false;
+    int persist_grid = 0;                // co-resident workgroups of the persistent kernel
 };
 
 static int set_err(eik_ctx* c, int code, const char* fmt, ...) {
@@ -152,6 +158,12 @@ int eik_set_option(eik_ctx* c, int opt, double v) {
         case EIK_OPT_GRID: c->grid = v > 0 ? (int)v : 4 * c->cu_count; break;
         case EIK_OPT_TOL: c->tol = v > 0 ? v : 0.0; break;
         case EIK_OPT_DELTA: c->delta = v > 0 ? v : 0.0; break;
+        case EIK_OPT_MODE:
+            if (v != EIK_MODE_LIST && v != EIK_MODE_PERSISTENT) return set_err(c, EIK_ERR_ARG, "bad mode %g", v);
+            c->mode = (int)v;
+            break;
+        case EIK_OPT_QTIMEOUT: c->qtimeout_s = v > 0 ? v : 30.0; break;
+        case EIK_OPT_MAX_VISITS: c->max_visits = v > 0 ? (unsigned long long)v : 0ull; break;
         default: return set_err(c, EIK_ERR_ARG, "unknown option %d", opt);
     }
     return EIK_OK;
@@ -188,8 +200,15 @@ int eik_fim2d_create(eik_ctx* c, int64_t B, int64_t H, int64_t W, int dtype, eik
     a.tiles_per_map = (int)(ntx * nty);
     a.capacity = (int)tiles;
     for (auto& g : a.ghost) g = nullptr;
+    // FIFO slots: a power of two with ample headroom over the tiles (each tile holds at most one
+    // filled slot; the margin keeps a slow poller's slot from being lapped by the tail)
+    uint64_t q = 4096;
+    while (q < 8 * (uint64_t)tiles) q <<= 1;
     hipError_t e = hipSuccess;
     if ((e = f->lists.ensure(sizeof(int) * 3 * tiles)) != hipSuccess ||
+        (e = f->qctl.ensure(kQueueCtlBytes)) != hipSuccess || (e = f->qslot.ensure(sizeof(unsigned) * q)) != hipSuccess ||
+        (e = f->qstate.ensure(sizeof(unsigned) * tiles)) != hipSuccess ||
+        (e = hipHostMalloc((void**)&f->h_q, kQueueCtlBytes)) != hipSuccess ||
         (e = f->counts.ensure(sizeof(int) * 64)) != hipSuccess || (e = f->mark.ensure(sizeof(unsigned) * tiles)) != hipSuccess ||
         (e = f->key.ensure(sizeof(unsigned) * tiles)) != hipSuccess ||
         (e = f->visits.ensure(sizeof(unsigned long long))) != hipSuccess ||
@@ -207,6 +226,13 @@ int eik_fim2d_create(eik_ctx* c, int64_t B, int64_t H, int64_t W, int dtype, eik
     a.minkey = (unsigned*)f->counts.p + 16;
     a.visits = (unsigned long long*)f->visits.p;
     a.edge_dirty = nullptr;
+    a.qhead = (unsigned long long*)f->qctl.p;
+    a.qtail = (unsigned long long*)((char*)f->qctl.p + 64);
+    a.qactive = (int*)((char*)f->qctl.p + 128);
+    a.qerror = (unsigned*)((char*)f->qctl.p + 192);
+    a.qslot = (unsigned*)f->qslot.p;
+    a.qmask = (unsigned)(q - 1);
+    a.qstate = (unsigned*)f->qstate.p;
     // safety cap: a monotone solve visits each tile a bounded number of times; negative costs
     // (invalid input on a device buffer) would otherwise iterate forever.
     f->max_iters = 64 * (ntx + nty) + 8 * tiles / B + 4096;
@@ -218,6 +244,7 @@ void eik_fim2d_destroy(eik_fim2d* f) {
     if (!f) return;
     if (f->h_counts) (void)hipHostFree(f->h_counts);
     if (f->h_visits) (void)hipHostFree(f->h_visits);
+    if (f->h_q) (void)hipHostFree(f->h_q);
     if (f->ev_start) (void)hipEventDestroy(f->ev_start);
     if (f->ev_stop) (void)hipEventDestroy(f->ev_stop);
     for (auto ev : f->ev_pool) (void)hipEventDestroy(ev);
@@ -246,6 +273,11 @@ int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
     f->a.max_rounds = c->max_rounds;
     f->a.keep = (float)(1.0 - c->tol);
     f->a.delta = c->delta > 0 ? (float)c->delta : __builtin_inff();
+    // persistent mode needs 32-bit byte offsets per map (buffer resources) and no ordering window
+    const bool fits = f->H * f->W * (f->f64 ? 8 : 4) < (int64_t)UINT32_MAX;
+    f->a.mode = (c->mode == kModePersistent && fits && !(c->delta > 0)) ? kModePersistent : kModeList;
+    f->a.qtimeout = (unsigned long long)(c->qtimeout_s * 1e8);  // s_memrealtime: 100 MHz
+    f->a.qbudget = c->max_visits ? c->max_visits : 1024ull * (unsigned long long)(f->B * f->a.tiles_per_map) + (1ull << 20);
     f->iterations = 0;
     f->host_syncs = 0;
     f->sweep_ms = 0.0;
@@ -277,6 +309,37 @@ int eik_fim2d_iterate(eik_fim2d* f, int64_t max_iters, int64_t* active) {
     int64_t done = 0;
     int h = 1;
     const int grid = c->grid > 0 ? c->grid : 4 * c->cu_count;
+    if (f->a.mode == kModePersistent) {  // one launch runs the local solve to its fixed point
+        if (max_iters < 1) {
+            if (active) *active = -1;
+            return EIK_OK;
+        }
+        if (c->timing) {
+            while (f->ev_pool.size() < f->ev_used + 2) {
+                hipEvent_t ev;
+                HIPCHK(c, hipEventCreate(&ev));
+                f->ev_pool.push_back(ev);
+            }
+            HIPCHK(c, hipEventRecord(f->ev_pool[f->ev_used++], f->stream));
+        }
+        if (f->persist_grid == 0) f->persist_grid = fim2d_persist_resident(f->f64, c->cu_count);
+        HIPCHK(c, fim2d_persist(f->a, f->f64, std::min(grid, f->persist_grid), f->stream));
+        if (c->timing) HIPCHK(c, hipEventRecord(f->ev_pool[f->ev_used++], f->stream));
+        ++f->iterations;
+        HIPCHK(c, hipMemcpyAsync(f->h_q, f->qctl.p, kQueueCtlBytes, hipMemcpyDeviceToHost, f->stream));
+        HIPCHK(c, hipStreamSynchronize(f->stream));
+        ++f->host_syncs;
+        if (c->timing) drain_timing(f);
+        const unsigned err = f->h_q[192 / 4];
+        if (err & 1u)
+            return set_err(c, EIK_ERR_HIP, "persistent solver: a queue wait exceeded %.1f s (EIK_OPT_QTIMEOUT)",
+                           c->qtimeout_s);
+        if (err & 2u)
+            return set_err(c, EIK_ERR_NOCONVERGE, "no convergence within %llu tile visits (negative costs?)",
+                           (unsigned long long)f->a.qbudget);
+        if (active) *active = f->h_q[128 / 4];
+        return EIK_OK;
+    }
     while (done < max_iters) {
         const int64_t K = std::min<int64_t>(c->sync_every, max_iters - done);
         for (int64_t k = 0; k < K; ++k) {
@@ -309,6 +372,12 @@ int eik_fim2d_iterate(eik_fim2d* f, int64_t max_iters, int64_t* active) {
 int eik_fim2d_active(eik_fim2d* f, int64_t* active) {
     if (!f || !active) return EIK_ERR_ARG;
     eik_ctx* c = f->ctx;
+    if (f->a.mode == kModePersistent) {
+        HIPCHK(c, hipMemcpyAsync(f->h_q, f->qctl.p, kQueueCtlBytes, hipMemcpyDeviceToHost, f->stream));
+        HIPCHK(c, hipStreamSynchronize(f->stream));
+        *active = f->h_q[128 / 4];
+        return EIK_OK;
+    }
     HIPCHK(c, hipMemcpyAsync(f->h_counts, (int*)f->counts.p + (f->iterations % 3), sizeof(int), hipMemcpyDeviceToHost,
                              f->stream));
     HIPCHK(c, hipStreamSynchronize(f->stream));

@@ -5,30 +5,136 @@
 // same discrete Godunov solution (the reference FMM equals the
 // Jacobi fixed point to 1e-13):
 //
-//  * the raster is cut into 64x64 tiles; an ACTIVE LIST of tiles is kept on the device;
-//  * one workgroup (4 x wave64) per active tile stages cost + T (+1-cell halo) in LDS and runs
-//    ONE round of four concurrent quadrant sweeps (one per wave).  Each sweep is Gauss-Seidel
-//    along skewed anti-diagonals (lane l = column, step s = row s-l), so the upstream x value
-//    comes from lane l-1 through a DPP wave shift and the upstream y value from the lane's own
-//    previous step: one round propagates any characteristic in that quadrant across the tile;
-//  * updates are monotone min-updates (T = min(T, godunov(...))) merged with ds_min, so the
-//    racing waves and the stale halos of concurrently processed tiles are all benign;
-//  * a tile whose values changed re-enqueues itself; a tile whose boundary row/column changed
-//    enqueues that neighbour (dedup by a per-tile mark, appended with one atomic per tile);
-//  * the host runs outer iterations (one launch each) until the list is empty.
+//  * the raster is cut into 64x64 tiles; one workgroup (4 x wave64) per tile visit stages
+//    cost + T (+1-cell halo) in LDS and runs four concurrent quadrant sweeps (one per wave).
+//    Each sweep is Gauss-Seidel along skewed anti-diagonals (lane l = column, step s = row
+//    s-l): the upstream x value comes from lane l-1 through a DPP wave shift, the upstream y
+//    value from the lane's own previous step, so one round propagates any characteristic in
+//    that quadrant across the tile;
+//  * updates are monotone min-updates merged with ds_min, so racing waves and stale halos of
+//    concurrently processed tiles only delay convergence;
+//  * a tile whose values changed is revisited; a tile whose edge values undercut a neighbour's
+//    adjacent cell activates that neighbour.
 //
-// The same kernel serves B independent maps (tile id = map * tiles_per_map + tile) and a
-// subdomain of a domain-decomposed raster (ghost strips N/S/W/E read in place of the
-// out-of-range neighbours; edge-row changes are flagged for the halo exchange).
+// Two drivers share the tile body:
+//  * LIST mode (fim2d_sweep_kernel): one launch per outer iteration over a device-side active
+//    list (triple-buffered, dedup by per-tile marks); kernel boundaries order all memory.
+//  * PERSISTENT mode (fim2d_persist_kernel): ONE launch per solve.  Workgroups take tickets
+//    from a device FIFO of tiles and process a tile as soon as it is activated -- no launch
+//    gaps, no waiting for the slowest tile of an iteration.  Hand-offs follow the gfx950 recipe
+//    for in-launch visibility (cdna_hip_programming.md Guideline 16, with sc1 loads): every
+//    T store is write-through (sc1) and drained (s_waitcnt vmcnt(0) in every storing wave,
+//    then a workgroup barrier) before the activating atomics; every T load is an sc1 load.
+//    A per-tile state word (PENDING / BUSY) deduplicates the queue and defers activations of a
+//    busy tile to its finish; a counter of non-idle tiles detects termination; every spin is
+//    bounded by a wall-clock timeout that raises an error flag instead of hanging.
+//
+// The same kernels serve B independent maps (tile id = map * tiles_per_map + tile) and a
+// subdomain of a domain-decomposed raster (ghost strips N/S/W/E stand in for out-of-range
+// neighbours; edge activations are flagged for the halo exchange).
 #include "eik_common.hpp"
 #include "eik_kernels.hpp"
 
 namespace eik {
 
+constexpr unsigned kPending = 1u, kBusy = 2u;
+
+// ------------------------------------------------------------------- memory access policy
+// Plain accesses (LIST mode) or coherent sc1 buffer accesses (PERSISTENT mode).
+template <typename R, bool COH>
+struct TMem;
+
 template <typename R>
-__device__ __forceinline__ R load_T(const Fim2dArgs& a, const R* __restrict__ T, int64_t gy, int64_t gx) {
+struct TMem<R, false> {
+    R* p;
+    __device__ TMem(R* base, int64_t) : p(base) {}
+    __device__ R ld(int64_t i) const { return p[i]; }
+    __device__ void ld4(int64_t i, R (&v)[4]) const {
+        if constexpr (sizeof(R) == 4) {
+            const float4 t = *reinterpret_cast<const float4*>(p + i);
+            v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+        } else {
+            const double2 t0 = *reinterpret_cast<const double2*>(p + i);
+            const double2 t1 = *reinterpret_cast<const double2*>(p + i + 2);
+            v[0] = t0.x; v[1] = t0.y; v[2] = t1.x; v[3] = t1.y;
+        }
+    }
+    __device__ void st(int64_t i, R v) const { p[i] = v; }
+    __device__ void st4(int64_t i, const R (&v)[4]) const {
+        if constexpr (sizeof(R) == 4) {
+            *reinterpret_cast<float4*>(p + i) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+            *reinterpret_cast<double2*>(p + i) = make_double2(v[0], v[1]);
+            *reinterpret_cast<double2*>(p + i + 2) = make_double2(v[2], v[3]);
+        }
+    }
+};
+
+constexpr int kSC1 = 16;  // aux cache-policy bits of the raw buffer builtins: sc1 (agent coherence)
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+template <typename R>
+struct TMem<R, true> {
+    __amdgpu_buffer_rsrc_t rs;
+    // n * sizeof(R) < 2^32 is checked by the host before it selects this mode
+    __device__ TMem(R* base, int64_t n)
+        : rs(__builtin_amdgcn_make_buffer_rsrc(base, 0, (int)(uint32_t)(n * (int64_t)sizeof(R)), 0x00020000)) {}
+    __device__ R ld(int64_t i) const {
+        const unsigned off = (unsigned)(i * (int64_t)sizeof(R));
+        if constexpr (sizeof(R) == 4) {
+            return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, kSC1));
+        } else {
+            const u32x2 u = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, kSC1);
+            return __longlong_as_double((long long)(((unsigned long long)u[1] << 32) | u[0]));
+        }
+    }
+    __device__ void ld4(int64_t i, R (&v)[4]) const {
+        const unsigned off = (unsigned)(i * (int64_t)sizeof(R));
+        if constexpr (sizeof(R) == 4) {
+            const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, kSC1);
+            v[0] = __uint_as_float(u[0]); v[1] = __uint_as_float(u[1]);
+            v[2] = __uint_as_float(u[2]); v[3] = __uint_as_float(u[3]);
+        } else {
+            const u32x4 u0 = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, kSC1);
+            const u32x4 u1 = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, kSC1);
+            v[0] = __longlong_as_double((long long)(((unsigned long long)u0[1] << 32) | u0[0]));
+            v[1] = __longlong_as_double((long long)(((unsigned long long)u0[3] << 32) | u0[2]));
+            v[2] = __longlong_as_double((long long)(((unsigned long long)u1[1] << 32) | u1[0]));
+            v[3] = __longlong_as_double((long long)(((unsigned long long)u1[3] << 32) | u1[2]));
+        }
+    }
+    __device__ void st(int64_t i, R v) const {
+        const unsigned off = (unsigned)(i * (int64_t)sizeof(R));
+        if constexpr (sizeof(R) == 4) {
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, off, 0, kSC1);
+        } else {
+            const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+            const u32x2 u = {(unsigned)b, (unsigned)(b >> 32)};
+            __builtin_amdgcn_raw_buffer_store_b64(u, rs, off, 0, kSC1);
+        }
+    }
+    __device__ void st4(int64_t i, const R (&v)[4]) const {
+        const unsigned off = (unsigned)(i * (int64_t)sizeof(R));
+        if constexpr (sizeof(R) == 4) {
+            const u32x4 u = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+            __builtin_amdgcn_raw_buffer_store_b128(u, rs, off, 0, kSC1);
+        } else {
+            unsigned long long b[4];
+            for (int k = 0; k < 4; ++k) b[k] = (unsigned long long)__double_as_longlong(v[k]);
+            const u32x4 u0 = {(unsigned)b[0], (unsigned)(b[0] >> 32), (unsigned)b[1], (unsigned)(b[1] >> 32)};
+            const u32x4 u1 = {(unsigned)b[2], (unsigned)(b[2] >> 32), (unsigned)b[3], (unsigned)(b[3] >> 32)};
+            __builtin_amdgcn_raw_buffer_store_b128(u0, rs, off, 0, kSC1);
+            __builtin_amdgcn_raw_buffer_store_b128(u1, rs, off + 16, 0, kSC1);
+        }
+    }
+};
+
+template <typename R, bool COH>
+__device__ __forceinline__ R load_T(const Fim2dArgs& a, const TMem<R, COH>& T, int64_t gy, int64_t gx) {
     constexpr R INF = Real<R>::inf();
-    if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) return T[gy * a.W + gx];
+    if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) return T.ld(gy * a.W + gx);
+    // ghost strips only change between launches (merge kernel): plain loads
     if (gy == -1 && gx >= 0 && gx < a.W) return a.ghost[0] ? static_cast<const R*>(a.ghost[0])[gx] : INF;
     if (gy == a.H && gx >= 0 && gx < a.W) return a.ghost[1] ? static_cast<const R*>(a.ghost[1])[gx] : INF;
     if (gx == -1 && gy >= 0 && gy < a.H) return a.ghost[2] ? static_cast<const R*>(a.ghost[2])[gy] : INF;
@@ -36,6 +142,8 @@ __device__ __forceinline__ R load_T(const Fim2dArgs& a, const R* __restrict__ T,
     return INF;
 }
 
+// -------------------------------------------------------------------- activation helpers
+// LIST mode: append to the next iteration's list (dedup by mark).
 __device__ __forceinline__ void enqueue(const Fim2dArgs& a, int tile, int list, unsigned stamp, float key) {
     if (a.delta < __builtin_inff()) {  // ordered mode only: keep the entering-T keys
         const unsigned kb = __float_as_uint(key);  // non-negative: float order == unsigned order
@@ -50,6 +158,27 @@ __device__ __forceinline__ void enqueue(const Fim2dArgs& a, int tile, int list, 
     }
 }
 
+// PERSISTENT mode: append to the FIFO unless the tile is already pending (nothing to do) or
+// busy (its processor re-queues it when it finishes).
+__device__ __forceinline__ void qslot_put(const Fim2dArgs& a, int tile) {
+    const unsigned long long pos = atomicAdd(a.qtail, 1ull);
+    __hip_atomic_store(&a.qslot[pos & a.qmask], (unsigned)tile + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void qpush(const Fim2dArgs& a, int tile) {
+    if (atomicOr(&a.qstate[tile], kPending) == 0u) {
+        atomicAdd(a.qactive, 1);  // before the slot store: a waiter never sees "empty and idle"
+        qslot_put(a, tile);
+    }
+}
+
+__device__ __forceinline__ void activate(const Fim2dArgs& a, int tile, int list, unsigned stamp, float key) {
+    if (a.mode == kModePersistent)
+        qpush(a, tile);
+    else
+        enqueue(a, tile, list, stamp, key);
+}
+
+// ------------------------------------------------------------------------- quadrant sweep
 // One quadrant sweep of the staged tile.  DX/DY = +-1: direction of propagation.
 // Lane l owns column x; at step s it updates row r = s - l (skewed Gauss-Seidel), so its
 // upstream x neighbour is lane l-1's previous result (DPP) and its upstream y neighbour its own.
@@ -93,23 +222,208 @@ __device__ __forceinline__ bool sweep_quadrant(R* __restrict__ Ts, const R* __re
     return changed;
 }
 
+// LDS of one tile visit
+template <typename R>
+struct TileLds {
+    // Tbuf: tile + halo ring (66 x 66 at offset kLds), plus one guard row above and below (the
+    // clamped r = -1 / 64 steps read one row beyond the halo: in-bounds, +inf, and masked by the
+    // +inf halo cost anyway)
+    R Tbuf[(kLds + 2) * kLds];
+    R Cs[kLds * kLds];  // same layout as Ts; halo ring = +inf
+    unsigned round, flags;
+    unsigned key[5];    // min new value entering: self, N, S, W, E (f32 bits; ordered mode)
+    int defer, tile, last;
+};
+
+// ---------------------------------------------------------------------------- tile body
+// Stage, sweep and write back one tile; leaves the activation decisions in L.flags (bits 0..3:
+// neighbour N/S/W/E can improve; 32/64: changed subdomain S/E edge inside a partial tile),
+// L.last (the last round changed something) and L.key.  Ends with a workgroup barrier; in
+// COH mode every wave has drained its write-through stores before it.
+template <typename R, bool COH>
+__device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileLds<R>& L, R keep) {
+    constexpr R INF = Real<R>::inf();
+    R* const Ts = L.Tbuf + kLds;
+    R* const Cs = L.Cs;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int map = tile / a.tiles_per_map;
+    const int rem = tile - map * a.tiles_per_map;
+    const int ty = rem / a.ntx, tx = rem - (rem / a.ntx) * a.ntx;
+    const R* __restrict__ cost = static_cast<const R*>(a.cost) + (int64_t)map * a.H * a.W;
+    const TMem<R, COH> T(static_cast<R*>(a.T) + (int64_t)map * a.H * a.W, a.H * a.W);
+    const int64_t y0 = (int64_t)ty * kTile, x0 = (int64_t)tx * kTile;
+    const bool full = (y0 + kTile <= a.H) && (x0 + kTile <= a.W) && ((a.W & 3) == 0);
+
+    if (tid == 0) {
+        L.round = 0;
+        L.flags = 0;
+    }
+    if (tid < 5) L.key[tid] = 0x7f800000u;
+    // ---- stage the tile: 16 cells per thread (4 rows x 4 consecutive columns)
+    R told[16];
+    const int cx = (tid & 15) * 4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int ry = (tid >> 4) + 16 * k;
+        const int64_t gy = y0 + ry;
+        R tv[4];
+        R* cr = &Cs[(ry + 1) * kLds + cx + 1];
+        if (full) {
+            T.ld4(gy * a.W + x0 + cx, tv);
+            if constexpr (sizeof(R) == 4) {
+                const float4 c4 = *reinterpret_cast<const float4*>(&cost[gy * a.W + x0 + cx]);
+                cr[0] = c4.x; cr[1] = c4.y; cr[2] = c4.z; cr[3] = c4.w;
+            } else {
+                const double2 c0 = *reinterpret_cast<const double2*>(&cost[gy * a.W + x0 + cx]);
+                const double2 c1 = *reinterpret_cast<const double2*>(&cost[gy * a.W + x0 + cx + 2]);
+                cr[0] = c0.x; cr[1] = c0.y; cr[2] = c1.x; cr[3] = c1.y;
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int64_t gx = x0 + cx + e;
+                const bool in = gy < a.H && gx < a.W;
+                tv[e] = load_T<R, COH>(a, T, gy, gx);  // ghost cells land in padding
+                cr[e] = in ? cost[gy * a.W + gx] : INF;
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            told[4 * k + e] = tv[e];
+            Ts[(ry + 1) * kLds + cx + e + 1] = tv[e];
+        }
+    }
+    // halo ring: wave 0 north row, 1 south row, 2 west column, 3 east column
+    {
+        R v;
+        if (wave == 0)      v = load_T<R, COH>(a, T, y0 - 1, x0 + lane);
+        else if (wave == 1) v = load_T<R, COH>(a, T, y0 + kTile, x0 + lane);
+        else if (wave == 2) v = load_T<R, COH>(a, T, y0 + lane, x0 - 1);
+        else                v = load_T<R, COH>(a, T, y0 + lane, x0 + kTile);
+        int h;
+        if (wave == 0)      h = 0 * kLds + lane + 1;
+        else if (wave == 1) h = (kLds - 1) * kLds + lane + 1;
+        else if (wave == 2) h = (lane + 1) * kLds + 0;
+        else                h = (lane + 1) * kLds + kLds - 1;
+        Ts[h] = v;
+        Cs[h] = INF;
+        if (lane < 4) Cs[(lane >> 1) * (kLds - 1) * kLds + (lane & 1) * (kLds - 1)] = INF;  // corners
+    }
+    __syncthreads();
+
+    // ---- sweep rounds (4 quadrant directions concurrently, one per wave)
+    bool last_changed = false;
+    for (int round = 0;; ++round) {
+        bool ch;
+        if (wave == 0)      ch = sweep_quadrant<R, +1, +1>(Ts, Cs, lane, keep);
+        else if (wave == 1) ch = sweep_quadrant<R, -1, +1>(Ts, Cs, lane, keep);
+        else if (wave == 2) ch = sweep_quadrant<R, +1, -1>(Ts, Cs, lane, keep);
+        else                ch = sweep_quadrant<R, -1, -1>(Ts, Cs, lane, keep);
+        if (__any(ch) && lane == 0) atomicOr(&L.round, 1u << (round & 31));
+        __syncthreads();
+        last_changed = (L.round >> (round & 31)) & 1u;
+        if (!last_changed || round + 1 >= a.max_rounds) break;
+    }
+
+    // ---- write back changed cells, collect side flags (and entering values, ordered mode)
+    unsigned fl = 0;
+    R kmin_self = INF, kmin[4] = {INF, INF, INF, INF};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int ry = (tid >> 4) + 16 * k;
+        const int64_t gy = y0 + ry;
+        R nv[4];
+        bool any = false;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            nv[e] = Ts[(ry + 1) * kLds + cx + e + 1];
+            any |= nv[e] < told[4 * k + e];
+            if (nv[e] < told[4 * k + e] * keep) {
+                kmin_self = umin(kmin_self, nv[e]);
+                // A neighbour can only improve if this edge value undercuts the neighbour's
+                // adjacent cell (the halo value, stale => larger => conservative).
+                const int lx = cx + e + 1, ly = ry + 1;
+                if (ry == 0 && nv[e] < Ts[lx]) { fl |= 1u; kmin[0] = umin(kmin[0], nv[e]); }
+                if (ry == kTile - 1 && nv[e] < Ts[(kLds - 1) * kLds + lx]) { fl |= 2u; kmin[1] = umin(kmin[1], nv[e]); }
+                if (cx + e == 0 && nv[e] < Ts[ly * kLds]) { fl |= 4u; kmin[2] = umin(kmin[2], nv[e]); }
+                if (cx + e == kTile - 1 && nv[e] < Ts[ly * kLds + kLds - 1]) { fl |= 8u; kmin[3] = umin(kmin[3], nv[e]); }
+                const int64_t gx = x0 + cx + e;  // subdomain edges inside a partial tile (DD)
+                if (gy == a.H - 1 && ry != kTile - 1) fl |= 32u;
+                if (gx == a.W - 1 && cx + e != kTile - 1) fl |= 64u;
+            }
+        }
+        if (any) {
+            if (full) {
+                T.st4(gy * a.W + x0 + cx, nv);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int64_t gx = x0 + cx + e;
+                    if (gy < a.H && gx < a.W && nv[e] < told[4 * k + e]) T.st(gy * a.W + gx, nv[e]);
+                }
+            }
+        }
+    }
+    if (fl) atomicOr(&L.flags, fl);
+    if (a.delta < INF) {
+        if (kmin_self < INF) atomicMin(&L.key[0], __float_as_uint((float)kmin_self));
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (kmin[q] < INF) atomicMin(&L.key[q + 1], __float_as_uint((float)kmin[q]));
+    }
+    if (tid == 0) L.last = last_changed;
+    if constexpr (COH) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+    __syncthreads();
+}
+
+// Activations after a tile visit: thread q < 5 handles one candidate (their atomics overlap).
+template <typename R>
+__device__ __forceinline__ void activate_after(const Fim2dArgs& a, int tile, const TileLds<R>& L, int list,
+                                               unsigned stamp) {
+    const int tid = threadIdx.x;
+    if (tid >= 5) return;
+    const unsigned f = L.flags;
+    const int map = tile / a.tiles_per_map;
+    const int rem = tile - map * a.tiles_per_map;
+    const int ty = rem / a.ntx, tx = rem - (rem / a.ntx) * a.ntx;
+    const int base = map * a.tiles_per_map;
+    const float kk = __uint_as_float(L.key[tid]);
+    if (tid == 0 && L.last) {
+        if (a.mode == kModePersistent)
+            atomicOr(&a.qstate[tile], kPending);  // busy: re-queued by its own finish
+        else
+            enqueue(a, tile, list, stamp, kk);
+    }
+    if (tid == 1 && (f & 1u) && ty > 0) activate(a, base + rem - a.ntx, list, stamp, kk);
+    if (tid == 2 && (f & 2u) && ty + 1 < a.nty) activate(a, base + rem + a.ntx, list, stamp, kk);
+    if (tid == 3 && (f & 4u) && tx > 0) activate(a, base + rem - 1, list, stamp, kk);
+    if (tid == 4 && (f & 8u) && tx + 1 < a.ntx) activate(a, base + rem + 1, list, stamp, kk);
+    if (tid == 0 && a.edge_dirty) {  // subdomain edges (domain decomposition)
+        unsigned e = 0;
+        if ((f & 1u) && ty == 0) e |= 1u;
+        if (((f & 2u) || (f & 32u)) && ty + 1 == a.nty) e |= 2u;
+        if ((f & 4u) && tx == 0) e |= 4u;
+        if (((f & 8u) || (f & 64u)) && tx + 1 == a.ntx) e |= 8u;
+        if (e) atomicOr(a.edge_dirty, e);
+    }
+}
+
+template <typename R>
+__device__ __forceinline__ void init_guard_rows(TileLds<R>& L) {
+    const int tid = threadIdx.x;
+    if (tid < kLds) {
+        L.Tbuf[tid] = Real<R>::inf();
+        L.Tbuf[(kLds + 1) * kLds + tid] = Real<R>::inf();
+    }
+}
+
+// ------------------------------------------------------------------------ LIST-mode driver
 template <typename R>
 __global__ __launch_bounds__(kThreads) void fim2d_sweep_kernel(Fim2dArgs a) {
     constexpr R INF = Real<R>::inf();
-    // Ts: tile + halo ring, plus one guard row above and below (the clamped r = -1 / 64 steps
-    // read one row beyond the halo: in-bounds, +inf, and masked by the +inf halo cost anyway)
-    __shared__ R Tbuf[(kLds + 2) * kLds];
-    __shared__ R Cs[kLds * kLds];  // same layout as Ts; halo ring = +inf
-    R* const Ts = Tbuf + kLds;
-    __shared__ unsigned s_round, s_flags;
-    __shared__ unsigned s_key[5];  // min new value: self, N, S, W, E (f32 bits)
-    __shared__ int s_defer;
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid < kLds) {
-        Tbuf[tid] = INF;
-        Tbuf[(kLds + 1) * kLds + tid] = INF;
-    }
+    __shared__ TileLds<R> L;
+    const int tid = threadIdx.x;
+    init_guard_rows(L);
     const int cur = a.iter % 3, nxt = (a.iter + 1) % 3, rst = (a.iter + 2) % 3;
     const int cnt = a.counts[cur];
     if (blockIdx.x == 0 && tid == 0) {
@@ -125,189 +439,106 @@ __global__ __launch_bounds__(kThreads) void fim2d_sweep_kernel(Fim2dArgs a) {
         if (a.delta < INF) {  // ordered mode: defer tiles whose entering T is beyond the window
             if (tid == 0) {
                 const float k = __uint_as_float(atomicOr(&a.key[tile], 0u));
-                s_defer = k > thr;
+                L.defer = k > thr;
                 if (k > thr) enqueue(a, tile, nxt, stamp, k);
                 else atomicExch(&a.key[tile], 0x7f800000u);  // entering values count afresh
             }
             __syncthreads();
-            const bool defer = s_defer;
+            const bool defer = L.defer;
             __syncthreads();
             if (defer) continue;  // uniform across the workgroup
         }
-        const int map = tile / a.tiles_per_map;
-        const int rem = tile - map * a.tiles_per_map;
-        const int ty = rem / a.ntx, tx = rem - (rem / a.ntx) * a.ntx;
-        const R* __restrict__ cost = static_cast<const R*>(a.cost) + (int64_t)map * a.H * a.W;
-        R* __restrict__ T = static_cast<R*>(a.T) + (int64_t)map * a.H * a.W;
-        const int64_t y0 = (int64_t)ty * kTile, x0 = (int64_t)tx * kTile;
-        const bool full = (y0 + kTile <= a.H) && (x0 + kTile <= a.W) && ((a.W & 3) == 0);
-
-        if (tid == 0) {
-            s_round = 0;
-            s_flags = 0;
-        }
-        if (tid < 5) s_key[tid] = 0x7f800000u;
-        // ---- stage the tile: 16 cells per thread (4 rows x 4 consecutive columns)
-        R told[16];
-        const int cx = (tid & 15) * 4;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int ry = (tid >> 4) + 16 * k;
-            const int64_t gy = y0 + ry;
-            if (full) {
-                if constexpr (sizeof(R) == 4) {
-                    const float4 t4 = *reinterpret_cast<const float4*>(&T[gy * a.W + x0 + cx]);
-                    const float4 c4 = *reinterpret_cast<const float4*>(&cost[gy * a.W + x0 + cx]);
-                    told[4 * k + 0] = t4.x; told[4 * k + 1] = t4.y; told[4 * k + 2] = t4.z; told[4 * k + 3] = t4.w;
-                    R* cr = &Cs[(ry + 1) * kLds + cx + 1];
-                    cr[0] = c4.x; cr[1] = c4.y; cr[2] = c4.z; cr[3] = c4.w;
-                } else {
-                    const double2 t0 = *reinterpret_cast<const double2*>(&T[gy * a.W + x0 + cx]);
-                    const double2 t1 = *reinterpret_cast<const double2*>(&T[gy * a.W + x0 + cx + 2]);
-                    const double2 c0 = *reinterpret_cast<const double2*>(&cost[gy * a.W + x0 + cx]);
-                    const double2 c1 = *reinterpret_cast<const double2*>(&cost[gy * a.W + x0 + cx + 2]);
-                    told[4 * k + 0] = t0.x; told[4 * k + 1] = t0.y; told[4 * k + 2] = t1.x; told[4 * k + 3] = t1.y;
-                    R* cr = &Cs[(ry + 1) * kLds + cx + 1];
-                    cr[0] = c0.x; cr[1] = c0.y; cr[2] = c1.x; cr[3] = c1.y;
-                }
-            } else {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int64_t gx = x0 + cx + e;
-                    const bool in = gy < a.H && gx < a.W;
-                    told[4 * k + e] = load_T<R>(a, T, gy, gx);  // ghost cells land in padding
-                    Cs[(ry + 1) * kLds + cx + e + 1] = in ? cost[gy * a.W + gx] : INF;
-                }
-            }
-#pragma unroll
-            for (int e = 0; e < 4; ++e) Ts[(ry + 1) * kLds + cx + e + 1] = told[4 * k + e];
-        }
-        // halo ring: wave 0 north row, 1 south row, 2 west column, 3 east column
-        {
-            R v;
-            if (wave == 0)      v = load_T<R>(a, T, y0 - 1, x0 + lane);
-            else if (wave == 1) v = load_T<R>(a, T, y0 + kTile, x0 + lane);
-            else if (wave == 2) v = load_T<R>(a, T, y0 + lane, x0 - 1);
-            else                v = load_T<R>(a, T, y0 + lane, x0 + kTile);
-            int h;
-            if (wave == 0)      h = 0 * kLds + lane + 1;
-            else if (wave == 1) h = (kLds - 1) * kLds + lane + 1;
-            else if (wave == 2) h = (lane + 1) * kLds + 0;
-            else                h = (lane + 1) * kLds + kLds - 1;
-            Ts[h] = v;
-            Cs[h] = INF;
-            if (lane < 4) Cs[(lane >> 1) * (kLds - 1) * kLds + (lane & 1) * (kLds - 1)] = INF;  // corners
-        }
-        __syncthreads();
-
-        // ---- sweep rounds (4 quadrant directions concurrently, one per wave)
-        bool last_changed = false;
-        for (int round = 0;; ++round) {
-            bool ch;
-            if (wave == 0)      ch = sweep_quadrant<R, +1, +1>(Ts, Cs, lane, keep);
-            else if (wave == 1) ch = sweep_quadrant<R, -1, +1>(Ts, Cs, lane, keep);
-            else if (wave == 2) ch = sweep_quadrant<R, +1, -1>(Ts, Cs, lane, keep);
-            else                ch = sweep_quadrant<R, -1, -1>(Ts, Cs, lane, keep);
-            if (__any(ch) && lane == 0) atomicOr(&s_round, 1u << (round & 31));
-            __syncthreads();
-            last_changed = (s_round >> (round & 31)) & 1u;
-            if (!last_changed || round + 1 >= a.max_rounds) break;
-        }
-
-        // ---- write back changed cells, collect side flags and the smallest entering values
-        unsigned fl = 0;
-        R kmin_self = INF, kmin[4] = {INF, INF, INF, INF};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int ry = (tid >> 4) + 16 * k;
-            const int64_t gy = y0 + ry;
-            R nv[4];
-            bool any = false;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                nv[e] = Ts[(ry + 1) * kLds + cx + e + 1];
-                const bool chg = nv[e] < told[4 * k + e];
-                any |= chg;
-                if (nv[e] < told[4 * k + e] * keep) {
-                    kmin_self = umin(kmin_self, nv[e]);
-                    // A neighbour can only improve if this edge value undercuts the neighbour's
-                    // adjacent cell (the halo value, stale => larger => conservative).
-                    const int lx = cx + e + 1, ly = ry + 1;
-#ifdef EIK_NO_FILTER
-                    if (ry == 0) fl |= 1u;
-                    if (ry == kTile - 1) fl |= 2u;
-                    if (cx + e == 0) fl |= 4u;
-                    if (cx + e == kTile - 1) fl |= 8u;
-#else
-                    if (ry == 0 && nv[e] < Ts[lx]) { fl |= 1u; kmin[0] = umin(kmin[0], nv[e]); }
-                    if (ry == kTile - 1 && nv[e] < Ts[(kLds - 1) * kLds + lx]) { fl |= 2u; kmin[1] = umin(kmin[1], nv[e]); }
-                    if (cx + e == 0 && nv[e] < Ts[ly * kLds]) { fl |= 4u; kmin[2] = umin(kmin[2], nv[e]); }
-                    if (cx + e == kTile - 1 && nv[e] < Ts[ly * kLds + kLds - 1]) { fl |= 8u; kmin[3] = umin(kmin[3], nv[e]); }
-#endif
-                    const int64_t gx = x0 + cx + e;                     // subdomain edges (DD)
-                    if (gy == a.H - 1 && ry != kTile - 1) fl |= 32u;
-                    if (gx == a.W - 1 && cx + e != kTile - 1) fl |= 64u;
-                }
-            }
-            if (any) {
-                if (full) {
-                    if constexpr (sizeof(R) == 4) {
-                        *reinterpret_cast<float4*>(&T[gy * a.W + x0 + cx]) = make_float4(nv[0], nv[1], nv[2], nv[3]);
-                    } else {
-                        *reinterpret_cast<double2*>(&T[gy * a.W + x0 + cx]) = make_double2(nv[0], nv[1]);
-                        *reinterpret_cast<double2*>(&T[gy * a.W + x0 + cx + 2]) = make_double2(nv[2], nv[3]);
-                    }
-                } else {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const int64_t gx = x0 + cx + e;
-                        if (gy < a.H && gx < a.W && nv[e] < told[4 * k + e]) T[gy * a.W + gx] = nv[e];
-                    }
-                }
-            }
-        }
-        if (fl) atomicOr(&s_flags, fl);
-        if (kmin_self < INF) atomicMin(&s_key[0], __float_as_uint((float)kmin_self));
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-            if (kmin[q] < INF) atomicMin(&s_key[q + 1], __float_as_uint((float)kmin[q]));
-        __syncthreads();
-        if (tid < 5) {  // up to 5 enqueues, one per lane, so their atomics overlap
-            const unsigned f = s_flags;
-            const int base = map * a.tiles_per_map;
-            const float kk = __uint_as_float(s_key[tid]);
-            if (tid == 0 && last_changed) enqueue(a, tile, nxt, stamp, kk);
-            if (tid == 1 && (f & 1u) && ty > 0) enqueue(a, base + rem - a.ntx, nxt, stamp, kk);
-            if (tid == 2 && (f & 2u) && ty + 1 < a.nty) enqueue(a, base + rem + a.ntx, nxt, stamp, kk);
-            if (tid == 3 && (f & 4u) && tx > 0) enqueue(a, base + rem - 1, nxt, stamp, kk);
-            if (tid == 4 && (f & 8u) && tx + 1 < a.ntx) enqueue(a, base + rem + 1, nxt, stamp, kk);
-            if (tid == 0 && a.edge_dirty) {  // subdomain edges (domain decomposition)
-                unsigned e = 0;
-                if ((f & 1u) && ty == 0) e |= 1u;
-                if (((f & 2u) || (f & 32u)) && ty + 1 == a.nty) e |= 2u;
-                if ((f & 4u) && tx == 0) e |= 4u;
-                if (((f & 8u) || (f & 64u)) && tx + 1 == a.ntx) e |= 8u;
-                if (e) atomicOr(a.edge_dirty, e);
-            }
-            if (tid == 0 && a.visits) atomicAdd(a.visits, 1ull);
-        }
+        process_tile<R, false>(a, tile, L, keep);
+        activate_after(a, tile, L, nxt, stamp);
+        if (tid == 0 && a.visits) atomicAdd(a.visits, 1ull);
         __syncthreads();  // LDS reuse by the next tile of this workgroup
     }
 }
 
-// T = inf everywhere; T[goal] = 0; marks cleared.  Goals: one per map (gx < 0: none).
+// ------------------------------------------------------------------- PERSISTENT driver
+// Take a ticket and wait for its slot: the next queued tile, or -1 when the solve has ended
+// (no tile pending or busy) or failed.  ONE lane polls (relaxed agent-scope loads = sc1).
+__device__ __forceinline__ int qgrab(const Fim2dArgs& a) {
+    if (__hip_atomic_load(a.qerror, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return -1;
+    const unsigned long long pos = atomicAdd(a.qhead, 1ull);
+    unsigned* slot = &a.qslot[pos & a.qmask];
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (unsigned spin = 0;; ++spin) {
+        const unsigned v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v != 0u) {
+            // free the slot BEFORE the tile can be re-queued (slot reuse)
+            __hip_atomic_store(slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int tile = (int)(v - 1u);
+            // pending -> busy before T is read: any activation from here on makes the finish
+            // re-queue the tile, so no update is lost
+            atomicExch(&a.qstate[tile], kBusy);
+            return tile;
+        }
+        if ((spin & 7u) == 7u) {
+            if (__hip_atomic_load(a.qactive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return -1;
+            if (__hip_atomic_load(a.qerror, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return -1;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > a.qtimeout) {  // never hang
+                atomicOr(a.qerror, 1u);
+                return -1;
+            }
+        }
+        __builtin_amdgcn_s_sleep(8);
+    }
+}
+
+// Retire a visited tile (after its activations completed): re-queue it if it was activated
+// while busy (it stays counted), else it stops counting as active.
+__device__ __forceinline__ void qfinish(const Fim2dArgs& a, int tile) {
+    if (atomicAdd(a.visits, 1ull) >= a.qbudget) atomicOr(a.qerror, 2u);
+    const unsigned old = atomicAnd(&a.qstate[tile], ~kBusy);
+    if (old & kPending)
+        qslot_put(a, tile);
+    else
+        atomicSub(a.qactive, 1);
+}
+
+template <typename R>
+__global__ __launch_bounds__(kThreads) void fim2d_persist_kernel(Fim2dArgs a) {
+    __shared__ TileLds<R> L;
+    init_guard_rows(L);
+    const R keep = (R)a.keep;
+    int tile = -1;
+    for (;;) {
+        // wave 0 retires the previous tile (lanes 0..4 activate, lane 0 finishes) and takes the
+        // next one; the other waves go straight to the barrier
+        if (threadIdx.x < 64) {
+            if (tile >= 0) {
+                activate_after(a, tile, L, 0, 0u);
+                // the activations' counter increments complete before the finish decrements
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (threadIdx.x == 0) qfinish(a, tile);
+            }
+            if (threadIdx.x == 0) L.tile = qgrab(a);
+        }
+        __syncthreads();
+        tile = __builtin_amdgcn_readfirstlane(L.tile);
+        if (tile < 0) break;  // uniform: solve finished (or failed)
+        process_tile<R, true>(a, tile, L, keep);  // sc1 loads; sc1 stores drained + barrier
+    }
+}
+// ------------------------------------------------------------------------ init / seeding
+// T = inf everywhere; marks / keys / queue state cleared.
 template <typename R>
 __global__ void fim2d_init_kernel(R* __restrict__ T, int64_t n, unsigned* __restrict__ mark, int64_t ntiles,
-                                  unsigned* __restrict__ key, unsigned* __restrict__ minkey) {
+                                  unsigned* __restrict__ key, unsigned* __restrict__ minkey, unsigned* __restrict__ qstate,
+                                  unsigned* __restrict__ qslot, int64_t nslots) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) T[i] = Real<R>::inf();
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ntiles; i += stride) {
         mark[i] = 0;
         key[i] = 0x7f800000u;
+        if (qstate) qstate[i] = 0;
     }
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += stride) qslot[i] = 0;
     if (blockIdx.x == 0 && threadIdx.x < 3) minkey[threadIdx.x] = threadIdx.x == 0 ? 0u : 0x7f800000u;
 }
 
+// T[goal] = 0 and the goal tile activated.  Goals: one per map (gx < 0: none).
 template <typename R>
 __global__ void fim2d_seed_kernel(Fim2dArgs a, const int64_t* __restrict__ goals, int nmaps) {
     const int m = blockIdx.x * blockDim.x + threadIdx.x;
@@ -320,14 +551,22 @@ __global__ void fim2d_seed_kernel(Fim2dArgs a, const int64_t* __restrict__ goals
     if (gx < 0 || gy < 0 || gx >= a.W || gy >= a.H) return;
     static_cast<R*>(a.T)[(int64_t)m * a.H * a.W + gy * a.W + gx] = R(0);
     const int tile = m * a.tiles_per_map + (int)(gy / kTile) * a.ntx + (int)(gx / kTile);
+    if (a.mode == kModePersistent) {
+        qpush(a, tile);
+        return;
+    }
     a.mark[tile] = 1;  // enqueued for iteration 0
     a.key[tile] = 0u;  // T = 0 enters at the goal
     const int pos = atomicAdd(&a.counts[0], 1);
     a.lists[pos] = tile;
 }
 
-// Domain decomposition: ghost = min(ghost, recv) and enqueue (for iteration `iter`) every edge
-// tile next to a ghost cell that decreased.  side: 0 N, 1 S, 2 W, 3 E.
+// After each persistent launch: the tickets of its idle waiters ran ahead of the tail --
+// restart the ticket counter at the tail (every slot is empty when the launch ends).
+__global__ void fim2d_qrewind_kernel(Fim2dArgs a) { *a.qhead = *a.qtail; }
+
+// Domain decomposition: ghost = min(ghost, recv) and activate every edge tile next to a ghost
+// cell that decreased (for list iteration `iter`, or into the FIFO).  side: 0 N 1 S 2 W 3 E.
 template <typename R>
 __global__ void fim2d_merge_ghost_kernel(Fim2dArgs a, int side, const R* __restrict__ recv, int64_t len) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -344,7 +583,7 @@ __global__ void fim2d_merge_ghost_kernel(Fim2dArgs a, int side, const R* __restr
             ty = (int)(i / kTile);
             tx = side == 2 ? 0 : a.ntx - 1;
         }
-        enqueue(a, ty * a.ntx + tx, a.iter % 3, a.iter + 1, (float)v);
+        activate(a, ty * a.ntx + tx, a.iter % 3, a.iter + 1, (float)v);
     }
 }
 
@@ -365,14 +604,34 @@ __global__ void fim2d_pack_edges_kernel(Fim2dArgs a, R* __restrict__ n, R* __res
 }
 
 // ------------------------------------------------------------------------- host launchers
-template <typename R>
-static hipError_t launch_sweep(const Fim2dArgs& a, int grid, hipStream_t st) {
-    hipLaunchKernelGGL(fim2d_sweep_kernel<R>, dim3(grid), dim3(kThreads), 0, st, a);
+hipError_t fim2d_sweep(const Fim2dArgs& a, bool f64, int grid, hipStream_t st) {
+    if (f64)
+        hipLaunchKernelGGL(fim2d_sweep_kernel<double>, dim3(grid), dim3(kThreads), 0, st, a);
+    else
+        hipLaunchKernelGGL(fim2d_sweep_kernel<float>, dim3(grid), dim3(kThreads), 0, st, a);
     return hipGetLastError();
 }
 
-hipError_t fim2d_sweep(const Fim2dArgs& a, bool f64, int grid, hipStream_t st) {
-    return f64 ? launch_sweep<double>(a, grid, st) : launch_sweep<float>(a, grid, st);
+// Workgroups of the persistent kernel that can be co-resident (a larger grid only adds
+// workgroups that start after the solve ended and leave at once).
+int fim2d_persist_resident(bool f64, int cus) {
+    int per_cu = 0;
+    const hipError_t e = f64 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fim2d_persist_kernel<double>,
+                                                                            kThreads, 0)
+                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fim2d_persist_kernel<float>,
+                                                                            kThreads, 0);
+    if (e != hipSuccess || per_cu < 1) per_cu = 1;
+    return per_cu * cus;
+}
+
+hipError_t fim2d_persist(const Fim2dArgs& a, bool f64, int grid, hipStream_t st) {
+    if (f64)
+        hipLaunchKernelGGL(fim2d_persist_kernel<double>, dim3(grid), dim3(kThreads), 0, st, a);
+    else
+        hipLaunchKernelGGL(fim2d_persist_kernel<float>, dim3(grid), dim3(kThreads), 0, st, a);
+    // before anything (merge kernel, next launch) appends again
+    hipLaunchKernelGGL(fim2d_qrewind_kernel, dim3(1), dim3(1), 0, st, a);
+    return hipGetLastError();
 }
 
 hipError_t fim2d_init(const Fim2dArgs& a, bool f64, int nmaps, const int64_t* d_goals, hipStream_t st) {
@@ -380,14 +639,16 @@ hipError_t fim2d_init(const Fim2dArgs& a, bool f64, int nmaps, const int64_t* d_
     const int64_t ntiles = (int64_t)nmaps * a.tiles_per_map;
     const int grid = (int)std::min<int64_t>(4096, (n + 255) / 256);
     hipError_t e0 = hipMemsetAsync(a.counts, 0, sizeof(int) * 4, st);
+    if (e0 == hipSuccess && a.qhead) e0 = hipMemsetAsync(a.qhead, 0, kQueueCtlBytes, st);  // head tail active error
     if (e0 != hipSuccess) return e0;
+    const int64_t nslots = a.qslot ? (int64_t)a.qmask + 1 : 0;
     if (f64) {
         hipLaunchKernelGGL(fim2d_init_kernel<double>, dim3(grid), dim3(256), 0, st, static_cast<double*>(a.T), n,
-                           a.mark, ntiles, a.key, a.minkey);
+                           a.mark, ntiles, a.key, a.minkey, a.qstate, a.qslot, nslots);
         hipLaunchKernelGGL(fim2d_seed_kernel<double>, dim3((nmaps + 255) / 256), dim3(256), 0, st, a, d_goals, nmaps);
     } else {
         hipLaunchKernelGGL(fim2d_init_kernel<float>, dim3(grid), dim3(256), 0, st, static_cast<float*>(a.T), n,
-                           a.mark, ntiles, a.key, a.minkey);
+                           a.mark, ntiles, a.key, a.minkey, a.qstate, a.qslot, nslots);
         hipLaunchKernelGGL(fim2d_seed_kernel<float>, dim3((nmaps + 255) / 256), dim3(256), 0, st, a, d_goals, nmaps);
     }
     return hipGetLastError();

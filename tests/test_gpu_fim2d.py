@@ -19,11 +19,15 @@ RTOL32 = 2e-5
 ATOL64 = 1e-9
 
 
-@pytest.fixture(scope="module")
-def ctx():
+@pytest.fixture(scope="module", params=["persistent", "list"])
+def ctx(request):
+    """Both solver drivers: one persistent launch over the device FIFO (default), and one
+    launch per outer iteration over the active list."""
     import eikonal
+    from eikonal import _lib as L
 
     c = eikonal.Context(0)
+    c.set_option(L.OPT_MODE, L.MODE_PERSISTENT if request.param == "persistent" else L.MODE_LIST)
     yield c
     c.close()
 
@@ -163,4 +167,4 @@ def test_stats_count_visits(ctx):
     c = np.ones((512, 512), np.float32)
     ctx.tmap2d(c, [256, 256], dtype=np.float32)
     s = ctx.stats()
-    assert s["tile_visits"] >= 64 and s["iterations"] >= 8 and s["solve_ms"] > 0
+    assert s["tile_visits"] >= 64 and s["iterations"] >= 1 and s["solve_ms"] > 0
