@@ -11,9 +11,10 @@ centre, halo exchange over RCCL (eikonal/dd.py).  A "step" = one full solve of t
 (T init -> converged), inputs resident in HBM.  value = cells of the global raster x steps /
 max-over-ranks wall time (Gcells/s).
 
-Also reported: roofline of the dominant kernel (fim2d_sweep_kernel: per-launch hipEvents on the
-solver stream over the timed region, algorithmic bytes = tile visits x 50176 B), ms-to-path
-(host cost -> host path, N = 1), and the CPU baseline (oracle C heap FMM, 1 thread, N = 1).
+Also reported: roofline of the dominant kernel (fim2d_persist_kernel, one launch per solve:
+hipEvents around it on the solver stream over the timed region; algorithmic bytes = full tile
+visits x 50176 B + in-place passes x 17408 B), ms-to-path (host cost -> host path,
+N = 1), and the CPU baseline (oracle C heap FMM, 1 thread, N = 1).
 """
 import argparse
 import json
@@ -35,6 +36,7 @@ from eikonal import _lib as L  # noqa: E402
 METRIC = "Eikonal Gcells/s + ms-to-path, 4k² & 16k² costmap at 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 BYTES_PER_VISIT = 4 * (3 * 64 * 64 + 4 * 64)  # fp32: cost read + T read + T write + halo read
+BYTES_PER_PASS = 4 * (64 * 64 + 4 * 64)  # fp32 in-place pass: T write + halo re-read
 
 
 def env_int(k, d):
@@ -90,9 +92,10 @@ def main():
         step()
 
     def timed(instrument):
-        """K steps between barrier + synchronize; returns (max-over-ranks seconds, visits, sweep_ms, iters)."""
+        """K steps between barrier + synchronize; returns (max-over-ranks seconds, visits, passes,
+        sweep_ms, launches)."""
         ctx.set_option(L.OPT_TIMING, 1 if instrument else 0)
-        visits, sweep_ms, iters = 0, 0.0, 0
+        visits, passes, sweep_ms, iters = 0, 0, 0.0, 0
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -102,6 +105,7 @@ def main():
             if instrument:
                 s = fim.stats()
                 visits += s["tile_visits"]
+                passes += s["inplace_passes"]
                 sweep_ms += s["sweep_ms"]
                 iters += s["iterations"]
         torch.cuda.synchronize()
@@ -113,19 +117,20 @@ def main():
             tt = torch.tensor([el], device=dev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             el = tt.item()
-        return el, visits, sweep_ms, iters
+        return el, visits, passes, sweep_ms, iters
 
     # 1) the measurement: no per-launch instrumentation inside the timed region
-    el, _, _, _ = timed(False)
+    el, _, _, _, _ = timed(False)
     # 2) the same K steps again with a hipEvent pair around every sweep launch (roofline)
-    el_i, visits, sweep_ms, iters = (0.0, 0, 0.0, 0) if args.no_timing else timed(True)
+    el_i, visits, passes, sweep_ms, iters = (0.0, 0, 0, 0.0, 0) if args.no_timing else timed(True)
 
     value = H * W * args.steps / el / 1e9
     ms_per_step = el / args.steps * 1e3
 
     # roofline of the dominant kernel (rank-local: this rank's launches and its event time)
     launches = iters
-    achieved = (visits * BYTES_PER_VISIT / (sweep_ms * 1e-3) / 1e9) if sweep_ms > 0 else None
+    alg_bytes = visits * BYTES_PER_VISIT + passes * BYTES_PER_PASS
+    achieved = (alg_bytes / (sweep_ms * 1e-3) / 1e9) if sweep_ms > 0 else None
     traffic = None
     if os.path.exists(args.pmc_traffic):
         try:
@@ -134,17 +139,18 @@ def main():
             traffic = None
     roof = {
         "bound": "hbm",
-        "kernel": "fim2d_sweep_kernel<float>",
+        "kernel": "fim2d_persist_kernel<float>",
         "achieved": round(achieved, 2) if achieved else None,
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
         "traffic": traffic,
-        "alg_bytes_per_launch": round(visits * BYTES_PER_VISIT / max(launches, 1)),
+        "alg_bytes_per_launch": round(alg_bytes / max(launches, 1)),
         "avg_launch_us": round(sweep_ms * 1e3 / max(launches, 1), 2),
         "instrumented_ms_per_step": round(el_i / args.steps * 1e3, 4),
         "launches_per_solve": round(launches / args.steps, 1),
         "tile_visits_per_solve": round(visits / args.steps, 1),
+        "inplace_passes_per_solve": round(passes / args.steps, 1),
     }
 
     out = {

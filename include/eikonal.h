@@ -60,6 +60,8 @@ typedef struct {
     double solve_ms;      /* device time of the last solve (hipEvents, init..converged)         */
     double sweep_ms;      /* summed device time of the sweep launches (timing option on)        */
     double bytes_alg;     /* algorithmic bytes of the sweep launches (tile_visits x bytes/visit) */
+    int64_t inplace_passes; /* persistent mode: extra in-place passes of busy tiles (halo refresh
+                               + sweep + write-back of the tile already in LDS)                 */
 } eik_stats;
 
 /* options (eik_set_option) */

@@ -80,6 +80,25 @@ __device__ __forceinline__ double godunov2_step(double a, double b, double c) {
     return c < d ? lo + c : t2;
 }
 
+// Sweep-step form without the 1D branch: with d clamped to c, lo + (d + sqrt(2c^2 - d^2)) / 2
+// equals lo + c exactly when d >= c, i.e. the 1D update falls out of the 2D form.  The clamp is
+// an unsigned min (no canonicalisation; a NaN d -- both neighbours +inf -- becomes c and the
+// result stays +inf).  Inputs are non-negative, +inf, never NaN.
+__device__ __forceinline__ float godunov2_fast(float a, float b, float c) {
+    const float lo = umin(a, b), hi = umax(a, b);
+    const float d = umin(hi - lo, c);
+    const float c2 = c * c;
+    const float q = __builtin_fmaf(-d, d, c2) + c2;  // 2c^2 - d^2 >= c^2 >= 0
+    return __builtin_fmaf(0.5f, d + __builtin_amdgcn_sqrtf(q), lo);
+}
+__device__ __forceinline__ double godunov2_fast(double a, double b, double c) {
+    const double lo = umin(a, b), hi = umax(a, b);
+    const double d = umin(hi - lo, c);
+    const double c2 = c * c;
+    const double q = __builtin_fma(-d, d, c2) + c2;
+    return __builtin_fma(0.5, d + __builtin_sqrt(q), lo);
+}
+
 // Whole-wave shift by one lane (lane i <- lane i-1) on the DPP path: v_mov_b32_dpp wave_shr:1.
 // Keeps the Gauss-Seidel dependency of the skewed sweep in registers (no LDS round trip).
 __device__ __forceinline__ float wave_shr1(float v) {

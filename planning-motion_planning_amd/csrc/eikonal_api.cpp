@@ -111,6 +111,8 @@ static int set_err(eik_ctx* c, int code, const char* fmt, ...) {
     } while (0)
 
 static int bytes_per_visit(bool f64) { return (f64 ? 8 : 4) * (3 * kTile * kTile + 4 * kTile); }
+// in-place pass of a busy tile (persistent mode): T write-back + halo ring re-read
+static int bytes_per_pass(bool f64) { return (f64 ? 8 : 4) * (kTile * kTile + 4 * kTile); }
 
 extern "C" {
 
@@ -211,10 +213,10 @@ int eik_fim2d_create(eik_ctx* c, int64_t B, int64_t H, int64_t W, int dtype, eik
         (e = hipHostMalloc((void**)&f->h_q, kQueueCtlBytes)) != hipSuccess ||
         (e = f->counts.ensure(sizeof(int) * 64)) != hipSuccess || (e = f->mark.ensure(sizeof(unsigned) * tiles)) != hipSuccess ||
         (e = f->key.ensure(sizeof(unsigned) * tiles)) != hipSuccess ||
-        (e = f->visits.ensure(sizeof(unsigned long long))) != hipSuccess ||
+        (e = f->visits.ensure(2 * sizeof(unsigned long long))) != hipSuccess ||
         (e = f->edge.ensure(sizeof(unsigned) * 4)) != hipSuccess || (e = f->goals.ensure(sizeof(int64_t) * 2 * B)) != hipSuccess ||
         (e = hipHostMalloc((void**)&f->h_counts, sizeof(int) * 64)) != hipSuccess ||
-        (e = hipHostMalloc((void**)&f->h_visits, sizeof(unsigned long long))) != hipSuccess ||
+        (e = hipHostMalloc((void**)&f->h_visits, 2 * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipEventCreate(&f->ev_start)) != hipSuccess || (e = hipEventCreate(&f->ev_stop)) != hipSuccess) {
         eik_fim2d_destroy(f);
         return set_err(c, EIK_ERR_NOMEM, "fim2d allocation: %s", hipGetErrorString(e));
@@ -285,7 +287,7 @@ int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
     f->ev_used = 0;
     HIPCHK(c, hipEventRecord(f->ev_start, f->stream));
     HIPCHK(c, hipMemcpyAsync(f->goals.p, goals, sizeof(int64_t) * 2 * f->B, hipMemcpyHostToDevice, f->stream));
-    HIPCHK(c, hipMemsetAsync(f->visits.p, 0, sizeof(unsigned long long), f->stream));
+    HIPCHK(c, hipMemsetAsync(f->visits.p, 0, 2 * sizeof(unsigned long long), f->stream));
     HIPCHK(c, hipMemsetAsync(f->edge.p, 0, sizeof(unsigned) * 4, f->stream));
     HIPCHK(c, fim2d_init(f->a, f->f64, (int)f->B, (const int64_t*)f->goals.p, f->stream));
     f->started = true;
@@ -388,7 +390,7 @@ int eik_fim2d_active(eik_fim2d* f, int64_t* active) {
 static int finish_solve(eik_fim2d* f) {
     eik_ctx* c = f->ctx;
     HIPCHK(c, hipEventRecord(f->ev_stop, f->stream));
-    HIPCHK(c, hipMemcpyAsync(f->h_visits, f->visits.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, f->stream));
+    HIPCHK(c, hipMemcpyAsync(f->h_visits, f->visits.p, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, f->stream));
     HIPCHK(c, hipStreamSynchronize(f->stream));
     float ms = 0.f;
     (void)hipEventElapsedTime(&ms, f->ev_start, f->ev_stop);
@@ -428,16 +430,18 @@ int eik_fim2d_stats(eik_fim2d* f, eik_stats* out) {
     if (!f || !out) return EIK_ERR_ARG;
     if (f->started) {
         eik_ctx* c = f->ctx;
-        HIPCHK(c, hipMemcpyAsync(f->h_visits, f->visits.p, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+        HIPCHK(c, hipMemcpyAsync(f->h_visits, f->visits.p, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                                  f->stream));
         HIPCHK(c, hipStreamSynchronize(f->stream));
     }
     out->iterations = f->iterations;
-    out->tile_visits = (int64_t)*f->h_visits;
+    out->tile_visits = (int64_t)f->h_visits[0];
+    out->inplace_passes = (int64_t)f->h_visits[1];
     out->host_syncs = f->host_syncs;
     out->solve_ms = f->solve_ms;
     out->sweep_ms = f->sweep_ms;
     out->bytes_alg = (double)out->tile_visits * bytes_per_visit(f->f64) +
+                     (double)out->inplace_passes * bytes_per_pass(f->f64) +
                      (double)f->B * f->H * f->W * (f->f64 ? 8 : 4);
     return EIK_OK;
 }

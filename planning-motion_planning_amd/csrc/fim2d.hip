@@ -37,7 +37,30 @@
 
 namespace eik {
 
+// per-tile queue state (persistent mode): pending / busy, plus what activated the tile since its
+// last visit -- a halo side that improved (its information flows away from that side) or the
+// tile itself (last visit changed it: every direction)
 constexpr unsigned kPending = 1u, kBusy = 2u;
+constexpr unsigned kFromN = 4u, kFromS = 8u, kFromW = 16u, kFromE = 32u, kSelf = 64u;
+
+// Quadrant sweeps that can carry the triggering information: wave 0 (+x,+y) and 1 (-x,+y) move
+// it away from the north edge, 2 and 3 from the south; 0 and 2 from the west, 1 and 3 from the
+// east.  A visit that runs a subset and changes nothing is still a fixed point of the local
+// update (every cell was evaluated against final neighbours); one that changes something
+// re-activates itself with kSelf, i.e. all four.
+__device__ __forceinline__ unsigned sweep_dirs(unsigned trig) {
+    if (trig & kSelf) return 0xFu;
+    unsigned d = 0;
+    if (trig & kFromN) d |= 0x3u;
+    if (trig & kFromS) d |= 0xCu;
+    if (trig & kFromW) d |= 0x5u;
+    if (trig & kFromE) d |= 0xAu;
+    return d ? d : 0xFu;
+}
+#ifndef EIK_PROBE
+#define EIK_PROBE(k) ((void)0)  // phase timing hooks (scratch profiling harness)
+#define EIK_VISIT(trig, dirs) ((void)0)
+#endif
 
 // ------------------------------------------------------------------- memory access policy
 // Plain accesses (LIST mode) or coherent sc1 buffer accesses (PERSISTENT mode).
@@ -164,59 +187,96 @@ __device__ __forceinline__ void qslot_put(const Fim2dArgs& a, int tile) {
     const unsigned long long pos = atomicAdd(a.qtail, 1ull);
     __hip_atomic_store(&a.qslot[pos & a.qmask], (unsigned)tile + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void qpush(const Fim2dArgs& a, int tile) {
-    if (atomicOr(&a.qstate[tile], kPending) == 0u) {
+__device__ __forceinline__ void qpush(const Fim2dArgs& a, int tile, unsigned trig) {
+    if (atomicOr(&a.qstate[tile], kPending | trig) == 0u) {
         atomicAdd(a.qactive, 1);  // before the slot store: a waiter never sees "empty and idle"
         qslot_put(a, tile);
     }
 }
 
-__device__ __forceinline__ void activate(const Fim2dArgs& a, int tile, int list, unsigned stamp, float key) {
+__device__ __forceinline__ void activate(const Fim2dArgs& a, int tile, int list, unsigned stamp, float key,
+                                         unsigned trig) {
     if (a.mode == kModePersistent)
-        qpush(a, tile);
+        qpush(a, tile, trig);
     else
         enqueue(a, tile, list, stamp, key);
 }
 
+// Neighbour activations of a write-back with flags f: thread q in 1..4 handles one side (their
+// atomics overlap); thread 0 flags changed subdomain edges for the halo exchange.
+__device__ __forceinline__ void activate_neighbours(const Fim2dArgs& a, int tile, unsigned f, const unsigned* key,
+                                                    int list, unsigned stamp) {
+    const int tid = threadIdx.x;
+    if (tid >= 5) return;
+    const int map = tile / a.tiles_per_map;
+    const int rem = tile - map * a.tiles_per_map;
+    const int ty = rem / a.ntx, tx = rem - (rem / a.ntx) * a.ntx;
+    const int base = map * a.tiles_per_map;
+    const float kk = __uint_as_float(key[tid]);
+    // (this tile's north edge is the north neighbour's south halo, ...)
+    if (tid == 1 && (f & 1u) && ty > 0) activate(a, base + rem - a.ntx, list, stamp, kk, kFromS);
+    if (tid == 2 && (f & 2u) && ty + 1 < a.nty) activate(a, base + rem + a.ntx, list, stamp, kk, kFromN);
+    if (tid == 3 && (f & 4u) && tx > 0) activate(a, base + rem - 1, list, stamp, kk, kFromE);
+    if (tid == 4 && (f & 8u) && tx + 1 < a.ntx) activate(a, base + rem + 1, list, stamp, kk, kFromW);
+    if (tid == 0 && a.edge_dirty) {  // subdomain edges (domain decomposition)
+        unsigned e = 0;
+        if ((f & 1u) && ty == 0) e |= 1u;
+        if (((f & 2u) || (f & 32u)) && ty + 1 == a.nty) e |= 2u;
+        if ((f & 4u) && tx == 0) e |= 4u;
+        if (((f & 8u) || (f & 64u)) && tx + 1 == a.ntx) e |= 8u;
+        if (e) atomicOr(a.edge_dirty, e);
+    }
+}
+
 // ------------------------------------------------------------------------- quadrant sweep
+// Cs sits right after the Ts ring in TileLds: Cs - Ts is a compile-time constant, so every LDS
+// access of a sweep step is one per-lane address plus an immediate offset.
+constexpr int kCsOff = (kLds + 1) * kLds;  // elements
+
 // One quadrant sweep of the staged tile.  DX/DY = +-1: direction of propagation.
 // Lane l owns column x; at step s it updates row r = s - l (skewed Gauss-Seidel), so its
 // upstream x neighbour is lane l-1's previous result (DPP) and its upstream y neighbour its own.
-// Branch- and select-free: r is clamped to [-1, 64]; rows -1 and 64 are the halo rows, whose
-// cost is +inf in Cs (same 66-stride layout as Ts), so a lane outside the tile computes +inf or
-// NaN and its ds_min / min / `<` are no-ops.  Every LDS access of a step shares one address.
-template <typename R, int DX, int DY>
-__device__ __forceinline__ bool sweep_quadrant(R* __restrict__ Ts, const R* __restrict__ Cs, int lane, R keep) {
-    const int x = DX > 0 ? lane : kTile - 1 - lane;
-    const int col = x + 1;
-    bool changed = false;
-
-    auto addr = [&](int s) {
-        int r = s - lane;
-        r = r < -1 ? -1 : (r > kTile ? kTile : r);
-        const int lr = DY > 0 ? r + 1 : kTile - r;  // LDS row 0..65
-        return lr * kLds + col;
+// Branch- and select-free: r is clamped to [-1, 64] (one add + one med3 on the byte offset);
+// rows -1 and 64 are the halo rows, whose cost is +inf in Cs, so a lane outside the tile
+// computes +inf or NaN and its ds_min / min / `<` are no-ops.  TRACK: also report whether any
+// cell decreased by more than the tolerance (only needed for multi-round visits; single-round
+// visits read it off the write-back).
+template <typename R, int DX, int DY, bool TRACK>
+__device__ __forceinline__ bool sweep_quadrant(R* __restrict__ Ts, int lane, R keep) {
+    constexpr int S = (int)sizeof(R);
+    constexpr int kRow = kLds * S;
+    char* const base = reinterpret_cast<char*>(Ts);
+    auto ld = [&](int off) { return *reinterpret_cast<const R*>(base + off); };
+    const int col = (DX > 0 ? lane : kTile - 1 - lane) + 1;
+    const int lo_b = col * S, hi_b = (kLds - 1) * kRow + col * S;  // LDS rows 0 and 65
+    // step s: tile row r = s - lane -> LDS row (DY > 0 ? r + 1 : 64 - r), clamped to [0, 65]
+    int raw = DY > 0 ? (1 - lane) * kRow + col * S : (kTile + lane) * kRow + col * S;
+    auto clampb = [&](int x) {  // one v_med3_i32 (the compiler emits min + cmp + cndmask)
+        int r;
+        asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo_b), "v"(hi_b));
+        return r;
     };
+    bool changed = false;
     // the upstream halo row value is the lane's "previous row" result before it starts
-    R cur = Ts[(DY > 0 ? 0 : kLds - 1) * kLds + col];
-    int o = addr(0);
-    R p_old = Ts[o], p_dnx = Ts[o + DX], p_dny = Ts[o + DY * kLds], p_upx = Ts[o - DX], p_c = Cs[o];
+    R cur = ld((DY > 0 ? 0 : kLds - 1) * kRow + col * S);
+    int o = clampb(raw);
+    R p_old = ld(o), p_dnx = ld(o + DX * S), p_dny = ld(o + DY * kRow), p_upx = ld(o - DX * S),
+      p_c = ld(o + kCsOff * S);
 #pragma clang loop unroll_count(2)
     for (int s = 0; s < 2 * kTile; ++s) {
         const R old = p_old, dnx = p_dnx, dny = p_dny, uxh = p_upx, c = p_c;
         const int oc = o;
-        o = addr(s + 1);  // next step's loads issue before this step's ds_min (no intra-wave RAW)
-        p_old = Ts[o];
-        p_dnx = Ts[o + DX];
-        p_dny = Ts[o + DY * kLds];
-        p_upx = Ts[o - DX];
-        p_c = Cs[o];
+        raw += DY * kRow;
+        o = clampb(raw);  // next step's loads issue before this step's ds_min (no intra-wave RAW)
+        p_old = ld(o);
+        p_dnx = ld(o + DX * S);
+        p_dny = ld(o + DY * kRow);
+        p_upx = ld(o - DX * S);
+        p_c = ld(o + kCsOff * S);
         const R upx = wave_shr1(cur, uxh);  // lane 0: halo column
-        const R a = umin(upx, dnx);
-        const R b = umin(cur, dny);
-        const R w = godunov2_step(a, b, c);
-        lds_min(&Ts[oc], w);
-        changed |= w < old * keep;
+        const R w = godunov2_fast(umin(upx, dnx), umin(cur, dny), c);
+        lds_min(reinterpret_cast<R*>(base + oc), w);
+        if constexpr (TRACK) changed |= w < old * keep;
         cur = umin(w, old);  // NaN (both-inf case) sorts above every value: keeps old
     }
     return changed;
@@ -233,13 +293,19 @@ struct TileLds {
     unsigned round, flags;
     unsigned key[5];    // min new value entering: self, N, S, W, E (f32 bits; ordered mode)
     int defer, tile, last;
+    unsigned dirs;      // quadrant sweeps of this visit (bit w: wave w's direction)
 };
+static_assert(offsetof(TileLds<float>, Cs) == sizeof(float) * (kLds + 2) * kLds, "Cs must follow Tbuf");
+static_assert(offsetof(TileLds<double>, Cs) == sizeof(double) * (kLds + 2) * kLds, "Cs must follow Tbuf");
 
 // ---------------------------------------------------------------------------- tile body
 // Stage, sweep and write back one tile; leaves the activation decisions in L.flags (bits 0..3:
-// neighbour N/S/W/E can improve; 32/64: changed subdomain S/E edge inside a partial tile),
-// L.last (the last round changed something) and L.key.  Ends with a workgroup barrier; in
-// COH mode every wave has drained its write-through stores before it.
+// neighbour N/S/W/E can improve; 32/64: changed subdomain S/E edge inside a partial tile;
+// 128: some cell decreased by more than the tolerance), L.last (multi-round visits: the last
+// round changed something; -1 for single-round visits, which use flags bit 7) and L.key.
+// The caller sets L.dirs (quadrant sweeps to run) before the barrier that precedes the call.
+// Ends with a workgroup barrier; in COH mode every wave has drained its write-through stores
+// before it.
 template <typename R, bool COH>
 __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileLds<R>& L, R keep) {
     constexpr R INF = Real<R>::inf();
@@ -254,6 +320,7 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
     const int64_t y0 = (int64_t)ty * kTile, x0 = (int64_t)tx * kTile;
     const bool full = (y0 + kTile <= a.H) && (x0 + kTile <= a.W) && ((a.W & 3) == 0);
 
+    EIK_PROBE(0);
     if (tid == 0) {
         L.round = 0;
         L.flags = 0;
@@ -294,117 +361,140 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
         }
     }
     // halo ring: wave 0 north row, 1 south row, 2 west column, 3 east column
-    {
-        R v;
-        if (wave == 0)      v = load_T<R, COH>(a, T, y0 - 1, x0 + lane);
-        else if (wave == 1) v = load_T<R, COH>(a, T, y0 + kTile, x0 + lane);
-        else if (wave == 2) v = load_T<R, COH>(a, T, y0 + lane, x0 - 1);
-        else                v = load_T<R, COH>(a, T, y0 + lane, x0 + kTile);
-        int h;
-        if (wave == 0)      h = 0 * kLds + lane + 1;
-        else if (wave == 1) h = (kLds - 1) * kLds + lane + 1;
-        else if (wave == 2) h = (lane + 1) * kLds + 0;
-        else                h = (lane + 1) * kLds + kLds - 1;
-        Ts[h] = v;
-        Cs[h] = INF;
-        if (lane < 4) Cs[(lane >> 1) * (kLds - 1) * kLds + (lane & 1) * (kLds - 1)] = INF;  // corners
-    }
+    int h;
+    if (wave == 0)      h = 0 * kLds + lane + 1;
+    else if (wave == 1) h = (kLds - 1) * kLds + lane + 1;
+    else if (wave == 2) h = (lane + 1) * kLds + 0;
+    else                h = (lane + 1) * kLds + kLds - 1;
+    auto load_halo = [&]() {
+        if (wave == 0)      return load_T<R, COH>(a, T, y0 - 1, x0 + lane);
+        else if (wave == 1) return load_T<R, COH>(a, T, y0 + kTile, x0 + lane);
+        else if (wave == 2) return load_T<R, COH>(a, T, y0 + lane, x0 - 1);
+        else                return load_T<R, COH>(a, T, y0 + lane, x0 + kTile);
+    };
+    Ts[h] = load_halo();
+    Cs[h] = INF;
+    if (lane < 4) Cs[(lane >> 1) * (kLds - 1) * kLds + (lane & 1) * (kLds - 1)] = INF;  // corners
     __syncthreads();
+    EIK_PROBE(1);
 
-    // ---- sweep rounds (4 quadrant directions concurrently, one per wave)
-    bool last_changed = false;
-    for (int round = 0;; ++round) {
-        bool ch;
-        if (wave == 0)      ch = sweep_quadrant<R, +1, +1>(Ts, Cs, lane, keep);
-        else if (wave == 1) ch = sweep_quadrant<R, -1, +1>(Ts, Cs, lane, keep);
-        else if (wave == 2) ch = sweep_quadrant<R, +1, -1>(Ts, Cs, lane, keep);
-        else                ch = sweep_quadrant<R, -1, -1>(Ts, Cs, lane, keep);
-        if (__any(ch) && lane == 0) atomicOr(&L.round, 1u << (round & 31));
-        __syncthreads();
-        last_changed = (L.round >> (round & 31)) & 1u;
-        if (!last_changed || round + 1 >= a.max_rounds) break;
-    }
-
-    // ---- write back changed cells, collect side flags (and entering values, ordered mode)
-    unsigned fl = 0;
-    R kmin_self = INF, kmin[4] = {INF, INF, INF, INF};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int ry = (tid >> 4) + 16 * k;
-        const int64_t gy = y0 + ry;
-        R nv[4];
-        bool any = false;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            nv[e] = Ts[(ry + 1) * kLds + cx + e + 1];
-            any |= nv[e] < told[4 * k + e];
-            if (nv[e] < told[4 * k + e] * keep) {
-                kmin_self = umin(kmin_self, nv[e]);
-                // A neighbour can only improve if this edge value undercuts the neighbour's
-                // adjacent cell (the halo value, stale => larger => conservative).
-                const int lx = cx + e + 1, ly = ry + 1;
-                if (ry == 0 && nv[e] < Ts[lx]) { fl |= 1u; kmin[0] = umin(kmin[0], nv[e]); }
-                if (ry == kTile - 1 && nv[e] < Ts[(kLds - 1) * kLds + lx]) { fl |= 2u; kmin[1] = umin(kmin[1], nv[e]); }
-                if (cx + e == 0 && nv[e] < Ts[ly * kLds]) { fl |= 4u; kmin[2] = umin(kmin[2], nv[e]); }
-                if (cx + e == kTile - 1 && nv[e] < Ts[ly * kLds + kLds - 1]) { fl |= 8u; kmin[3] = umin(kmin[3], nv[e]); }
-                const int64_t gx = x0 + cx + e;  // subdomain edges inside a partial tile (DD)
-                if (gy == a.H - 1 && ry != kTile - 1) fl |= 32u;
-                if (gx == a.W - 1 && cx + e != kTile - 1) fl |= 64u;
+    // PERSISTENT mode revisits a tile that changed IN PLACE, up to kPasses times: its interior
+    // is already in LDS and nobody else writes it while it is busy, so a pass only refreshes the
+    // halo ring, activates the neighbours its last write-back improved, and sweeps again -- no
+    // restaging, no queue round trip.  (List mode: one pass; a changed tile re-lists itself.)
+    constexpr int kPasses = COH ? 8 : 1;
+    for (int pass = 0;; ++pass) {
+        // ---- sweep rounds (quadrant directions concurrently, one per wave; `dirs` selects them)
+        const bool sweep = (L.dirs >> wave) & 1u;
+        bool last_changed = false;
+        if (a.max_rounds == 1) {  // single round: "changed" is read off the write-back below
+            if (sweep) {
+                if (wave == 0)      sweep_quadrant<R, +1, +1, false>(Ts, lane, keep);
+                else if (wave == 1) sweep_quadrant<R, -1, +1, false>(Ts, lane, keep);
+                else if (wave == 2) sweep_quadrant<R, +1, -1, false>(Ts, lane, keep);
+                else                sweep_quadrant<R, -1, -1, false>(Ts, lane, keep);
+            }
+            __syncthreads();
+        } else {
+            for (int round = 0;; ++round) {
+                bool ch = false;
+                if (sweep) {
+                    if (wave == 0)      ch = sweep_quadrant<R, +1, +1, true>(Ts, lane, keep);
+                    else if (wave == 1) ch = sweep_quadrant<R, -1, +1, true>(Ts, lane, keep);
+                    else if (wave == 2) ch = sweep_quadrant<R, +1, -1, true>(Ts, lane, keep);
+                    else                ch = sweep_quadrant<R, -1, -1, true>(Ts, lane, keep);
+                }
+                if (__any(ch) && lane == 0) atomicOr(&L.round, 1u << (round & 31));
+                __syncthreads();
+                last_changed = (L.round >> (round & 31)) & 1u;
+                if (!last_changed || round + 1 >= a.max_rounds) break;
             }
         }
-        if (any) {
-            if (full) {
-                T.st4(gy * a.W + x0 + cx, nv);
-            } else {
+
+        EIK_PROBE(2);
+        // ---- write back changed cells, collect side flags (and entering values, ordered mode)
+        unsigned fl = 0;
+        R kmin_self = INF, kmin[4] = {INF, INF, INF, INF};
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int64_t gx = x0 + cx + e;
-                    if (gy < a.H && gx < a.W && nv[e] < told[4 * k + e]) T.st(gy * a.W + gx, nv[e]);
+        for (int k = 0; k < 4; ++k) {
+            const int ry = (tid >> 4) + 16 * k;
+            const int64_t gy = y0 + ry;
+            R nv[4];
+            bool any = false;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                nv[e] = Ts[(ry + 1) * kLds + cx + e + 1];
+                any |= nv[e] < told[4 * k + e];
+                if (nv[e] < told[4 * k + e] * keep) {
+                    fl |= 128u;  // changed in this visit
+                    kmin_self = umin(kmin_self, nv[e]);
+                    // A neighbour can only improve if this edge value undercuts the neighbour's
+                    // adjacent cell (the halo value, stale => larger => conservative).
+                    const int lx = cx + e + 1, ly = ry + 1;
+                    if (ry == 0 && nv[e] < Ts[lx]) { fl |= 1u; kmin[0] = umin(kmin[0], nv[e]); }
+                    if (ry == kTile - 1 && nv[e] < Ts[(kLds - 1) * kLds + lx]) { fl |= 2u; kmin[1] = umin(kmin[1], nv[e]); }
+                    if (cx + e == 0 && nv[e] < Ts[ly * kLds]) { fl |= 4u; kmin[2] = umin(kmin[2], nv[e]); }
+                    if (cx + e == kTile - 1 && nv[e] < Ts[ly * kLds + kLds - 1]) { fl |= 8u; kmin[3] = umin(kmin[3], nv[e]); }
+                    const int64_t gx = x0 + cx + e;  // subdomain edges inside a partial tile (DD)
+                    if (gy == a.H - 1 && ry != kTile - 1) fl |= 32u;
+                    if (gx == a.W - 1 && cx + e != kTile - 1) fl |= 64u;
                 }
             }
+            if (any) {
+                if (full) {
+                    T.st4(gy * a.W + x0 + cx, nv);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int64_t gx = x0 + cx + e;
+                        if (gy < a.H && gx < a.W && nv[e] < told[4 * k + e]) T.st(gy * a.W + gx, nv[e]);
+                    }
+                }
+            }
+            if constexpr (kPasses > 1) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) told[4 * k + e] = nv[e];  // what memory holds now
+            }
+        }
+        if (fl) atomicOr(&L.flags, fl);
+        if (a.delta < INF) {
+            if (kmin_self < INF) atomicMin(&L.key[0], __float_as_uint((float)kmin_self));
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (kmin[q] < INF) atomicMin(&L.key[q + 1], __float_as_uint((float)kmin[q]));
+        }
+        if (tid == 0) L.last = a.max_rounds == 1 ? -1 : (int)last_changed;  // -1: see flags bit 7
+        if constexpr (COH) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+        __syncthreads();
+        if constexpr (kPasses > 1) {
+            const unsigned f = L.flags;  // uniform
+            if (!(f & 128u) || pass + 1 >= kPasses || a.max_rounds != 1) break;
+            if (tid == 0 && a.visits) atomicAdd(a.visits + 1, 1ull);  // in-place passes (stats)
+            activate_neighbours(a, tile, f, L.key, 0, 0u);  // lanes 0..4 (T already drained)
+            Ts[h] = load_halo();
+            __syncthreads();  // every wave has read L.flags and its halo side is in
+            if (tid == 0) {
+                L.flags = 0;
+                L.dirs = 0xFu;  // a self revisit: every direction
+            }
+        } else {
+            break;
         }
     }
-    if (fl) atomicOr(&L.flags, fl);
-    if (a.delta < INF) {
-        if (kmin_self < INF) atomicMin(&L.key[0], __float_as_uint((float)kmin_self));
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-            if (kmin[q] < INF) atomicMin(&L.key[q + 1], __float_as_uint((float)kmin[q]));
-    }
-    if (tid == 0) L.last = last_changed;
-    if constexpr (COH) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
-    __syncthreads();
+    EIK_PROBE(3);
 }
 
-// Activations after a tile visit: thread q < 5 handles one candidate (their atomics overlap).
+// Activations after a tile visit: the neighbours, and the tile itself if it changed.
 template <typename R>
 __device__ __forceinline__ void activate_after(const Fim2dArgs& a, int tile, const TileLds<R>& L, int list,
                                                unsigned stamp) {
-    const int tid = threadIdx.x;
-    if (tid >= 5) return;
     const unsigned f = L.flags;
-    const int map = tile / a.tiles_per_map;
-    const int rem = tile - map * a.tiles_per_map;
-    const int ty = rem / a.ntx, tx = rem - (rem / a.ntx) * a.ntx;
-    const int base = map * a.tiles_per_map;
-    const float kk = __uint_as_float(L.key[tid]);
-    if (tid == 0 && L.last) {
+    activate_neighbours(a, tile, f, L.key, list, stamp);
+    if (threadIdx.x == 0 && (L.last < 0 ? (f & 128u) != 0u : L.last != 0)) {
         if (a.mode == kModePersistent)
-            atomicOr(&a.qstate[tile], kPending);  // busy: re-queued by its own finish
+            atomicOr(&a.qstate[tile], kPending | kSelf);  // busy: re-queued by its own finish
         else
-            enqueue(a, tile, list, stamp, kk);
-    }
-    if (tid == 1 && (f & 1u) && ty > 0) activate(a, base + rem - a.ntx, list, stamp, kk);
-    if (tid == 2 && (f & 2u) && ty + 1 < a.nty) activate(a, base + rem + a.ntx, list, stamp, kk);
-    if (tid == 3 && (f & 4u) && tx > 0) activate(a, base + rem - 1, list, stamp, kk);
-    if (tid == 4 && (f & 8u) && tx + 1 < a.ntx) activate(a, base + rem + 1, list, stamp, kk);
-    if (tid == 0 && a.edge_dirty) {  // subdomain edges (domain decomposition)
-        unsigned e = 0;
-        if ((f & 1u) && ty == 0) e |= 1u;
-        if (((f & 2u) || (f & 32u)) && ty + 1 == a.nty) e |= 2u;
-        if ((f & 4u) && tx == 0) e |= 4u;
-        if (((f & 8u) || (f & 64u)) && tx + 1 == a.ntx) e |= 8u;
-        if (e) atomicOr(a.edge_dirty, e);
+            enqueue(a, tile, list, stamp, __uint_as_float(L.key[0]));
     }
 }
 
@@ -433,6 +523,7 @@ __global__ __launch_bounds__(kThreads) void fim2d_sweep_kernel(Fim2dArgs a) {
     const unsigned stamp = a.iter + 2;  // "enqueued for iteration iter+1"
     const float thr = __uint_as_float(a.minkey[cur]) + a.delta;  // ordering window of this launch
     const R keep = (R)a.keep;
+    if (tid == 0) L.dirs = 0xFu;  // list mode: every visit runs all four quadrant sweeps
 
     for (int it = blockIdx.x; it < cnt; it += gridDim.x) {
         const int tile = a.lists[(int64_t)cur * a.capacity + it];
@@ -458,7 +549,7 @@ __global__ __launch_bounds__(kThreads) void fim2d_sweep_kernel(Fim2dArgs a) {
 // ------------------------------------------------------------------- PERSISTENT driver
 // Take a ticket and wait for its slot: the next queued tile, or -1 when the solve has ended
 // (no tile pending or busy) or failed.  ONE lane polls (relaxed agent-scope loads = sc1).
-__device__ __forceinline__ int qgrab(const Fim2dArgs& a) {
+__device__ __forceinline__ int qgrab(const Fim2dArgs& a, unsigned& trig) {
     if (__hip_atomic_load(a.qerror, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return -1;
     const unsigned long long pos = atomicAdd(a.qhead, 1ull);
     unsigned* slot = &a.qslot[pos & a.qmask];
@@ -471,7 +562,7 @@ __device__ __forceinline__ int qgrab(const Fim2dArgs& a) {
             const int tile = (int)(v - 1u);
             // pending -> busy before T is read: any activation from here on makes the finish
             // re-queue the tile, so no update is lost
-            atomicExch(&a.qstate[tile], kBusy);
+            trig = atomicExch(&a.qstate[tile], kBusy);  // consumed after the staging loads
             return tile;
         }
         if ((spin & 7u) == 7u) {
@@ -489,7 +580,6 @@ __device__ __forceinline__ int qgrab(const Fim2dArgs& a) {
 // Retire a visited tile (after its activations completed): re-queue it if it was activated
 // while busy (it stays counted), else it stops counting as active.
 __device__ __forceinline__ void qfinish(const Fim2dArgs& a, int tile) {
-    if (atomicAdd(a.visits, 1ull) >= a.qbudget) atomicOr(a.qerror, 2u);
     const unsigned old = atomicAnd(&a.qstate[tile], ~kBusy);
     if (old & kPending)
         qslot_put(a, tile);
@@ -503,23 +593,39 @@ __global__ __launch_bounds__(kThreads) void fim2d_persist_kernel(Fim2dArgs a) {
     init_guard_rows(L);
     const R keep = (R)a.keep;
     int tile = -1;
+    unsigned nvis = 0;  // wave 0 lane 0: visits not yet added to the global counter
     for (;;) {
-        // wave 0 retires the previous tile (lanes 0..4 activate, lane 0 finishes) and takes the
-        // next one; the other waves go straight to the barrier
+        // wave 0 retires the previous tile (lanes 0..4 activate, then lane 0 finishes) while
+        // wave 1 takes the next one; waves 2 and 3 go straight to the barrier
         if (threadIdx.x < 64) {
             if (tile >= 0) {
+                EIK_PROBE(4);
                 activate_after(a, tile, L, 0, 0u);
                 // the activations' counter increments complete before the finish decrements
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (threadIdx.x == 0) qfinish(a, tile);
+                if (threadIdx.x == 0) {
+                    qfinish(a, tile);
+                    if (++nvis == 64u) {  // visit cap (negative costs never converge)
+                        if (atomicAdd(a.visits, 64ull) + 64ull >= a.qbudget) atomicOr(a.qerror, 2u);
+                        nvis = 0;
+                    }
+                }
             }
-            if (threadIdx.x == 0) L.tile = qgrab(a);
+            EIK_PROBE(5);
+        } else if (threadIdx.x == 64) {
+            unsigned trig = 0;
+            const int t = qgrab(a, trig);
+            L.tile = t;
+            L.dirs = sweep_dirs(trig);
+            if (t >= 0) EIK_VISIT(trig, L.dirs);
         }
         __syncthreads();
+        EIK_PROBE(6);
         tile = __builtin_amdgcn_readfirstlane(L.tile);
         if (tile < 0) break;  // uniform: solve finished (or failed)
         process_tile<R, true>(a, tile, L, keep);  // sc1 loads; sc1 stores drained + barrier
     }
+    if (threadIdx.x == 0 && nvis) atomicAdd(a.visits, (unsigned long long)nvis);
 }
 // ------------------------------------------------------------------------ init / seeding
 // T = inf everywhere; marks / keys / queue state cleared.
@@ -552,7 +658,7 @@ __global__ void fim2d_seed_kernel(Fim2dArgs a, const int64_t* __restrict__ goals
     static_cast<R*>(a.T)[(int64_t)m * a.H * a.W + gy * a.W + gx] = R(0);
     const int tile = m * a.tiles_per_map + (int)(gy / kTile) * a.ntx + (int)(gx / kTile);
     if (a.mode == kModePersistent) {
-        qpush(a, tile);
+        qpush(a, tile, kSelf);
         return;
     }
     a.mark[tile] = 1;  // enqueued for iteration 0
@@ -583,7 +689,7 @@ __global__ void fim2d_merge_ghost_kernel(Fim2dArgs a, int side, const R* __restr
             ty = (int)(i / kTile);
             tx = side == 2 ? 0 : a.ntx - 1;
         }
-        activate(a, ty * a.ntx + tx, a.iter % 3, a.iter + 1, (float)v);
+        activate(a, ty * a.ntx + tx, a.iter % 3, a.iter + 1, (float)v, kFromN << side);
     }
 }
 
