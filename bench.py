@@ -146,6 +146,9 @@ def main():
         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
         "traffic": traffic,
         "alg_bytes_per_launch": round(alg_bytes / max(launches, 1)),
+        # one read of cost + one write of T per cell, and the FIM redundancy over it
+        "lower_bound_gbs": round(8 * H * W / (el / args.steps) / 1e9, 2),
+        "redundancy": round(alg_bytes / max(launches, 1) / (8 * H * W), 2) if launches else None,
         "avg_launch_us": round(sweep_ms * 1e3 / max(launches, 1), 2),
         "instrumented_ms_per_step": round(el_i / args.steps * 1e3, 4),
         "launches_per_solve": round(launches / args.steps, 1),

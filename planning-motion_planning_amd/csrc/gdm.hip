@@ -10,7 +10,7 @@
 // Arithmetic is IEEE fp64 with contraction disabled.  The one deliberate difference: the
 // reference squares numpy scalars with `x**2`, which goes through glibc pow() and is not
 // always correctly rounded; the device uses the exact product x*x (<= 1 ulp per square,
-// tolerance stated in tests/test_gpu_parity.py).
+// tolerance stated in tests/test_gpu_path.py).
 #include "eik_common.hpp"
 #include "eik_kernels.hpp"
 
