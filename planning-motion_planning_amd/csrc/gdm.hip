@@ -60,107 +60,202 @@ __device__ __forceinline__ double interp2_patch(double a, double b, const double
     return b == 0 ? a00 + a10 * a : a00 + a10 * a + a01 * b + a11 * a * b;
 }
 
+// interp2_patch with the four cases of :327-336 evaluated and selected (no divergent branches on
+// the walker's critical path; same operations in the same order as each case)
+__device__ __forceinline__ double interp2_sel(double a, double b, double g00, double g01, double g10, double g11) {
+    const double a00 = g00;
+    const double a10 = g01 - g00;
+    const double a01 = g10 - g00;
+    const double a11 = g11 + g00 - g01 - g10;
+    const double ra = a00 + a10 * a;            // b == 0
+    const double rb = a00 + a01 * b;            // a == 0
+    const double rf = ra + a01 * b + a11 * a * b;
+    return a == 0 ? (b == 0 ? a00 : rb) : (b == 0 ? ra : rf);
+}
+
 __device__ __forceinline__ double norm2(double a, double b) { return __builtin_sqrt(a * a + b * b); }
 
 enum { kGdmDone = 0, kGdmFallback = 1, kGdmError = 2 };
 
-// LDS window around the walker: the inf-aware normalised gradient (Gnx, Gny) of a 32 x 32 node
-// block is computed by all 64 lanes when the walker's 2 x 2 interpolation corners leave the
-// block (every ~30 steps at tau = 0.5); each step then reads 8 values from LDS.  The gradient at
-// a node depends on T only, so precomputing it is exactly the reference's per-step
-// computeGradient evaluated earlier.
-constexpr int kG = 32;  // gradient block side (nodes)
+// Path kernel layout: ONE workgroup of 16 waves.  Wave 0 is the walker: it runs the reference
+// loop (:173-232) step by step, reading the inf-aware normalised gradient (Gnx, Gny) of the four
+// bilinear corners from an LDS window of 64 x 64 nodes.  Waves 1..15 are builders: they compute
+// the gradient of a window (computeGradient's body, :262-297, at every node of the window) from
+// T in HBM into one of two LDS buffers.  When the walker comes within kPrefetch nodes of an
+// inner window edge it requests the window centred on itself into the idle buffer and keeps
+// walking; when it leaves the current window it switches (waiting only if the build is still
+// running, or if it turned away from the prefetched window).  The gradient at a node depends on
+// T only, so precomputing it is exactly the reference's per-step computeGradient evaluated
+// earlier: the path is bit-identical to the single-lane form.
+constexpr int kPW = 64;                          // window side (nodes), one builder lane per column
+constexpr int kPathThreads = 1024;               // 16 waves: walker + 15 builders
+constexpr int kBuilders = kPathThreads / 64 - 1;
+constexpr int kRowsPerBuilder = (kPW + kBuilders - 1) / kBuilders;
+constexpr int kPrefetch = 16;                    // nodes from an inner edge that trigger a prefetch
+constexpr unsigned long long kPathSpin = 200000000ull;  // 2 s of s_memrealtime (100 MHz): never hang
 
-struct Win {
-    double gx[kG][kG + 1], gy[kG][kG + 1];
-    double t[kG + 2][kG + 3];  // T on the block + 1-node margin
-    int64_t x0, y0;
+struct PathLds {
+    double2 g[2][kPW][kPW];  // (Gnx, Gny) per node, 2 x 64 KiB
+    long long req_x0, req_y0;
+    int req_seq;             // walker -> builders: request number (-1: quit)
+    int req_b;               // target buffer of the request
+    int done;                // builders -> walker: finished builds x kBuilders
 };
 
-// computeGradient body at (j, i) reading the T window (FastMarching.py:262-297)
-__device__ void grad_win(const Win& w, int64_t m, int64_t n, int64_t j, int64_t i, double& gnx, double& gny) {
-#define TW(J, I) w.t[(J) - w.y0 + 1][(I) - w.x0 + 1]
-    double gy, gx;
-    if (j == 0)
-        gy = TW(1, i) - TW(0, i);
-    else if (j == m - 1)
-        gy = TW(j, i) - TW(j - 1, i);
-    else if (__builtin_isinf(TW(j + 1, i)))
-        gy = __builtin_isinf(TW(j - 1, i)) ? 0.0 : TW(j, i) - TW(j - 1, i);
-    else
-        gy = __builtin_isinf(TW(j - 1, i)) ? TW(j + 1, i) - TW(j, i) : (TW(j + 1, i) - TW(j - 1, i)) / 2;
-    if (i == 0)
-        gx = TW(j, 1) - TW(j, 0);
-    else if (i == n - 1)
-        gx = TW(j, i) - TW(j, i - 1);
-    else if (__builtin_isinf(TW(j, i + 1)))
-        gx = __builtin_isinf(TW(j, i - 1)) ? 0.0 : TW(j, i) - TW(j, i - 1);
-    else
-        gx = __builtin_isinf(TW(j, i - 1)) ? TW(j, i + 1) - TW(j, i) : (TW(j, i + 1) - TW(j, i - 1)) / 2;
-#undef TW
-    const double den = __builtin_sqrt(gx * gx + gy * gy);
-    gnx = gx / den;
-    gny = gy / den;
+// Builder wave `w` fills rows w, w + kBuilders, ... of window buffer b (origin x0, y0).  Every T
+// load of a wave is issued before any is used (5 neighbours x kRowsPerBuilder rows per lane), so
+// a build costs about one HBM/L2 round trip plus the arithmetic.
+template <typename R>
+__device__ void build_window(PathLds& s, const R* __restrict__ T, int64_t H, int64_t W, int b, int64_t x0,
+                             int64_t y0, int w) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = x0 + lane;
+    const bool col_ok = i < W;
+    const int64_t ic = col_ok ? i : W - 1;
+    const int64_t iw = ic > 0 ? ic - 1 : 0, ie = ic + 1 < W ? ic + 1 : W - 1;
+    double c[kRowsPerBuilder], nn[kRowsPerBuilder], ss[kRowsPerBuilder], ww[kRowsPerBuilder], ee[kRowsPerBuilder];
+#pragma unroll
+    for (int k = 0; k < kRowsPerBuilder; ++k) {
+        const int r = w + k * kBuilders;
+        int64_t j = y0 + r;
+        j = (r < kPW && j < H) ? j : H - 1;
+        const int64_t jn = j > 0 ? j - 1 : 0, js = j + 1 < H ? j + 1 : H - 1;
+        c[k] = (double)T[j * W + ic];
+        nn[k] = (double)T[jn * W + ic];
+        ss[k] = (double)T[js * W + ic];
+        ww[k] = (double)T[j * W + iw];
+        ee[k] = (double)T[j * W + ie];
+    }
+#pragma unroll
+    for (int k = 0; k < kRowsPerBuilder; ++k) {
+        const int r = w + k * kBuilders;
+        const int64_t j = y0 + r;
+        if (r >= kPW || j >= H || !col_ok) continue;
+        double gy, gx;  // FastMarching.py:262-294 with the five loaded values
+        if (j == 0)
+            gy = ss[k] - c[k];
+        else if (j == H - 1)
+            gy = c[k] - nn[k];
+        else if (__builtin_isinf(ss[k]))
+            gy = __builtin_isinf(nn[k]) ? 0.0 : c[k] - nn[k];
+        else
+            gy = __builtin_isinf(nn[k]) ? ss[k] - c[k] : (ss[k] - nn[k]) / 2;
+        if (i == 0)
+            gx = ee[k] - c[k];
+        else if (i == W - 1)
+            gx = c[k] - ww[k];
+        else if (__builtin_isinf(ee[k]))
+            gx = __builtin_isinf(ww[k]) ? 0.0 : c[k] - ww[k];
+        else
+            gx = __builtin_isinf(ww[k]) ? ee[k] - c[k] : (ee[k] - ww[k]) / 2;
+        const double den = __builtin_sqrt(gx * gx + gy * gy);  // :296-297
+        s.g[b][r][lane] = make_double2(gx / den, gy / den);
+    }
 }
 
 template <typename R>
-__device__ void win_load(Win& w, const R* __restrict__ T, int64_t H, int64_t W, int64_t i, int64_t j) {
-    int64_t x0 = i - kG / 2, y0 = j - kG / 2;
-    x0 = x0 + kG > W ? W - kG : x0;
-    y0 = y0 + kG > H ? H - kG : y0;
-    x0 = x0 < 0 ? 0 : x0;
-    y0 = y0 < 0 ? 0 : y0;
-    __syncthreads();
-    const int lane = threadIdx.x;
-    if (lane == 0) {
-        w.x0 = x0;
-        w.y0 = y0;
+__device__ void path_builder(PathLds& s, const R* __restrict__ T, int64_t H, int64_t W) {
+    const int w = (int)(threadIdx.x >> 6) - 1;
+    int seen = 0;
+    unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        const int q = __hip_atomic_load(&s.req_seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (q < 0) return;
+        if (q == seen) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kPathSpin) return;  // walker gone: give up
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        seen = q;
+        build_window<R>(s, T, H, W, s.req_b, s.req_x0, s.req_y0, w);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(&s.done, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        t0 = __builtin_amdgcn_s_memrealtime();
     }
-    for (int e = lane; e < (kG + 2) * (kG + 2); e += 64) {
-        const int r = e / (kG + 2), c = e - r * (kG + 2);
-        const int64_t gy = y0 - 1 + r, gx = x0 - 1 + c;
-        w.t[r][c] = (gy >= 0 && gy < H && gx >= 0 && gx < W) ? (double)T[gy * W + gx] : 0.0;
-    }
-    __syncthreads();
-    for (int e = lane; e < kG * kG; e += 64) {
-        const int r = e / kG, c = e - r * kG;
-        const int64_t gy = y0 + r, gx = x0 + c;
-        if (gy < H && gx < W) grad_win(w, H, W, gy, gx, w.gx[r][c], w.gy[r][c]);
-    }
-    __syncthreads();
 }
 
 template <typename R>
-__global__ __launch_bounds__(64) void gdm2d_kernel(Gdm2dArgs a) {
-    __shared__ Win w;
+__global__ __launch_bounds__(kPathThreads) void gdm2d_kernel(Gdm2dArgs a) {
+    __shared__ PathLds s;
     const R* __restrict__ T = static_cast<const R*>(a.T);
     const int64_t H = a.H, W = a.W;
+    if (threadIdx.x == 0) {
+        s.req_seq = 0;
+        s.done = 0;
+    }
+    __syncthreads();
+    if (threadIdx.x >= 64) {
+        path_builder<R>(s, T, H, W);
+        return;
+    }
+    // ---- walker (wave 0; every lane runs the same uniform loop, lane 0 stores)
     const bool lead = threadIdx.x == 0;
     double* out = a.out;
     int status = kGdmDone;
-    double px = a.ix, py = a.iy;  // gamma[-1], kept in registers (all lanes)
+    double px = a.ix, py = a.iy;  // gamma[-1], kept in registers
     if (lead) {
         out[0] = px;
         out[1] = py;
     }
     int64_t n = 1;
     const double tau = a.tau;
-    w.x0 = -((int64_t)1 << 40);
-    w.y0 = -((int64_t)1 << 40);
-    __syncthreads();
+    // window origins of the two buffers (scalars, not an indexed array: no private->LDS promotion)
+    int64_t wx0 = -((int64_t)1 << 40), wx1 = wx0, wy0 = wx0, wy1 = wx0;
+    int cur = 0, seq = 0;
+    bool pending = false;
+    const int64_t xmax = W > kPW ? W - kPW : 0, ymax = H > kPW ? H - kPW : 0;
+    auto issue = [&](int b, int64_t i, int64_t j) {  // build the window centred on (i, j) into b
+        int64_t x0 = i - kPW / 2, y0 = j - kPW / 2;
+        x0 = x0 > xmax ? xmax : x0 < 0 ? 0 : x0;
+        y0 = y0 > ymax ? ymax : y0 < 0 ? 0 : y0;
+        if (b) { wx1 = x0; wy1 = y0; } else { wx0 = x0; wy0 = y0; }
+        s.req_x0 = x0;
+        s.req_y0 = y0;
+        s.req_b = b;
+        __hip_atomic_store(&s.req_seq, ++seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto wait_built = [&]() -> bool {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(&s.done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < seq * kBuilders) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kPathSpin) return false;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        return true;
+    };
+    auto inside = [&](int b, int64_t i, int64_t j) {
+        const int64_t x0 = b ? wx1 : wx0, y0 = b ? wy1 : wy0;
+        return i >= x0 && j >= y0 && i + 1 < x0 + kPW && j + 1 < y0 + kPW;
+    };
     for (long k = 0; k < a.steps; ++k) {
         if (__builtin_isnan(px) || __builtin_isnan(py)) { status = kGdmError; break; }
         const uint32_t i = (uint32_t)__builtin_trunc(px), j = (uint32_t)__builtin_trunc(py);
         if (i + 1 >= (uint64_t)W || j + 1 >= (uint64_t)H) { status = kGdmError; break; }
-        // the 2 x 2 interpolation corners must lie in the gradient block
-        if ((int64_t)i < w.x0 || (int64_t)j < w.y0 || (int64_t)i + 1 >= w.x0 + kG || (int64_t)j + 1 >= w.y0 + kG)
-            win_load<R>(w, T, H, W, i, j);
-        const int li = (int)(i - w.x0), lj = (int)(j - w.y0);
-        const double gx[2][2] = {{w.gx[lj][li], w.gx[lj][li + 1]}, {w.gx[lj + 1][li], w.gx[lj + 1][li + 1]}};
-        const double gy[2][2] = {{w.gy[lj][li], w.gy[lj][li + 1]}, {w.gy[lj + 1][li], w.gy[lj + 1][li + 1]}};
+        if (!inside(cur, i, j)) {  // the 2 x 2 interpolation corners left the window
+            const int nb = seq == 0 ? 0 : 1 - cur;
+            bool have = false;
+            if (pending) {
+                pending = false;
+                if (!wait_built()) { status = kGdmError; break; }
+                have = inside(nb, i, j);
+            }
+            if (!have) {
+                issue(nb, i, j);
+                if (!wait_built()) { status = kGdmError; break; }
+            }
+            cur = nb;
+        }
+        const int64_t cx0 = cur ? wx1 : wx0, cy0 = cur ? wy1 : wy0;
+        if (!pending && ((i - cx0 < kPrefetch && cx0 > 0) || (cx0 + kPW - 2 - i < kPrefetch && cx0 < xmax) ||
+                         (j - cy0 < kPrefetch && cy0 > 0) || (cy0 + kPW - 2 - j < kPrefetch && cy0 < ymax))) {
+            issue(1 - cur, i, j);
+            pending = true;
+        }
+        const int li = (int)(i - cx0), lj = (int)(j - cy0);
+        const double2 g00 = s.g[cur][lj][li], g01 = s.g[cur][lj][li + 1];
+        const double2 g10 = s.g[cur][lj + 1][li], g11 = s.g[cur][lj + 1][li + 1];
         const double fa = px - i, fb = py - j;
-        double dx = interp2_patch(fa, fb, gx);
-        double dy = interp2_patch(fa, fb, gy);
+        double dx = interp2_sel(fa, fb, g00.x, g01.x, g10.x, g11.x);  // :175
+        double dy = interp2_sel(fa, fb, g00.y, g01.y, g10.y, g11.y);  // :176
         if (__builtin_isnan(dx) || __builtin_isnan(dy)) {
             // NaN fallback (:178-218) as the reference behaves under numpy 2: the neighbour
             // probe `np.uint32(nearN + [0,-1])` raises OverflowError, caught at :217.
@@ -168,9 +263,9 @@ __global__ __launch_bounds__(64) void gdm2d_kernel(Gdm2dArgs a) {
                 int64_t nx = (int64_t)__builtin_rint(px), ny = (int64_t)__builtin_rint(py);
                 bool empty = false, oob = false;
                 for (;;) {
-                    const int64_t wx = nx < 0 ? nx + W : nx, wy = ny < 0 ? ny + H : ny;
-                    if (wx < 0 || wy < 0 || wx >= W || wy >= H) { oob = true; break; }
-                    if (!__builtin_isinf(tv(T, W, wy, wx))) break;
+                    const int64_t qx = nx < 0 ? nx + W : nx, qy = ny < 0 ? ny + H : ny;
+                    if (qx < 0 || qy < 0 || qx >= W || qy >= H) { oob = true; break; }
+                    if (!__builtin_isinf(tv(T, W, qy, qx))) break;
                     --n;
                     if (n == 0) { empty = true; break; }
                     nx = (int64_t)__builtin_rint(out[2 * (n - 1)]);
@@ -188,18 +283,12 @@ __global__ __launch_bounds__(64) void gdm2d_kernel(Gdm2dArgs a) {
             status = kGdmFallback;
             break;
         }
-        double sx, sy;
-        if (norm2(dx, dy) < 0.01) {  // :220-224
-            const double dnx = dx / __builtin_sqrt(dx * dx + dy * dy);
-            const double dny = dy / __builtin_sqrt(dx * dx + dy * dy);
-            sx = px - tau * dnx;
-            sy = py - tau * dny;
-        } else {  // :225-229 (dy normalised with the already-normalised dx)
-            dx = dx / __builtin_sqrt(dx * dx + dy * dy);
-            dy = dy / __builtin_sqrt(dx * dx + dy * dy);
-            sx = px - tau * dx;
-            sy = py - tau * dy;
-        }
+        // |(dx, dy)| is the same value in the test (:220) and both normalisations (:221-227)
+        const double nrm = __builtin_sqrt(dx * dx + dy * dy);
+        const double dxn = dx / nrm;  // both branches
+        // :220-224 (|g| < 0.01: unit step) or :225-229 (dy normalised with the already-normalised dx)
+        const double dyn = nrm < 0.01 ? dy / nrm : dy / __builtin_sqrt(dxn * dxn + dy * dy);
+        const double sx = px - tau * dxn, sy = py - tau * dyn;
         if (n >= a.cap) { status = kGdmError; break; }
         if (lead) {
             out[2 * n] = sx;
@@ -208,8 +297,11 @@ __global__ __launch_bounds__(64) void gdm2d_kernel(Gdm2dArgs a) {
         ++n;
         px = sx;
         py = sy;
-        if (norm2(sx - a.ex, sy - a.ey) < 1.5) break;  // :231-232
+        // :231-232  sqrt(e) < 1.5  <=>  e < 2.25 for a correctly rounded sqrt (2.25 = 1.5^2 exactly)
+        const double ex = sx - a.ex, ey = sy - a.ey;
+        if (ex * ex + ey * ey < 2.25) break;
     }
+    __hip_atomic_store(&s.req_seq, -1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);  // builders exit
     if (lead) {
         if (status == kGdmDone && n < a.cap) {  // :234
             out[2 * n] = a.ex;
@@ -223,9 +315,9 @@ __global__ __launch_bounds__(64) void gdm2d_kernel(Gdm2dArgs a) {
 
 hipError_t gdm2d(const Gdm2dArgs& a, bool f64, hipStream_t st) {
     if (f64)
-        hipLaunchKernelGGL(gdm2d_kernel<double>, dim3(1), dim3(64), 0, st, a);
+        hipLaunchKernelGGL(gdm2d_kernel<double>, dim3(1), dim3(kPathThreads), 0, st, a);
     else
-        hipLaunchKernelGGL(gdm2d_kernel<float>, dim3(1), dim3(64), 0, st, a);
+        hipLaunchKernelGGL(gdm2d_kernel<float>, dim3(1), dim3(kPathThreads), 0, st, a);
     return hipGetLastError();
 }
 
