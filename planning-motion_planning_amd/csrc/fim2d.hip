@@ -241,10 +241,22 @@ constexpr int kCsOff = (kLds + 1) * kLds;  // elements
 // computes +inf or NaN and its ds_min / min / `<` are no-ops.  TRACK: also report whether any
 // cell decreased by more than the tolerance (only needed for multi-round visits; single-round
 // visits read it off the write-back).
+// Software pipeline depth of a sweep: the LDS reads of step s + kAhead are issued at step s,
+// so the ~100-cycle LDS round trip overlaps kAhead steps of the Godunov chain instead of being
+// exposed once per step.  Reading ahead is safe: a lane's own column is written only by itself,
+// the downstream-x column (lane l+1) reaches row r one step after lane l, and the upstream-x
+// value of lanes 1..63 comes from the DPP register path (the LDS upstream-x read serves lane 0,
+// whose upstream column is the halo, which no sweep writes).  Another wave's concurrent ds_min
+// may make a pre-read value stale (larger): that only delays convergence -- a visit whose
+// sweeps changed nothing had no concurrent writes, so its reads were exact.
+constexpr int kAhead = 4;
+
 template <typename R, int DX, int DY, bool TRACK>
 __device__ __forceinline__ bool sweep_quadrant(R* __restrict__ Ts, int lane, R keep) {
     constexpr int S = (int)sizeof(R);
     constexpr int kRow = kLds * S;
+    constexpr int D = kAhead;
+    static_assert((2 * kTile) % D == 0, "pipeline depth must divide the step count");
     char* const base = reinterpret_cast<char*>(Ts);
     auto ld = [&](int off) { return *reinterpret_cast<const R*>(base + off); };
     const int col = (DX > 0 ? lane : kTile - 1 - lane) + 1;
@@ -259,25 +271,33 @@ __device__ __forceinline__ bool sweep_quadrant(R* __restrict__ Ts, int lane, R k
     bool changed = false;
     // the upstream halo row value is the lane's "previous row" result before it starts
     R cur = ld((DY > 0 ? 0 : kLds - 1) * kRow + col * S);
-    int o = clampb(raw);
-    R p_old = ld(o), p_dnx = ld(o + DX * S), p_dny = ld(o + DY * kRow), p_upx = ld(o - DX * S),
-      p_c = ld(o + kCsOff * S);
-#pragma clang loop unroll_count(2)
-    for (int s = 0; s < 2 * kTile; ++s) {
-        const R old = p_old, dnx = p_dnx, dny = p_dny, uxh = p_upx, c = p_c;
-        const int oc = o;
+    int q_o[D];
+    R q_old[D], q_dnx[D], q_dny[D], q_upx[D], q_c[D];
+    auto fetch = [&](int u) {
+        const int o = clampb(raw);
         raw += DY * kRow;
-        o = clampb(raw);  // next step's loads issue before this step's ds_min (no intra-wave RAW)
-        p_old = ld(o);
-        p_dnx = ld(o + DX * S);
-        p_dny = ld(o + DY * kRow);
-        p_upx = ld(o - DX * S);
-        p_c = ld(o + kCsOff * S);
-        const R upx = wave_shr1(cur, uxh);  // lane 0: halo column
-        const R w = godunov2_fast(umin(upx, dnx), umin(cur, dny), c);
-        lds_min(reinterpret_cast<R*>(base + oc), w);
-        if constexpr (TRACK) changed |= w < old * keep;
-        cur = umin(w, old);  // NaN (both-inf case) sorts above every value: keeps old
+        q_o[u] = o;
+        q_old[u] = ld(o);
+        q_dnx[u] = ld(o + DX * S);
+        q_dny[u] = ld(o + DY * kRow);
+        q_upx[u] = ld(o - DX * S);
+        q_c[u] = ld(o + kCsOff * S);
+    };
+#pragma unroll
+    for (int u = 0; u < D; ++u) fetch(u);
+    for (int s = 0; s < 2 * kTile; s += D) {
+#pragma unroll
+        for (int u = 0; u < D; ++u) {
+            const R upx = wave_shr1(cur, q_upx[u]);  // lane 0: halo column
+            const R w = godunov2_fast(umin(upx, q_dnx[u]), umin(cur, q_dny[u]), q_c[u]);
+            lds_min(reinterpret_cast<R*>(base + q_o[u]), w);
+            if constexpr (TRACK) changed |= w < q_old[u] * keep;
+            cur = umin(w, q_old[u]);  // NaN (both-inf case) sorts above every value: keeps old
+            fetch(u);  // refill the slot: step s + u + D (past the last step: clamped halo rows)
+            // keep each step's instructions in place: hoisting a later step's use of a slot
+            // above this point would make the compiler wait for the newest reads (lgkmcnt(0))
+            __builtin_amdgcn_sched_barrier(0);
+        }
     }
     return changed;
 }
