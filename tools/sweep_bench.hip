@@ -1,5 +1,7 @@
 // Microbenchmark (not product code): cycles per skewed-sweep step of the FIM tile body in
-// isolation, for variants of the step.  One 64x64 fp32 tile staged in LDS per workgroup, the
+// isolation, for variants of the step.  (A register-resident variant -- each wave's tile copy in
+// VGPRs with a skewed layout, no LDS per step -- measured 108 cycles/step alone and 138 with its
+// per-pass LDS load/merge, vs 126 for V0, and lost intra-pass sharing between waves: dropped.)  One 64x64 fp32 tile staged in LDS per workgroup, the
 // four quadrant sweeps run concurrently by the four waves, R repetitions, s_memtime around them.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/sweep_bench.hip -o /tmp/sweep_bench
 #include <hip/hip_runtime.h>
@@ -59,26 +61,6 @@ __global__ __launch_bounds__(256) void kern(const float* cost, float* out, unsig
     __syncthreads();
     float* Ts = Tbuf + kLds;
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-    if constexpr (V == 4 || V == 5) {  // register-resident sweep (product path); 5: sweep only
-        const int fx = (wave & 1) ? 63 : 0, fy = (wave & 2) ? 63 : 0;
-        float Creg[kTile], Rg[kTile];
-        load_skewed(Cs, Creg, opaque(lane), fx, fy);
-        if (V == 5) load_skewed(Ts, Rg, opaque(lane), fx, fy);
-        for (int r = 0; r < reps; ++r) {
-            if (V == 4) load_skewed(Ts, Rg, opaque(lane), fx, fy);
-            const float top = Ts[(fy ? kLds - 1 : 0) * kLds + (lane ^ fx) + 1];
-            const float bot = Ts[(fy ? 0 : kLds - 1) * kLds + (lane ^ fx) + 1];
-            const float left = Ts[((lane ^ fy) + 1) * kLds + (fx ? kLds - 1 : 0)];
-            const float right = Ts[((lane ^ fy) + 1) * kLds + (fx ? 0 : kLds - 1)];
-            sweep_regs(Rg, Creg, lane, top, bot, left, right);
-            if (V == 4) {
-#pragma unroll
-                for (int k = 0, u = opaque(lane); k < kTile; ++k) lds_min(Ts + skew_index(k, u, fx, fy), Rg[k]);
-            }
-            __syncthreads();
-        }
-        if (V == 5) for (int k = 0, u = opaque(lane); k < kTile; ++k) lds_min(Ts + skew_index(k, u, fx, fy), Rg[k]);
-    } else
     for (int r = 0; r < reps; ++r) {
         if (wave == 0) sweepv<V, +1, +1>(Ts, lane);
         else if (wave == 1) sweepv<V, -1, +1>(Ts, lane);
@@ -115,8 +97,6 @@ int main() {
         run<1>("V1 plain ds_write", cost, out, cyc, grid, reps);
         run<2>("V2 no LDS in loop", cost, out, cyc, grid, reps);
         run<3>("V3 ds_min, no sqrt", cost, out, cyc, grid, reps);
-        run<4>("V4 registers (product)", cost, out, cyc, grid, reps);
-        run<5>("V5 registers, sweep only", cost, out, cyc, grid, reps);
     }
     return 0;
 }
