@@ -54,6 +54,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-path", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-launch events (roofline)")
+    ap.add_argument("--no-extra", action="store_true", help="skip the C3 / C5 secondary measurements")
+    ap.add_argument("--extra-steps", type=int, default=5)
     ap.add_argument("--pmc-traffic", type=str, default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -181,6 +183,14 @@ def main():
     if rank == 0 and world == 1 and not args.no_path:
         out.update(ms_to_path(cost, ctx, fim, dev, stream, goal_g))
 
+    if rank == 0 and world == 1 and not args.no_extra:
+        del T
+        torch.cuda.empty_cache()
+        out["extra_configs"] = {
+            "C3": bench_batch(ctx, dev, stream, args.extra_steps),
+            "C5": bench_layers(ctx, dev, stream, cost, goal_g, args.extra_steps),
+        }
+
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cost, goal_g)
 
@@ -220,6 +230,94 @@ def ms_to_path(cost, ctx, fim, dev, stream, goal, start=(256, 256), reps=3):
         lens.append(n)
     return {"ms_to_path": round(float(np.median(tot)), 3), "ms_to_path_device": round(float(np.median(devs)), 3),
             "path_points": int(lens[0]), "path_status": int(st_d.item()), "path_from": list(start)}
+
+
+def timed_loop(fn, steps, warmup=1):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def bench_batch(ctx, dev, stream, steps, B=128, N=1024):
+    """configs[2]: 128 maps of 1024^2 (terrain seeds 1000..1127, one goal per map), ONE batched
+    persistent solve (tiles of all maps share the device FIFO).  A step = the whole batch."""
+    cost = torch.empty((B, N, N), dtype=torch.float32, device=dev)
+    goals = []
+    rng = np.random.default_rng(1000)
+    for b in range(B):
+        cost[b] = terrain.cost_block(0, 0, N, N, N, N, seed=1000 + b, device=dev)
+        while True:  # a goal on a finite, low-cost cell
+            gx, gy = (int(v) for v in rng.integers(N // 8, N - N // 8, 2))
+            if float(cost[b, gy, gx]) < 50:
+                break
+        goals.append((gx, gy))
+    T = torch.empty_like(cost)
+    fim = eikonal.Fim2d(ctx, B, N, N, L.EIK_F32)
+    sec = timed_loop(lambda: fim.solve(cost.data_ptr(), T.data_ptr(), goals, stream.cuda_stream), steps)
+    st = fim.stats()
+    reach = float(torch.isfinite(T).float().mean())
+    fim.close()
+    del cost, T
+    torch.cuda.empty_cache()
+    return {"workload": f"configs[2]: batch {B} x {N}x{N} terrain maps (seeds 1000..{1000 + B - 1}), one goal each",
+            "value": round(B * N * N / sec / 1e9, 4), "unit": "Gcells/s", "ms_per_step": round(sec * 1e3, 4),
+            "steps": steps, "tile_visits_per_solve": st["tile_visits"], "inplace_passes_per_solve": st["inplace_passes"],
+            "reached_fraction": round(reach, 4)}
+
+
+def bench_layers(ctx, dev, stream, cost2d, goal, steps, Lz=3):
+    """configs[4]: coupled (x, y, locomotion-mode) 4096 x 4096 x 3 costmap, [y][x][z] (FM3D
+    layout), unit spacing between layers (FastMarching3D semantics): mode 0 = the C2 raster,
+    mode 1 = 1.6 x it and impassable above cost 100, mode 2 = 0.8 x it with 1-in-5 impassable
+    64 x 64 blocks.  As the planner builds its FM3D volumes (Coupled_motion_planner.py:355-356)
+    the z ends are padded with +inf layers: 5 layers in memory, 3 solved (the layered solver,
+    fim2dl.hip).  Solve from (goal, mode 0); then the FM3D path from (256, 256, mode 0).
+    Gcells/s counts the 3 real layers."""
+    H, W = cost2d.shape
+    c0 = cost2d
+    inf = torch.full_like(c0, float("inf"))
+    c1 = torch.where(c0 > 100, inf, 1.6 * c0)
+    yy = torch.arange(H, device=dev)[:, None] // 64
+    xx = torch.arange(W, device=dev)[None, :] // 64
+    c2 = torch.where(((yy + 2 * xx) % 5) == 0, inf, 0.8 * c0)
+    cost = torch.stack([inf, c0, c1, c2, inf], dim=-1).contiguous()
+    T = torch.empty_like(cost)
+    Lm = Lz + 2
+    g3 = np.array([goal[0], goal[1], 1], np.int64)
+
+    def solve():
+        ctx._chk(L.lib().eik_fim3d_solve(ctx._h, cost.data_ptr(), T.data_ptr(), H, W, Lm, L.EIK_F32, g3,
+                                         stream.cuda_stream))
+
+    sec = timed_loop(solve, steps)
+    st = ctx.stats()
+    cap = 30004
+    out_d = torch.empty((cap, 3), dtype=torch.float64, device=dev)
+    n_d = torch.zeros(1, dtype=torch.int64, device=dev)
+    st_d = torch.zeros(1, dtype=torch.int32, device=dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    ctx._chk(L.lib().eik_path3d_dev(ctx._h, T.data_ptr(), L.EIK_F32, H, W, Lm, np.array([256.0, 256.0, 1.0]),
+                                    np.array([float(goal[0]), float(goal[1]), 1.0]), 0.5, out_d.data_ptr(), cap,
+                                    n_d.data_ptr(), st_d.data_ptr(), stream.cuda_stream))
+    e1.record(stream)
+    torch.cuda.synchronize()
+    res = {"workload": f"configs[4]: coupled {H}x{W}x{Lz} layered costmap (x, y, locomotion mode), FM3D semantics, "
+                       f"z padded with +inf layers ({Lm} in memory)",
+           "reached_fraction": round(float(torch.isfinite(T[:, :, 1:1 + Lz]).float().mean()), 4),
+           "solve_ms_device": round(st.get("solve_ms", 0.0), 4),
+           "value": round(H * W * Lz / sec / 1e9, 4), "unit": "Gcells/s", "ms_per_step": round(sec * 1e3, 4),
+           "steps": steps, "launches_per_solve": st.get("iterations"), "tile_visits_per_solve": st.get("tile_visits"),
+           "path_ms_device": round(e0.elapsed_time(e1), 3), "path_points": int(n_d.item()),
+           "path_status": int(st_d.item())}
+    del cost, T
+    torch.cuda.empty_cache()
+    return res
 
 
 def cpu_baseline(cost, goal):

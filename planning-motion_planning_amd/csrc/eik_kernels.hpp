@@ -35,6 +35,9 @@ struct Fim2dArgs {
     unsigned* qstate;      // per tile: kPending | kBusy
     unsigned long long qtimeout;  // spin limit, s_memrealtime ticks (100 MHz)
     unsigned long long qbudget;   // tile-visit cap (negative costs never converge)
+    // layered solver (fim2dl.hip): cell (y, x) holds ls consecutive values, layers z0.. solved
+    int64_t ls;            // layer stride (1 for the 2D solver)
+    int z0;                // first solved layer
 };
 constexpr int kModeList = 0, kModePersistent = 1;
 constexpr size_t kQueueCtlBytes = 256;
@@ -45,6 +48,13 @@ hipError_t fim2d_persist(const Fim2dArgs& a, bool f64, int grid, hipStream_t st)
 int fim2d_persist_resident(bool f64, int cus);
 hipError_t fim2d_merge_ghost(const Fim2dArgs& a, bool f64, int side, const void* recv, int64_t len, hipStream_t st);
 hipError_t fim2d_pack_edges(const Fim2dArgs& a, bool f64, void* n, void* s, void* w, void* e, hipStream_t st);
+
+// Layered solver (fim2dl.hip): a [H][W][ls] fp32 volume, layers z0 .. z0+nl-1 (nl <= 4), on the
+// 2D tile engine (persistent mode only; a.ls / a.z0 set, no ghosts, no ordering window).
+hipError_t fim2dl_init(const Fim2dArgs& a, int64_t gx, int64_t gy, int64_t gz, hipStream_t st);
+hipError_t fim2dl_persist(const Fim2dArgs& a, int nl, int grid, hipStream_t st);
+int fim2dl_persist_resident(int nl, int cus);
+hipError_t layer_finite(const float* cost, int64_t hw, int64_t L, int64_t z, int* d_flag, hipStream_t st);
 
 // 3D FIM over one H x W x L volume ([y][x][z], FastMarching3D.py layout).
 struct Fim3dArgs {

@@ -64,6 +64,8 @@ struct eik_ctx {
     int grid = 0;
     eik_stats last{};
     eik_fim2d* cached = nullptr;  // solver reused by the host-buffer entry points
+    eik_fim2d* cached_l = nullptr;  // queue state of the layered 3D solver (fim2dl.hip)
+    int resident_l[5] = {0, 0, 0, 0, 0};  // co-resident workgroups of fim2dl_persist_kernel<nl>
     DevBuf cost, T, T2, goals, work, misc;
     DevBuf l3, c3, m3, v3;             // 3D solver scratch (lists, counts, marks, visits)
     int max_passes3 = 24;
@@ -145,6 +147,7 @@ void eik_destroy(eik_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->cached) eik_fim2d_destroy(c->cached);
+    if (c->cached_l) eik_fim2d_destroy(c->cached_l);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -202,6 +205,8 @@ int eik_fim2d_create(eik_ctx* c, int64_t B, int64_t H, int64_t W, int dtype, eik
     a.tiles_per_map = (int)(ntx * nty);
     a.capacity = (int)tiles;
     for (auto& g : a.ghost) g = nullptr;
+    a.ls = 1;
+    a.z0 = 0;
     // FIFO slots: a power of two with ample headroom over the tiles (each tile holds at most one
     // filled slot; the margin keeps a slow poller's slot from being lapped by the tail)
     uint64_t q = 4096;
@@ -595,6 +600,88 @@ int eik_path2d_f64(eik_ctx* c, const double* T, int64_t H, int64_t W, const doub
 }
 
 // ------------------------------------------------------------------------------ 3D
+// Few-layer fp32 volumes (the rover's (x, y, mode) costmaps) on the layered 2D-tile solver:
+// layers z0 .. z0+nl-1 of a [H][W][L] volume, one persistent launch.
+static int solve_layered(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, int64_t W, int64_t L, int z0, int nl,
+                         const int64_t goal[3], hipStream_t st) {
+    eik_fim2d* f = c->cached_l;
+    if (!f || f->H != H || f->W != W) {
+        if (f) eik_fim2d_destroy(f);
+        c->cached_l = nullptr;
+        int rc = eik_fim2d_create(c, 1, H, W, EIK_F32, &f);
+        if (rc) return rc;
+        c->cached_l = f;
+    }
+    Fim2dArgs a = f->a;
+    a.cost = d_cost;
+    a.T = d_T;
+    a.ls = L;
+    a.z0 = z0;
+    a.mode = kModePersistent;
+    a.max_rounds = 1;
+    a.keep = (float)(1.0 - c->tol);
+    a.delta = __builtin_inff();
+    a.edge_dirty = nullptr;
+    for (auto& g : a.ghost) g = nullptr;
+    a.qtimeout = (unsigned long long)(c->qtimeout_s * 1e8);
+    a.qbudget = c->max_visits ? c->max_visits : 1024ull * (unsigned long long)a.tiles_per_map + (1ull << 20);
+    if (c->resident_l[nl] == 0) c->resident_l[nl] = fim2dl_persist_resident(nl, c->cu_count);
+    const int grid = std::min(c->grid > 0 ? c->grid : 4 * c->cu_count, c->resident_l[nl]);
+    HIPCHK(c, hipEventRecord(f->ev_start, st));
+    HIPCHK(c, hipMemsetAsync(f->visits.p, 0, 2 * sizeof(unsigned long long), st));
+    HIPCHK(c, fim2dl_init(a, goal[0], goal[1], goal[2], st));
+    HIPCHK(c, fim2dl_persist(a, nl, grid, st));
+    HIPCHK(c, hipEventRecord(f->ev_stop, st));
+    HIPCHK(c, hipMemcpyAsync(f->h_q, f->qctl.p, kQueueCtlBytes, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(f->h_visits, f->visits.p, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    const unsigned err = f->h_q[192 / 4];
+    if (err & 1u)
+        return set_err(c, EIK_ERR_HIP, "layered solver: a queue wait exceeded %.1f s (EIK_OPT_QTIMEOUT)", c->qtimeout_s);
+    if (err & 2u)
+        return set_err(c, EIK_ERR_NOCONVERGE, "no convergence within %llu tile visits (negative costs?)",
+                       (unsigned long long)a.qbudget);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, f->ev_start, f->ev_stop);
+    c->last = eik_stats{};
+    c->last.iterations = 1;
+    c->last.tile_visits = (int64_t)f->h_visits[0];
+    c->last.inplace_passes = (int64_t)f->h_visits[1];
+    c->last.host_syncs = 1;
+    c->last.solve_ms = ms;
+    c->last.bytes_alg = 4.0 * nl *
+                        ((double)c->last.tile_visits * (3 * kTile * kTile + 4 * kTile) +
+                         (double)c->last.inplace_passes * (kTile * kTile + 4 * kTile)) +
+                        4.0 * H * W * L;
+    return EIK_OK;
+}
+
+// Layers [z0, z0 + nl) of an fp32 volume the layered solver can take, or nl = 0: L <= 4 layers,
+// or L <= 6 whose first and last layers are entirely +inf (the reference's z padding).
+static int layered_plan(eik_ctx* c, const void* d_cost, int64_t H, int64_t W, int64_t L, hipStream_t st, int* z0,
+                        int* nl) {
+    *z0 = 0;
+    *nl = 0;
+    if (L <= 4) {
+        *nl = (int)L;
+        return EIK_OK;
+    }
+    if (L > 6) return EIK_OK;
+    HIPCHK(c, c->misc.ensure(64));
+    int* d_flag = (int*)c->misc.p;
+    int h_flag = 0;
+    HIPCHK(c, hipMemsetAsync(d_flag, 0, sizeof(int), st));
+    HIPCHK(c, layer_finite((const float*)d_cost, H * W, L, 0, d_flag, st));
+    HIPCHK(c, layer_finite((const float*)d_cost, H * W, L, L - 1, d_flag, st));
+    HIPCHK(c, hipMemcpyAsync(&h_flag, d_flag, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    if (h_flag == 0) {
+        *z0 = 1;
+        *nl = (int)L - 2;
+    }
+    return EIK_OK;
+}
+
 int eik_fim3d_solve(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, int64_t W, int64_t L, int dtype,
                     const int64_t goal[3], void* stream) {
     if (!c || !d_cost || !d_T || !goal || H < 1 || W < 1 || L < 1)
@@ -604,6 +691,14 @@ int eik_fim3d_solve(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, int64_
                        (long)goal[2], (long)H, (long)W, (long)L);
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t st = (hipStream_t)stream;
+    if (dtype == EIK_F32 && c->mode == kModePersistent && c->max_rounds == 1 && H * W * L * 4 < (int64_t)UINT32_MAX) {
+        int z0 = 0, nl = 0;
+        int rc = layered_plan(c, d_cost, H, W, L, st, &z0, &nl);
+        if (rc) return rc;
+        if (nl > 0 && goal[2] >= z0 && goal[2] < z0 + nl) {
+            return solve_layered(c, d_cost, d_T, H, W, L, z0, nl, goal, st);
+        }
+    }
     Fim3dArgs a{};
     a.cost = d_cost;
     a.T = d_T;

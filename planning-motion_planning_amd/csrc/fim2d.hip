@@ -32,201 +32,9 @@
 // The same kernels serve B independent maps (tile id = map * tiles_per_map + tile) and a
 // subdomain of a domain-decomposed raster (ghost strips N/S/W/E stand in for out-of-range
 // neighbours; edge activations are flagged for the halo exchange).
-#include "eik_common.hpp"
-#include "eik_kernels.hpp"
+#include "fim_engine.hpp"
 
 namespace eik {
-
-// per-tile queue state (persistent mode): pending / busy, plus what activated the tile since its
-// last visit -- a halo side that improved (its information flows away from that side) or the
-// tile itself (last visit changed it: every direction)
-constexpr unsigned kPending = 1u, kBusy = 2u;
-constexpr unsigned kFromN = 4u, kFromS = 8u, kFromW = 16u, kFromE = 32u, kSelf = 64u;
-
-// Quadrant sweeps that can carry the triggering information: wave 0 (+x,+y) and 1 (-x,+y) move
-// it away from the north edge, 2 and 3 from the south; 0 and 2 from the west, 1 and 3 from the
-// east.  A visit that runs a subset and changes nothing is still a fixed point of the local
-// update (every cell was evaluated against final neighbours); one that changes something
-// re-activates itself with kSelf, i.e. all four.
-__device__ __forceinline__ unsigned sweep_dirs(unsigned trig) {
-    if (trig & kSelf) return 0xFu;
-    unsigned d = 0;
-    if (trig & kFromN) d |= 0x3u;
-    if (trig & kFromS) d |= 0xCu;
-    if (trig & kFromW) d |= 0x5u;
-    if (trig & kFromE) d |= 0xAu;
-    return d ? d : 0xFu;
-}
-#ifndef EIK_PROBE
-#define EIK_PROBE(k) ((void)0)  // phase timing hooks (scratch profiling harness)
-#define EIK_VISIT(trig, dirs) ((void)0)
-#endif
-
-// ------------------------------------------------------------------- memory access policy
-// Plain accesses (LIST mode) or coherent sc1 buffer accesses (PERSISTENT mode).
-template <typename R, bool COH>
-struct TMem;
-
-template <typename R>
-struct TMem<R, false> {
-    R* p;
-    __device__ TMem(R* base, int64_t) : p(base) {}
-    __device__ R ld(int64_t i) const { return p[i]; }
-    __device__ void ld4(int64_t i, R (&v)[4]) const {
-        if constexpr (sizeof(R) == 4) {
-            const float4 t = *reinterpret_cast<const float4*>(p + i);
-            v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
-        } else {
-            const double2 t0 = *reinterpret_cast<const double2*>(p + i);
-            const double2 t1 = *reinterpret_cast<const double2*>(p + i + 2);
-            v[0] = t0.x; v[1] = t0.y; v[2] = t1.x; v[3] = t1.y;
-        }
-    }
-    __device__ void st(int64_t i, R v) const { p[i] = v; }
-    __device__ void st4(int64_t i, const R (&v)[4]) const {
-        if constexpr (sizeof(R) == 4) {
-            *reinterpret_cast<float4*>(p + i) = make_float4(v[0], v[1], v[2], v[3]);
-        } else {
-            *reinterpret_cast<double2*>(p + i) = make_double2(v[0], v[1]);
-            *reinterpret_cast<double2*>(p + i + 2) = make_double2(v[2], v[3]);
-        }
-    }
-};
-
-constexpr int kSC1 = 16;  // aux cache-policy bits of the raw buffer builtins: sc1 (agent coherence)
-typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-
-template <typename R>
-struct TMem<R, true> {
-    __amdgpu_buffer_rsrc_t rs;
-    // n * sizeof(R) < 2^32 is checked by the host before it selects this mode
-    __device__ TMem(R* base, int64_t n)
-        : rs(__builtin_amdgcn_make_buffer_rsrc(base, 0, (int)(uint32_t)(n * (int64_t)sizeof(R)), 0x00020000)) {}
-    __device__ R ld(int64_t i) const {
-        const unsigned off = (unsigned)(i * (int64_t)sizeof(R));
-        if constexpr (sizeof(R) == 4) {
-            return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, kSC1));
-        } else {
-            const u32x2 u = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, kSC1);
-            return __longlong_as_double((long long)(((unsigned long long)u[1] << 32) | u[0]));
-        }
-    }
-    __device__ void ld4(int64_t i, R (&v)[4]) const {
-        const unsigned off = (unsigned)(i * (int64_t)sizeof(R));
-        if constexpr (sizeof(R) == 4) {
-            const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, kSC1);
-            v[0] = __uint_as_float(u[0]); v[1] = __uint_as_float(u[1]);
-            v[2] = __uint_as_float(u[2]); v[3] = __uint_as_float(u[3]);
-        } else {
-            const u32x4 u0 = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, kSC1);
-            const u32x4 u1 = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, kSC1);
-            v[0] = __longlong_as_double((long long)(((unsigned long long)u0[1] << 32) | u0[0]));
-            v[1] = __longlong_as_double((long long)(((unsigned long long)u0[3] << 32) | u0[2]));
-            v[2] = __longlong_as_double((long long)(((unsigned long long)u1[1] << 32) | u1[0]));
-            v[3] = __longlong_as_double((long long)(((unsigned long long)u1[3] << 32) | u1[2]));
-        }
-    }
-    __device__ void st(int64_t i, R v) const {
-        const unsigned off = (unsigned)(i * (int64_t)sizeof(R));
-        if constexpr (sizeof(R) == 4) {
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, off, 0, kSC1);
-        } else {
-            const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-            const u32x2 u = {(unsigned)b, (unsigned)(b >> 32)};
-            __builtin_amdgcn_raw_buffer_store_b64(u, rs, off, 0, kSC1);
-        }
-    }
-    __device__ void st4(int64_t i, const R (&v)[4]) const {
-        const unsigned off = (unsigned)(i * (int64_t)sizeof(R));
-        if constexpr (sizeof(R) == 4) {
-            const u32x4 u = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
-            __builtin_amdgcn_raw_buffer_store_b128(u, rs, off, 0, kSC1);
-        } else {
-            unsigned long long b[4];
-            for (int k = 0; k < 4; ++k) b[k] = (unsigned long long)__double_as_longlong(v[k]);
-            const u32x4 u0 = {(unsigned)b[0], (unsigned)(b[0] >> 32), (unsigned)b[1], (unsigned)(b[1] >> 32)};
-            const u32x4 u1 = {(unsigned)b[2], (unsigned)(b[2] >> 32), (unsigned)b[3], (unsigned)(b[3] >> 32)};
-            __builtin_amdgcn_raw_buffer_store_b128(u0, rs, off, 0, kSC1);
-            __builtin_amdgcn_raw_buffer_store_b128(u1, rs, off + 16, 0, kSC1);
-        }
-    }
-};
-
-template <typename R, bool COH>
-__device__ __forceinline__ R load_T(const Fim2dArgs& a, const TMem<R, COH>& T, int64_t gy, int64_t gx) {
-    constexpr R INF = Real<R>::inf();
-    if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) return T.ld(gy * a.W + gx);
-    // ghost strips only change between launches (merge kernel): plain loads
-    if (gy == -1 && gx >= 0 && gx < a.W) return a.ghost[0] ? static_cast<const R*>(a.ghost[0])[gx] : INF;
-    if (gy == a.H && gx >= 0 && gx < a.W) return a.ghost[1] ? static_cast<const R*>(a.ghost[1])[gx] : INF;
-    if (gx == -1 && gy >= 0 && gy < a.H) return a.ghost[2] ? static_cast<const R*>(a.ghost[2])[gy] : INF;
-    if (gx == a.W && gy >= 0 && gy < a.H) return a.ghost[3] ? static_cast<const R*>(a.ghost[3])[gy] : INF;
-    return INF;
-}
-
-// -------------------------------------------------------------------- activation helpers
-// LIST mode: append to the next iteration's list (dedup by mark).
-__device__ __forceinline__ void enqueue(const Fim2dArgs& a, int tile, int list, unsigned stamp, float key) {
-    if (a.delta < __builtin_inff()) {  // ordered mode only: keep the entering-T keys
-        const unsigned kb = __float_as_uint(key);  // non-negative: float order == unsigned order
-        atomicMin(&a.key[tile], kb);
-        // one shared word per list: read first, so only a new minimum pays the contended atomic
-        if (kb < __hip_atomic_load(&a.minkey[list], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-            atomicMin(&a.minkey[list], kb);
-    }
-    if (atomicMax(&a.mark[tile], stamp) < stamp) {
-        const int pos = atomicAdd(&a.counts[list], 1);
-        a.lists[(int64_t)list * a.capacity + pos] = tile;
-    }
-}
-
-// PERSISTENT mode: append to the FIFO unless the tile is already pending (nothing to do) or
-// busy (its processor re-queues it when it finishes).
-__device__ __forceinline__ void qslot_put(const Fim2dArgs& a, int tile) {
-    const unsigned long long pos = atomicAdd(a.qtail, 1ull);
-    __hip_atomic_store(&a.qslot[pos & a.qmask], (unsigned)tile + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void qpush(const Fim2dArgs& a, int tile, unsigned trig) {
-    if (atomicOr(&a.qstate[tile], kPending | trig) == 0u) {
-        atomicAdd(a.qactive, 1);  // before the slot store: a waiter never sees "empty and idle"
-        qslot_put(a, tile);
-    }
-}
-
-__device__ __forceinline__ void activate(const Fim2dArgs& a, int tile, int list, unsigned stamp, float key,
-                                         unsigned trig) {
-    if (a.mode == kModePersistent)
-        qpush(a, tile, trig);
-    else
-        enqueue(a, tile, list, stamp, key);
-}
-
-// Neighbour activations of a write-back with flags f: thread q in 1..4 handles one side (their
-// atomics overlap); thread 0 flags changed subdomain edges for the halo exchange.
-__device__ __forceinline__ void activate_neighbours(const Fim2dArgs& a, int tile, unsigned f, const unsigned* key,
-                                                    int list, unsigned stamp) {
-    const int tid = threadIdx.x;
-    if (tid >= 5) return;
-    const int map = tile / a.tiles_per_map;
-    const int rem = tile - map * a.tiles_per_map;
-    const int ty = rem / a.ntx, tx = rem - (rem / a.ntx) * a.ntx;
-    const int base = map * a.tiles_per_map;
-    const float kk = __uint_as_float(key[tid]);
-    // (this tile's north edge is the north neighbour's south halo, ...)
-    if (tid == 1 && (f & 1u) && ty > 0) activate(a, base + rem - a.ntx, list, stamp, kk, kFromS);
-    if (tid == 2 && (f & 2u) && ty + 1 < a.nty) activate(a, base + rem + a.ntx, list, stamp, kk, kFromN);
-    if (tid == 3 && (f & 4u) && tx > 0) activate(a, base + rem - 1, list, stamp, kk, kFromE);
-    if (tid == 4 && (f & 8u) && tx + 1 < a.ntx) activate(a, base + rem + 1, list, stamp, kk, kFromW);
-    if (tid == 0 && a.edge_dirty) {  // subdomain edges (domain decomposition)
-        unsigned e = 0;
-        if ((f & 1u) && ty == 0) e |= 1u;
-        if (((f & 2u) || (f & 32u)) && ty + 1 == a.nty) e |= 2u;
-        if ((f & 4u) && tx == 0) e |= 4u;
-        if (((f & 8u) || (f & 64u)) && tx + 1 == a.ntx) e |= 8u;
-        if (e) atomicOr(a.edge_dirty, e);
-    }
-}
 
 // ------------------------------------------------------------------------- quadrant sweep
 // Cs sits right after the Ts ring in TileLds: Cs - Ts is a compile-time constant, so every LDS
@@ -564,47 +372,6 @@ __global__ __launch_bounds__(kThreads) void fim2d_sweep_kernel(Fim2dArgs a) {
         if (tid == 0 && a.visits) atomicAdd(a.visits, 1ull);
         __syncthreads();  // LDS reuse by the next tile of this workgroup
     }
-}
-
-// ------------------------------------------------------------------- PERSISTENT driver
-// Take a ticket and wait for its slot: the next queued tile, or -1 when the solve has ended
-// (no tile pending or busy) or failed.  ONE lane polls (relaxed agent-scope loads = sc1).
-__device__ __forceinline__ int qgrab(const Fim2dArgs& a, unsigned& trig) {
-    if (__hip_atomic_load(a.qerror, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return -1;
-    const unsigned long long pos = atomicAdd(a.qhead, 1ull);
-    unsigned* slot = &a.qslot[pos & a.qmask];
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    for (unsigned spin = 0;; ++spin) {
-        const unsigned v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (v != 0u) {
-            // free the slot BEFORE the tile can be re-queued (slot reuse)
-            __hip_atomic_store(slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int tile = (int)(v - 1u);
-            // pending -> busy before T is read: any activation from here on makes the finish
-            // re-queue the tile, so no update is lost
-            trig = atomicExch(&a.qstate[tile], kBusy);  // consumed after the staging loads
-            return tile;
-        }
-        if ((spin & 7u) == 7u) {
-            if (__hip_atomic_load(a.qactive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return -1;
-            if (__hip_atomic_load(a.qerror, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return -1;
-            if (__builtin_amdgcn_s_memrealtime() - t0 > a.qtimeout) {  // never hang
-                atomicOr(a.qerror, 1u);
-                return -1;
-            }
-        }
-        __builtin_amdgcn_s_sleep(8);
-    }
-}
-
-// Retire a visited tile (after its activations completed): re-queue it if it was activated
-// while busy (it stays counted), else it stops counting as active.
-__device__ __forceinline__ void qfinish(const Fim2dArgs& a, int tile) {
-    const unsigned old = atomicAnd(&a.qstate[tile], ~kBusy);
-    if (old & kPending)
-        qslot_put(a, tile);
-    else
-        atomicSub(a.qactive, 1);
 }
 
 template <typename R>

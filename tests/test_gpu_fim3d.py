@@ -77,3 +77,61 @@ def test_vs_oracle(ctx, shape, seed):
         O.set_strict(True)
     check(ctx.tmap3d(c, goal, dtype=np.float32), R, False)
     check(ctx.tmap3d(c, goal, dtype=np.float64), R, True)
+
+
+# --- layered solver (fim2dl.hip): fp32 volumes with <= 4 layers, or z-padded with all-inf
+# first/last layers (the reference's padding), go to the 2D-tile engine with per-cell layers.
+def _layered_case(shape, seed, pad=False, switch=False):
+    rng = np.random.default_rng(seed)
+    H, W, L = shape
+    c = rng.uniform(1, 4, shape)
+    c[rng.random(shape) < 0.08] = np.inf
+    if switch:  # layer 0 cheap on the left, layer 1 cheap on the right: paths change layer
+        c[:, : W // 2, 0] *= 0.3
+        c[:, W // 2 :, 1 % L] *= 0.3
+    if pad:
+        c = np.concatenate([np.full((H, W, 1), np.inf), c, np.full((H, W, 1), np.inf)], axis=2)
+    goal = np.array([W // 3, H // 2, (1 if pad else 0) + (L - 1) // 2])
+    c[goal[1], goal[0], goal[2]] = 1.0
+    return c, goal
+
+
+@pytest.mark.parametrize("shape,seed,pad,switch", [((130, 150, 2), 11, False, True), ((200, 230, 3), 12, False, False),
+                                                     ((64, 64, 4), 13, False, True), ((90, 140, 3), 14, True, True),
+                                                     ((300, 257, 3), 15, False, True), ((70, 65, 1), 16, False, False)])
+def test_layered_vs_oracle(ctx, shape, seed, pad, switch):
+    c, goal = _layered_case(shape, seed, pad, switch)
+    O.set_strict(False)
+    try:
+        R = O.fmm3d(c, goal, None)
+    finally:
+        O.set_strict(True)
+    T = ctx.tmap3d(c, goal, dtype=np.float32)
+    check(T, R, False)
+    if pad:
+        assert np.all(np.isinf(T[:, :, 0])) and np.all(np.isinf(T[:, :, -1]))
+
+
+def test_layered_device_entry(ctx):
+    """eik_fim3d_solve on device buffers (the bench's C5 route) equals the host entry point."""
+    import torch
+    from eikonal import _lib as L
+
+    c, goal = _layered_case((257, 300, 3), 21, pad=True, switch=True)
+    dev = torch.device("cuda", 0)
+    cd = torch.from_numpy(c.astype(np.float32)).to(dev)
+    Td = torch.empty_like(cd)
+    H, W, Lz = c.shape
+    st = torch.cuda.current_stream(dev)
+    ctx._chk(L.lib().eik_fim3d_solve(ctx._h, cd.data_ptr(), Td.data_ptr(), H, W, Lz, L.EIK_F32,
+                                     np.ascontiguousarray(goal, np.int64), st.cuda_stream))
+    torch.cuda.synchronize()
+    s = ctx.stats()
+    assert s["iterations"] == 1 and s["tile_visits"] > 0  # one persistent launch (layered solver)
+    T = Td.cpu().numpy()
+    O.set_strict(False)
+    try:
+        R = O.fmm3d(c, goal, None)
+    finally:
+        O.set_strict(True)
+    check(T, R, False)
