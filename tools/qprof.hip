@@ -17,7 +17,7 @@ using namespace eik;
 #define CK(x) do { hipError_t e = (x); if (e) { printf("%s -> %s\n", #x, hipGetErrorString(e)); exit(2);} } while (0)
 int main(int argc, char** argv) {
     int N = atoi(argv[1]), grid = atoi(argv[2]);
-    const char* cf = argc > 3 ? argv[3] : nullptr;
+    const char* cf = argc > 3 && strcmp(argv[3], "-") != 0 ? argv[3] : nullptr;  // "-": uniform cost
     int rounds = argc > 4 ? atoi(argv[4]) : 1;
     std::vector<float> hc((size_t)N * N, 1.f);
     if (cf) { FILE* f = fopen(cf, "rb"); if (!f || fread(hc.data(), 4, hc.size(), f) != hc.size()) { printf("bad cost file\n"); return 2; } fclose(f); }
@@ -29,13 +29,14 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(cost, hc.data(), 4ull * N * N, hipMemcpyHostToDevice));
     a.cost = cost; a.T = T; a.H = N; a.W = N; a.ntx = ntx; a.nty = ntx; a.tiles_per_map = tiles;
     CK(hipMalloc(&a.lists, 12ull * tiles)); CK(hipMalloc(&a.counts, 256)); CK(hipMalloc(&a.mark, 4ull * tiles));
-    a.capacity = tiles; a.max_rounds = rounds; a.keep = 1.f; CK(hipMalloc(&a.key, 4ull * tiles)); a.minkey = (unsigned*)a.counts + 16;
+    a.capacity = tiles; a.max_rounds = rounds; a.keep = 1.f - (argc > 5 ? (float)atof(argv[5]) : 0.f); CK(hipMalloc(&a.key, 4ull * tiles)); a.minkey = (unsigned*)a.counts + 16;
     a.delta = __builtin_inff(); CK(hipMalloc(&a.visits, 16));
     char* q; CK(hipMalloc(&q, 256)); a.qhead = (unsigned long long*)q; a.qtail = (unsigned long long*)(q + 64);
     a.qactive = (int*)(q + 128); a.qerror = (unsigned*)(q + 192); a.mode = kModePersistent;
     unsigned qn = 4096; while (qn < 8u * tiles) qn <<= 1;
     a.qmask = qn - 1; CK(hipMalloc(&a.qslot, 4ull * qn)); CK(hipMalloc(&a.qstate, 4ull * tiles));
     a.qtimeout = 1000000000ull; a.qbudget = 1ull << 40;
+    a.ls = 1; a.z0 = 0;
     int64_t* goals; CK(hipMalloc(&goals, 16)); int64_t hg[2] = {N / 2, N / 2}; CK(hipMemcpy(goals, hg, 16, hipMemcpyHostToDevice));
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     float ms = 0;
@@ -54,7 +55,7 @@ int main(int argc, char** argv) {
     double acc[8] = {0}, cnt[8] = {0};
     for (int b = 0; b < grid; ++b) for (int k = 0; k < 7; ++k) { if (k == 7) continue; acc[k] += hp[b * 32 + k] * 1e-2; cnt[k] += hp[b * 32 + 8 + k]; }
     const char* nm[7] = {"to-stage", "stage", "sweep", "wback+drain", "to-post", "post(act+fin)", "grab+barrier"};
-    printf("N=%d grid=%d rounds=%d: kernel %.3f ms, visits %llu (+%llu in place), err %u, active %d\n", N, grid, rounds, ms, v, vv[1], hq[48], (int)hq[32]);
+    printf("N=%d grid=%d rounds=%d keep=1-%.1e: kernel %.3f ms, visits %llu (+%llu in place), err %u, active %d\n", N, grid, rounds, 1.0 - a.keep, ms, v, vv[1], hq[48], (int)hq[32]);
     double sw = 0, self = 0; for (int b = 0; b < grid; ++b) { sw += hp[b * 32 + 16]; self += hp[b * 32 + 17]; }
     printf("  sweeps/visit %.3f, self-triggered visits %.1f%%\n", sw / v, 100.0 * self / v);
     double busy = 0;
