@@ -1,0 +1,37 @@
+"""Time the FM3D path kernel alone (device field, device path) on layered volumes."""
+import sys, time
+import numpy as np
+import torch
+sys.path.insert(0, 'planning-motion_planning_amd')
+import eikonal
+from eikonal import _lib as L
+
+dev = torch.device("cuda", 0)
+st = torch.cuda.current_stream(dev)
+ctx = eikonal.Context(0)
+for (H, W, Lz, pad) in [(1024, 1024, 3, True), (1024, 1024, 3, False), (2048, 2048, 3, True)]:
+    rng = np.random.default_rng(0)
+    c = torch.from_numpy(rng.uniform(1, 3, (H, W, Lz)).astype(np.float32)).to(dev)
+    if pad:
+        inf = torch.full((H, W, 1), float('inf'), device=dev)
+        c = torch.cat([inf, c, inf], dim=2).contiguous()
+    Lm = c.shape[2]
+    z = 1 if pad else 0
+    T = torch.empty_like(c)
+    g = np.array([W - 20, H - 20, z], np.int64)
+    ctx._chk(L.lib().eik_fim3d_solve(ctx._h, c.data_ptr(), T.data_ptr(), H, W, Lm, L.EIK_F32, g, st.cuda_stream))
+    cap = 30004
+    out = torch.empty((cap, 3), dtype=torch.float64, device=dev)
+    n = torch.zeros(1, dtype=torch.int64, device=dev)
+    s = torch.zeros(1, dtype=torch.int32, device=dev)
+    for rep in range(2):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        ctx._chk(L.lib().eik_path3d_dev(ctx._h, T.data_ptr(), L.EIK_F32, H, W, Lm, np.array([20.0, 20.0, z]),
+                                        np.array([float(g[0]), float(g[1]), float(z)]), 0.5, out.data_ptr(), cap,
+                                        n.data_ptr(), s.data_ptr(), st.cuda_stream))
+        e1.record(st)
+        torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1)
+    print(f"H={H} W={W} L={Lm} pad={pad}: path {int(n.item())} points status {int(s.item())}: {ms:.3f} ms, "
+          f"{ms * 1e3 / max(int(n.item()), 1):.2f} us/point", flush=True)
