@@ -70,12 +70,21 @@ __device__ __forceinline__ double interp2_sel(double a, double b, double g00, do
     const double ra = a00 + a10 * a;            // b == 0
     const double rb = a00 + a01 * b;            // a == 0
     const double rf = ra + a01 * b + a11 * a * b;
-    return a == 0 ? (b == 0 ? a00 : rb) : (b == 0 ? ra : rf);
+    // bitwise selects: the compiler turns the ?: form into branches on the walker's chain
+    const long long za = -(long long)(a == 0), zb = -(long long)(b == 0);
+    const long long r0 = (__double_as_longlong(rb) & ~zb) | (__double_as_longlong(a00) & zb);   // a == 0
+    const long long r1 = (__double_as_longlong(rf) & ~zb) | (__double_as_longlong(ra) & zb);    // a != 0
+    return __longlong_as_double((r1 & ~za) | (r0 & za));
 }
 
 __device__ __forceinline__ double norm2(double a, double b) { return __builtin_sqrt(a * a + b * b); }
 
 enum { kGdmDone = 0, kGdmFallback = 1, kGdmError = 2 };
+#ifndef EIK_P2PROBE
+#define EIK_P2PROBE(k) ((void)0)  // 2D walker phase timing hooks (tools/path2_prof.hip)
+#define EIK_P2DECL ((void)0)
+#define EIK_P2FLUSH ((void)0)
+#endif
 
 // Path kernel layout: ONE workgroup of 16 waves.  Wave 0 is the walker: it runs the reference
 // loop (:173-232) step by step, reading the inf-aware normalised gradient (Gnx, Gny) of the four
@@ -189,6 +198,7 @@ __global__ __launch_bounds__(kPathThreads) void gdm2d_kernel(Gdm2dArgs a) {
         return;
     }
     // ---- walker (wave 0; every lane runs the same uniform loop, lane 0 stores)
+    EIK_P2DECL;
     const bool lead = threadIdx.x == 0;
     double* out = a.out;
     int status = kGdmDone;
@@ -226,82 +236,113 @@ __global__ __launch_bounds__(kPathThreads) void gdm2d_kernel(Gdm2dArgs a) {
         const int64_t x0 = b ? wx1 : wx0, y0 = b ? wy1 : wy0;
         return i >= x0 && j >= y0 && i + 1 < x0 + kPW && j + 1 < y0 + kPW;
     };
-    for (long k = 0; k < a.steps; ++k) {
-        if (__builtin_isnan(px) || __builtin_isnan(py)) { status = kGdmError; break; }
+    // Fast path: while lo_x <= i <= hi_x and lo_y <= j <= hi_y nothing has to happen this step
+    // (the corners lie in the current window and, unless a build is pending, not within
+    // kPrefetch of an inner edge) -- four int32 compares on the step's dependency chain instead
+    // of the window bookkeeping, which runs only when the bounds are crossed.
+    int lo_x = 1, hi_x = 0, lo_y = 1, hi_y = 0;  // empty: the first step takes the slow path
+    int cx0i = 0, cy0i = 0;                     // current window origin
+    auto set_bounds = [&]() {
+        const int64_t x0 = cur ? wx1 : wx0, y0 = cur ? wy1 : wy0;
+        cx0i = (int)x0;
+        cy0i = (int)y0;
+        lo_x = cx0i + (!pending && x0 > 0 ? kPrefetch : 0);
+        hi_x = cx0i + kPW - 2 - (!pending && x0 < xmax ? kPrefetch : 0);
+        lo_y = cy0i + (!pending && y0 > 0 ? kPrefetch : 0);
+        hi_y = cy0i + kPW - 2 - (!pending && y0 < ymax ? kPrefetch : 0);
+        hi_x = hi_x < (int)W - 2 ? hi_x : (int)W - 2;  // inside the bounds implies i + 1 < W, j + 1 < H
+        hi_y = hi_y < (int)H - 2 ? hi_y : (int)H - 2;
+    };
+    // the point budget folded into the step count: point n = k + 1 is stored at step k (:173)
+    const long kmax = a.steps < a.cap - 1 ? a.steps : a.cap - 1;
+    long k = 0;
+    for (; k < kmax; ++k) {
+        EIK_P2PROBE(0);
         const uint32_t i = (uint32_t)__builtin_trunc(px), j = (uint32_t)__builtin_trunc(py);
-        if (i + 1 >= (uint64_t)W || j + 1 >= (uint64_t)H) { status = kGdmError; break; }
-        if (!inside(cur, i, j)) {  // the 2 x 2 interpolation corners left the window
-            const int nb = seq == 0 ? 0 : 1 - cur;
-            bool have = false;
-            if (pending) {
-                pending = false;
-                if (!wait_built()) { status = kGdmError; break; }
-                have = inside(nb, i, j);
+        // one test on the chain: NaN point, out of range, or window bookkeeping due
+        if (__builtin_isnan(px + py) || (int)i < lo_x || (int)i > hi_x || (int)j < lo_y || (int)j > hi_y) {
+            if (__builtin_isnan(px) || __builtin_isnan(py)) { status = kGdmError; break; }
+            if (i + 1 >= (uint64_t)W || j + 1 >= (uint64_t)H) { status = kGdmError; break; }
+            if (!inside(cur, i, j)) {  // the 2 x 2 interpolation corners left the window
+                const int nb = seq == 0 ? 0 : 1 - cur;
+                bool have = false;
+                if (pending) {
+                    pending = false;
+                    if (!wait_built()) { status = kGdmError; break; }
+                    have = inside(nb, i, j);
+                }
+                if (!have) {
+                    issue(nb, i, j);
+                    if (!wait_built()) { status = kGdmError; break; }
+                }
+                cur = nb;
             }
-            if (!have) {
-                issue(nb, i, j);
-                if (!wait_built()) { status = kGdmError; break; }
+            const int64_t cx0 = cur ? wx1 : wx0, cy0 = cur ? wy1 : wy0;
+            if (!pending && ((i - cx0 < kPrefetch && cx0 > 0) || (cx0 + kPW - 2 - i < kPrefetch && cx0 < xmax) ||
+                             (j - cy0 < kPrefetch && cy0 > 0) || (cy0 + kPW - 2 - j < kPrefetch && cy0 < ymax))) {
+                issue(1 - cur, i, j);
+                pending = true;
             }
-            cur = nb;
+            set_bounds();
         }
-        const int64_t cx0 = cur ? wx1 : wx0, cy0 = cur ? wy1 : wy0;
-        if (!pending && ((i - cx0 < kPrefetch && cx0 > 0) || (cx0 + kPW - 2 - i < kPrefetch && cx0 < xmax) ||
-                         (j - cy0 < kPrefetch && cy0 > 0) || (cy0 + kPW - 2 - j < kPrefetch && cy0 < ymax))) {
-            issue(1 - cur, i, j);
-            pending = true;
-        }
-        const int li = (int)(i - cx0), lj = (int)(j - cy0);
+        EIK_P2PROBE(1);
+        const int li = (int)i - cx0i, lj = (int)j - cy0i;
         const double2 g00 = s.g[cur][lj][li], g01 = s.g[cur][lj][li + 1];
         const double2 g10 = s.g[cur][lj + 1][li], g11 = s.g[cur][lj + 1][li + 1];
         const double fa = px - i, fb = py - j;
         double dx = interp2_sel(fa, fb, g00.x, g01.x, g10.x, g11.x);  // :175
         double dy = interp2_sel(fa, fb, g00.y, g01.y, g10.y, g11.y);  // :176
-        if (__builtin_isnan(dx) || __builtin_isnan(dy)) {
-            // NaN fallback (:178-218) as the reference behaves under numpy 2: the neighbour
-            // probe `np.uint32(nearN + [0,-1])` raises OverflowError, caught at :217.
-            if (lead) {
-                int64_t nx = (int64_t)__builtin_rint(px), ny = (int64_t)__builtin_rint(py);
-                bool empty = false, oob = false;
-                for (;;) {
-                    const int64_t qx = nx < 0 ? nx + W : nx, qy = ny < 0 ? ny + H : ny;
-                    if (qx < 0 || qy < 0 || qx >= W || qy >= H) { oob = true; break; }
-                    if (!__builtin_isinf(tv(T, W, qy, qx))) break;
-                    --n;
-                    if (n == 0) { empty = true; break; }
-                    nx = (int64_t)__builtin_rint(out[2 * (n - 1)]);
-                    ny = (int64_t)__builtin_rint(out[2 * (n - 1) + 1]);
-                }
-                if (!empty && !oob) {
-                    while (n > 0 && norm2(out[2 * (n - 1)] - (double)nx, out[2 * (n - 1) + 1] - (double)ny) < 1) --n;
-                    if (n < a.cap) {
-                        out[2 * n] = (double)nx;
-                        out[2 * n + 1] = (double)ny;
-                        ++n;
-                    }
-                }
-            }
-            status = kGdmFallback;
-            break;
-        }
+        EIK_P2PROBE(2);
         // |(dx, dy)| is the same value in the test (:220) and both normalisations (:221-227)
         const double nrm = __builtin_sqrt(dx * dx + dy * dy);
         const double dxn = dx / nrm;  // both branches
         // :220-224 (|g| < 0.01: unit step) or :225-229 (dy normalised with the already-normalised dx)
         const double dyn = nrm < 0.01 ? dy / nrm : dy / __builtin_sqrt(dxn * dxn + dy * dy);
         const double sx = px - tau * dxn, sy = py - tau * dyn;
-        if (n >= a.cap) { status = kGdmError; break; }
-        if (lead) {
-            out[2 * n] = sx;
-            out[2 * n + 1] = sy;
+        // :231-232  sqrt(e) < 1.5  <=>  e < 2.25 for a correctly rounded sqrt (2.25 = 1.5^2 exactly)
+        const double ex = sx - a.ex, ey = sy - a.ey;
+        const bool stop = ex * ex + ey * ey < 2.25;
+        EIK_P2PROBE(3);
+        // one test after the step: a NaN gradient (the fallback: nothing of this step is kept)
+        // or the stop radius; NaN in dx + dy also catches inf - inf, re-tested precisely
+        if (__builtin_isnan(dx + dy) || stop) {
+            if (__builtin_isnan(dx) || __builtin_isnan(dy)) {
+                // NaN fallback (:178-218) as the reference behaves under numpy 2: the neighbour
+                // probe `np.uint32(nearN + [0,-1])` raises OverflowError, caught at :217.
+                if (lead) {
+                    int64_t nx = (int64_t)__builtin_rint(px), ny = (int64_t)__builtin_rint(py);
+                    bool empty = false, oob = false;
+                    for (;;) {
+                        const int64_t qx = nx < 0 ? nx + W : nx, qy = ny < 0 ? ny + H : ny;
+                        if (qx < 0 || qy < 0 || qx >= W || qy >= H) { oob = true; break; }
+                        if (!__builtin_isinf(tv(T, W, qy, qx))) break;
+                        --n;
+                        if (n == 0) { empty = true; break; }
+                        nx = (int64_t)__builtin_rint(out[2 * (n - 1)]);
+                        ny = (int64_t)__builtin_rint(out[2 * (n - 1) + 1]);
+                    }
+                    if (!empty && !oob) {
+                        while (n > 0 && norm2(out[2 * (n - 1)] - (double)nx, out[2 * (n - 1) + 1] - (double)ny) < 1) --n;
+                        if (n < a.cap) {
+                            out[2 * n] = (double)nx;
+                            out[2 * n + 1] = (double)ny;
+                            ++n;
+                        }
+                    }
+                }
+                status = kGdmFallback;
+                break;
+            }
         }
+        *reinterpret_cast<double2*>(out + 2 * n) = make_double2(sx, sy);  // every lane: same address and value
         ++n;
         px = sx;
         py = sy;
-        // :231-232  sqrt(e) < 1.5  <=>  e < 2.25 for a correctly rounded sqrt (2.25 = 1.5^2 exactly)
-        const double ex = sx - a.ex, ey = sy - a.ey;
-        if (ex * ex + ey * ey < 2.25) break;
+        if (stop) break;
     }
+    if (k == kmax && kmax < a.steps && status == kGdmDone) status = kGdmError;  // out of point budget
     __hip_atomic_store(&s.req_seq, -1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);  // builders exit
+    EIK_P2FLUSH;
     if (lead) {
         if (status == kGdmDone && n < a.cap) {  // :234
             out[2 * n] = a.ex;
