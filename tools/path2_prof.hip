@@ -16,17 +16,25 @@ __device__ unsigned long long g_p2[16];
 #endif
 #include "../planning-motion_planning_amd/csrc/gdm.hip"
 using namespace eik;
-int main() {
+int main(int argc, char** argv) {
+    // default: smooth synthetic field; or: p2 <T.f32 file> (4096^2, the bench field, goal 2048,2048, start 256,256)
     const int H = 4096, W = 4096;
     std::vector<float> hT((size_t)H * W);
-    const int gx = W - 300, gy = H - 200;
-    for (int y = 0; y < H; ++y)
-        for (int x = 0; x < W; ++x) hT[(size_t)y * W + x] = std::hypot(x - gx, (y - gy) * 1.3f) + 20.f * std::sin(x * 0.01f);
+    int gx = W - 300, gy = H - 200, sx = 200, sy = 300;
+    if (argc > 1) {
+        FILE* f = fopen(argv[1], "rb");
+        if (!f || fread(hT.data(), 4, hT.size(), f) != hT.size()) { printf("bad T file\n"); return 2; }
+        fclose(f);
+        gx = 2048; gy = 2048; sx = 256; sy = 256;
+    } else {
+        for (int y = 0; y < H; ++y)
+            for (int x = 0; x < W; ++x) hT[(size_t)y * W + x] = std::hypot(x - gx, (y - gy) * 1.3f) + 20.f * std::sin(x * 0.01f);
+    }
     float* T; double* out; long long* n; int* st;
     (void)hipMalloc(&T, hT.size() * 4); (void)hipMalloc(&out, 30004 * 16); (void)hipMalloc(&n, 8); (void)hipMalloc(&st, 4);
     (void)hipMemcpy(T, hT.data(), hT.size() * 4, hipMemcpyHostToDevice);
     Gdm2dArgs a{};
-    a.T = T; a.H = H; a.W = W; a.ix = 200; a.iy = 300; a.ex = gx; a.ey = gy; a.tau = 0.5; a.steps = 30000;
+    a.T = T; a.H = H; a.W = W; a.ix = sx; a.iy = sy; a.ex = gx; a.ey = gy; a.tau = 0.5; a.steps = 30000;
     a.out = out; a.cap = 30004; a.n_out = (int64_t*)n; a.status = st;
     unsigned long long z[16] = {0};
     for (int rep = 0; rep < 2; ++rep) {
