@@ -189,6 +189,7 @@ def main():
         out["extra_configs"] = {
             "C3": bench_batch(ctx, dev, stream, args.extra_steps),
             "C5": bench_layers(ctx, dev, stream, cost, goal_g, args.extra_steps),
+            "costmap": bench_costmap(ctx, dev, stream, args.extra_steps, goal_g),
         }
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -318,6 +319,48 @@ def bench_layers(ctx, dev, stream, cost2d, goal, steps, Lz=3):
     del cost, T
     torch.cuda.empty_cache()
     return res
+
+
+def bench_costmap(ctx, dev, stream, steps, goal, N=4096, res=0.05):
+    """SURVEY.md §8(f) rank 1, the solver's input producer: the planner's cost raster built from
+    the 4096^2 DEM on the GPU (eik_costmap_dev: normals, slope obstacles, two hole fillings, five
+    disk morphologies, EDT ramp, 50 x 50 blur), f64 as the reference; then DEM -> path on the
+    device (cost map + f64 -> f32 + solve + path kernel)."""
+    Z = terrain.dem_block(0, 0, N, N, seed=42, device=dev).double().contiguous()
+    cost = torch.empty_like(Z)
+    obst = torch.empty(Z.shape, dtype=torch.uint8, device=dev)
+
+    def build():
+        ctx._chk(L.lib().eik_costmap_dev(ctx._h, Z.data_ptr(), N, N, res, res * N, None, cost.data_ptr(),
+                                         obst.data_ptr(), stream.cuda_stream))
+
+    sec = timed_loop(build, steps)
+    fim = eikonal.Fim2d(ctx, 1, N, N, L.EIK_F32)
+    cap = 30004
+    out_d = torch.empty((cap, 2), dtype=torch.float64, device=dev)
+    n_d = torch.zeros(1, dtype=torch.int64, device=dev)
+    st_d = torch.zeros(1, dtype=torch.int32, device=dev)
+    c32 = torch.empty(Z.shape, dtype=torch.float32, device=dev)
+    T = torch.empty_like(c32)
+    g = [int(goal[0]), int(goal[1])]
+
+    def dem_to_path():
+        build()
+        c32.copy_(cost)
+        fim.solve(c32.data_ptr(), T.data_ptr(), [tuple(g)], stream.cuda_stream)
+        ctx._chk(L.lib().eik_path2d_dev(ctx._h, T.data_ptr(), L.EIK_F32, N, N, np.array([256.0, 256.0]),
+                                        np.array([float(g[0]), float(g[1])]), 0.5, out_d.data_ptr(), cap,
+                                        n_d.data_ptr(), st_d.data_ptr(), stream.cuda_stream))
+
+    sec2 = timed_loop(dem_to_path, steps)
+    obst_frac = float(obst.float().mean())
+    fim.close()
+    return {"workload": f"cost raster of the planner (Coupled_motion_planner.py:1101-1216) from a {N}x{N} DEM "
+                        f"(terrain seed 42, res {res} m), f64",
+            "value": round(N * N / sec / 1e9, 4), "unit": "Gcells/s", "ms_per_step": round(sec * 1e3, 3),
+            "steps": steps, "obstacle_fraction": round(obst_frac, 4),
+            "ms_dem_to_path_device": round(sec2 * 1e3, 3), "path_points": int(n_d.item()),
+            "path_status": int(st_d.item())}
 
 
 def cpu_baseline(cost, goal):

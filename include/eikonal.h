@@ -178,6 +178,33 @@ int eik_path3d_dev(eik_ctx* ctx, const void* d_T, int dtype, int64_t H, int64_t 
                    const double end[3], double tau, double* d_out, int64_t cap, int64_t* d_n_out, int* d_status,
                    void* stream);
 
+/* ---- cost-raster builder (the solver's input producer) ----------
+ * Coupled_motion_planner.py main(), :1101-1216: DEM -> surface normals -> slope obstacles ->
+ * hole filling, disk erode/dilate -> 300 x obstacle + 10 x distance ramp -> 50 x 50 box blur ->
+ * +inf border.  Constants default to the reference's (slope 0.20 rad, rover diagonal 0.9 m,
+ * expansion 1 m, gradient 10, obstacle cost 300) when params is NULL. */
+typedef struct {
+    double slope_max;  /* rad, :1154 */
+    double diagonal;   /* m, rover body diagonal (corridor erosion radius = diagonal / 2), :1172 */
+    double expansion;  /* m, obstacle cost ramp radius, :1190 */
+    double gradient;   /* ramp cost scale, :1202 */
+    double high;       /* obstacle cost, :1187 */
+} eik_costmap_params;
+
+/* Z: H x W DEM (row-major, Zs of :1098-1101, spacing size / (n - 1) as linspace(0, size, n)).
+ * cost_out: H x W, [y][x] -- the reference's cMap.T, i.e. the array it passes to
+ * FM.biComputeTmap (:1222); obst_out (nullable): the final obstacle map (:1180-1184), 0/1. */
+int eik_costmap_f64(eik_ctx* ctx, const double* Z, int64_t H, int64_t W, double resolution, double size,
+                    const eik_costmap_params* params, double* cost_out, uint8_t* obst_out);
+/* the same on device buffers, async on `stream` except the two hole-filling solves */
+int eik_costmap_dev(eik_ctx* ctx, const double* d_Z, int64_t H, int64_t W, double resolution, double size,
+                    const eik_costmap_params* params, double* d_cost, uint8_t* d_obst, void* stream);
+/* surface_normal(resolution, size, z) :37-80 -> unit normals (H x W each) */
+int eik_surface_normal_f64(eik_ctx* ctx, const double* Z, int64_t H, int64_t W, double size, double* Nx, double* Ny,
+                           double* Nz);
+/* image_filling(im) :82-94 (cv2.floodFill from (0, 0), 4-connected) on a 0/1 uint8 image */
+int eik_image_fill_u8(eik_ctx* ctx, const uint8_t* im, int64_t H, int64_t W, uint8_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,158 @@
+"""CPU restatement of the reference's cost-raster builder (TEST INFRASTRUCTURE ONLY).
+
+Imported only by tests/ as the checker of the GPU builder (planning-motion_planning_amd/costmap,
+csrc/costmap.hip).  Reference: /root/reference/src/Coupled_motion_planner.py
+  surface_normal      :37-80     -> surface_normal()
+  image_filling       :82-94     -> image_filling()
+  structural_disk     :96-105    -> structural_disk()
+  main, cost map      :1101-1216 -> cost_map()
+The reference needs OpenCV (cv2), which is not installed here, so its cv2 calls are restated
+with their documented semantics and checked against brute-force definitions in
+tests/test_costmap_oracle.py:
+  cv2.erode / cv2.dilate (uint8 or float, structuring element `se`, anchor at its centre, default
+    border = morphologyDefaultBorderValue: pixels outside the image never win the min / max)
+  cv2.floodFill(im, mask, (0, 0), 1) with default flags: 4-connected, fills the seed's
+    connected set of pixels EQUAL to the seed value with 1
+scipy.signal.convolve2d and scipy.ndimage.distance_transform_edt are the reference's own calls.
+Parity of this module to the reference is therefore "pinned to restated cv2 semantics".
+"""
+import math
+
+import numpy as np
+from scipy import ndimage, signal
+
+EPS = np.finfo(float).eps  # sys.float_info.epsilon, Coupled_motion_planner.py:17
+
+
+def surface_normal(resolution, size, z):
+    """Coupled_motion_planner.py:37-80: unit normals of the DEM z on the grid
+    linspace(0, size, round(size / resolution)) in x and y, with quadratic edge extrapolation."""
+    n0 = int(round(size / resolution))
+    xm = np.linspace(0, size, n0)
+    ym = np.linspace(0, size, n0)
+    x, y = np.meshgrid(xm, ym)
+    m, n = x.shape
+
+    def pad(a):  # :51-56  3 a0 - 3 a1 + a2 on each side
+        a = np.vstack((3 * a[0, :] - 3 * a[1, :] + a[2, :], a, 3 * a[m - 1, :] - 3 * a[m - 2, :] + a[m - 3, :]))
+        return np.hstack((np.array([3 * a[:, 0] - 3 * a[:, 1] + a[:, 2]]).T, a,
+                          np.array([3 * a[:, n - 1] - 3 * a[:, n - 2] + a[:, n - 3]]).T))
+
+    xx, yy, zz = pad(x), pad(y), pad(np.asarray(z, dtype=np.float64))
+    s1 = np.array([[0, 0, 0], [1, 0, -1], [0, 0, 0]]) / 2  # :48-49
+    s2 = np.array([[0, -1, 0], [0, 0, 0], [0, 1, 0]]) / 2
+    ax = -signal.convolve2d(xx, np.flipud(s1), mode="valid")
+    ay = -signal.convolve2d(yy, np.flipud(s1), mode="valid")
+    az = -signal.convolve2d(zz, np.flipud(s1), mode="valid")
+    bx = signal.convolve2d(xx, np.flipud(s2), mode="valid")
+    by = signal.convolve2d(yy, np.flipud(s2), mode="valid")
+    bz = signal.convolve2d(zz, np.flipud(s2), mode="valid")
+    nx = -(ay * bz - az * by)  # :70-72
+    ny = -(az * bx - ax * bz)
+    nz = -(ax * by - ay * bx)
+    mag = np.sqrt(nx * nx + ny * ny + nz * nz)  # :74-75
+    mag[np.where(mag == 0)] = EPS
+    return nx / mag, ny / mag, nz / mag
+
+
+def structural_disk(r):
+    """Coupled_motion_planner.py:96-105: (2r+1)^2 uint8 disk, d = sqrt((r-i)^2 + (r-j)^2) <= r."""
+    se = np.zeros((2 * r + 1, 2 * r + 1), np.uint8)
+    for i in range(2 * r + 1):
+        for j in range(2 * r + 1):
+            if math.sqrt((r - i) ** 2 + (r - j) ** 2) <= r:
+                se[i][j] = 1
+    return se
+
+
+def _morph(im, se, op):
+    """cv2.erode (op=min) / cv2.dilate (op=max) with anchor at the centre of se; pixels outside
+    the image take no part (cv2's default border value for morphology)."""
+    im = np.asarray(im)
+    H, W = im.shape
+    r = se.shape[0] // 2
+    out = np.empty_like(im)
+    ident = np.iinfo(im.dtype).max if np.issubdtype(im.dtype, np.integer) else np.inf
+    if op is np.maximum:
+        ident = np.iinfo(im.dtype).min if np.issubdtype(im.dtype, np.integer) else -np.inf
+    acc = np.full(im.shape, ident, dtype=im.dtype)
+    for di in range(-r, r + 1):
+        for dj in range(-r, r + 1):
+            if not se[di + r, dj + r]:
+                continue
+            # acc[y, x] = op(acc[y, x], im[y + di, x + dj]) where in range
+            ys0, ys1 = max(0, -di), min(H, H - di)
+            xs0, xs1 = max(0, -dj), min(W, W - dj)
+            if ys0 >= ys1 or xs0 >= xs1:
+                continue
+            acc[ys0:ys1, xs0:xs1] = op(acc[ys0:ys1, xs0:xs1], im[ys0 + di:ys1 + di, xs0 + dj:xs1 + dj])
+    out[...] = acc
+    return out
+
+
+def erode(im, se):
+    return _morph(im, se, np.minimum)
+
+
+def dilate(im, se):
+    return _morph(im, se, np.maximum)
+
+
+def image_filling(im):
+    """Coupled_motion_planner.py:82-94 with cv2.floodFill restated: the 4-connected set of
+    pixels equal to im[0, 0] that contains (0, 0) is set to 1; then
+    im | (bitwise_not(filled) - 254) in uint8 arithmetic (holes -> 1; if im[0, 0] == 1 every
+    pixel ends up 1 -- the reference's behaviour)."""
+    im = np.asarray(im, dtype=np.uint8)
+    seedval = im[0, 0]
+    lab, _ = ndimage.label(im == seedval, structure=np.array([[0, 1, 0], [1, 1, 1], [0, 1, 0]]))
+    filled = im.copy()
+    filled[lab == lab[0, 0]] = 1
+    inv = (np.bitwise_not(filled).astype(np.int32) - 254).astype(np.uint8)  # uint8 wrap as numpy/cv2
+    return im | inv
+
+
+def cost_map(Zs, resolution, size, slope_max=0.20, diagonal=0.9, expansion=1.0, gradient=10.0):
+    """The cost raster of main() (Coupled_motion_planner.py:1100-1216) from the DEM Zs
+    (loaded at :1098-1099).  Cited lines are those of the reference file.  Returns (cMap, obstMap): cMap exactly as the reference holds it
+    before calling FM.biComputeTmap(cMap.T, ...) (i.e. indexed [x, y]), obstMap [y, x] float64."""
+    Zs = np.asarray(Zs, dtype=np.float64)
+    Zs = Zs - np.min(Zs)  # :1101
+    _, _, Nz = surface_normal(resolution, size, Zs)  # :1104
+    slope = np.arccos(Nz)  # :1145
+    obst = np.zeros(Zs.shape)
+    obst[slope > slope_max] = 1  # :1154 (borders cleared :1157-1160)
+    obst[0, :] = 0
+    obst[-1, :] = 0
+    obst[:, 0] = 0
+    obst[:, -1] = 0
+    obst = np.uint8(obst)
+    obst = image_filling(obst)  # :1163-1164
+    se = structural_disk(10)  # :1167-1169
+    obst = erode(obst, se)
+    obst = dilate(obst, se)
+    se = structural_disk(int(round((diagonal / 2) / resolution)))  # :1172-1178
+    obst = dilate(obst, se)
+    obst = image_filling(obst)
+    obst = erode(obst, se)
+    obst[0, :] = 1  # :1180-1184
+    obst[-1, :] = 1
+    obst[:, 0] = 1
+    obst[:, -1] = 1
+    obst = np.float64(obst)
+    high = obst * 300  # :1187
+    se = structural_disk(int(round(expansion / resolution)))  # :1190-1192
+    dil = dilate(obst, se)
+    dist = resolution * ndimage.distance_transform_edt(obst == 0)  # :1194
+    od = dil * (1 - dist / (np.max(dist)))  # :1196
+    pos = od > 0
+    if np.any(pos):
+        od[pos] = od[pos] - np.min(od[pos])  # :1197-1198
+    cmap = 1 + (high + od * gradient).T  # :1200-1205
+    h = np.ones((50, 50)) / 50 ** 2  # :1208-1210
+    cmap = signal.convolve2d(cmap, np.flipud(h), mode="same", fillvalue=300)
+    cmap[0, :] = np.inf  # :1213-1216
+    cmap[-1, :] = np.inf
+    cmap[:, 0] = np.inf
+    cmap[:, -1] = np.inf
+    return cmap, obst

@@ -1,0 +1,421 @@
+// costmap.hip -- the planner's cost-raster builder on gfx950: the producer of the Eikonal
+// solver's input (Coupled_motion_planner.py:37-105 and :1101-1216).
+//
+//   DEM Z --(min, quadratic-extrapolated central differences, cross product)--> unit normals
+//     --(arccos(Nz) > slope_max)--> obstacle mask --(flood fill, disk erode/dilate, ...)-->
+//     --(300 * obstacle + 10 * distance ramp, 50 x 50 box blur)--> cost raster
+//
+// All stages are HBM-bound elementwise / stencil / line passes.  Morphology with the
+// reference's disk structuring element (d <= r on integer offsets, structural_disk :96-105)
+// is computed EXACTLY through the squared Euclidean distance transform: dilate(A, disk r)(p) =
+// [dist^2(p, A) <= r^2], erode(A, disk r)(p) = A(p) and [dist^2(p, not A) > r^2] (pixels outside
+// the image take no part, as cv2's default morphology border).  The EDT is the separable exact
+// one (column distances, then the lower envelope of parabolas per row), in int32 -- the same
+// squared distances scipy.ndimage.distance_transform_edt takes the sqrt of (:1194).  The flood
+// fill of image_filling (:82-94, cv2.floodFill 4-connected from (0, 0)) is reachability, i.e.
+// the block-FIM solver itself with cost 1 on the seed's value and +inf elsewhere (host side).
+//
+// Floating point: IEEE f64 without contraction, the reference's operation order where it is
+// defined (stencils: two non-zero taps, exact halvings; normals; ramp); the box blur sums in a
+// different order than scipy's convolve2d (relative 1e-15).
+#include "eik_common.hpp"
+#include "eik_kernels.hpp"
+
+#pragma clang fp contract(off)
+
+namespace eik {
+
+constexpr int kCmThreads = 256;
+
+// linspace(0, size, n)[i] as numpy computes it: i * step, the last element exactly `size`
+__device__ __forceinline__ double lin(double size, int64_t n, int64_t i) {
+    const double step = size / (double)(n - 1);
+    return i == n - 1 ? size : (double)i * step;
+}
+
+// value of the quadratically extrapolated padding (Coupled_motion_planner.py:51-56) of a 1D grid
+__device__ __forceinline__ double lin_pad(double size, int64_t n, int64_t i) {
+    if (i < 0) return 3 * lin(size, n, 0) - 3 * lin(size, n, 1) + lin(size, n, 2);
+    if (i >= n) return 3 * lin(size, n, n - 1) - 3 * lin(size, n, n - 2) + lin(size, n, n - 3);
+    return lin(size, n, i);
+}
+
+// Z - zmin with the reference's padding: vertical padding first, then the horizontal padding of
+// the vertically padded array (:51-56), so corners extrapolate the padded rows.
+struct Zpad {
+    const double* Z;
+    int64_t H, W;
+    double zmin;
+    __device__ double at(int64_t y, int64_t x) const { return Z[y * W + x] - zmin; }
+    __device__ double vpad(int64_t y, int64_t x) const {  // rows -1..H, x in [0, W)
+        if (y < 0) return 3 * at(0, x) - 3 * at(1, x) + at(2, x);
+        if (y >= H) return 3 * at(H - 1, x) - 3 * at(H - 2, x) + at(H - 3, x);
+        return at(y, x);
+    }
+    __device__ double operator()(int64_t y, int64_t x) const {  // rows -1..H, cols -1..W
+        if (x < 0) return 3 * vpad(y, 0) - 3 * vpad(y, 1) + vpad(y, 2);
+        if (x >= W) return 3 * vpad(y, W - 1) - 3 * vpad(y, W - 2) + vpad(y, W - 3);
+        return vpad(y, x);
+    }
+};
+
+// min of Z (bit-pattern atomic on the order-preserving map of doubles)
+__device__ __forceinline__ unsigned long long dkey(double v) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    return (b >> 63) ? ~b : (b | (1ull << 63));
+}
+__device__ __forceinline__ double dval(unsigned long long k) {
+    return __longlong_as_double((long long)((k >> 63) ? (k & ~(1ull << 63)) : ~k));
+}
+
+__global__ void cm_min_kernel(const double* __restrict__ Z, int64_t n, unsigned long long* out) {
+    unsigned long long best = ~0ull;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const unsigned long long k = dkey(Z[i]);
+        best = k < best ? k : best;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long v = __shfl_xor(best, o);
+        best = v < best ? v : best;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMin(out, best);
+}
+
+// surface_normal (:37-80) per node; obstacle = arccos(Nz) > slope_max (:1145-1154), border 0
+// (:1157-1160).  Optional Nx/Ny/Nz outputs (the Python drop-in's surface_normal).
+__global__ void cm_normals_kernel(const double* __restrict__ Z, int64_t H, int64_t W, double size,
+                                  const unsigned long long* __restrict__ zmin_key, double slope_max,
+                                  unsigned char* __restrict__ obst, double* __restrict__ Nx, double* __restrict__ Ny,
+                                  double* __restrict__ Nz) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= H * W) return;
+    const int64_t y = idx / W, x = idx - (idx / W) * W;
+    const Zpad zp{Z, H, W, dval(*zmin_key)};
+    // stencil1 (x): conv = 0.5 A[y][x+1] + (-0.5) A[y][x-1], a = -conv (:58-60)
+    // stencil2 (y): conv = 0.5 A[y+1][x] + (-0.5) A[y-1][x], b = conv (:62-64)
+    const double xp = lin_pad(size, W, x + 1), xm = lin_pad(size, W, x - 1);
+    const double yp = lin_pad(size, H, y + 1), ym = lin_pad(size, H, y - 1);
+    const double xc = lin_pad(size, W, x), yc = lin_pad(size, H, y);
+    const double ax = -(0.5 * xp + -0.5 * xm);
+    const double ay = -(0.5 * yc + -0.5 * yc);
+    const double az = -(0.5 * zp(y, x + 1) + -0.5 * zp(y, x - 1));
+    const double bx = 0.5 * xc + -0.5 * xc;
+    const double by = 0.5 * yp + -0.5 * ym;
+    const double bz = 0.5 * zp(y + 1, x) + -0.5 * zp(y - 1, x);
+    const double nx = -(ay * bz - az * by);  // :70-72
+    const double ny = -(az * bx - ax * bz);
+    const double nz = -(ax * by - ay * bx);
+    double mag = __builtin_sqrt(nx * nx + ny * ny + nz * nz);  // :74-75
+    if (mag == 0) mag = 2.220446049250313e-16;
+    const double nzn = nz / mag;
+    if (Nx) {
+        Nx[idx] = nx / mag;
+        Ny[idx] = ny / mag;
+        Nz[idx] = nzn;
+    }
+    if (obst) {
+        const bool border = y == 0 || x == 0 || y == H - 1 || x == W - 1;
+        obst[idx] = (!border && acos(nzn) > slope_max) ? 1 : 0;
+    }
+}
+
+// ---- exact squared EDT to the pixels where feat(p) is true ------------------------------
+// pass 1, one thread per column: g = |y - nearest feature row in the column| (or kFar)
+constexpr int kFar = 1 << 29;
+
+template <typename F>
+__global__ void cm_edt_cols_kernel(F feat, int64_t H, int64_t W, int* __restrict__ g) {
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= W) return;
+    int d = kFar;
+    for (int64_t y = 0; y < H; ++y) {
+        d = feat(y * W + x) ? 0 : (d >= kFar ? kFar : d + 1);
+        g[y * W + x] = d;
+    }
+    d = kFar;
+    for (int64_t y = H - 1; y >= 0; --y) {
+        const int v = g[y * W + x];
+        d = v == 0 ? 0 : (d >= kFar ? kFar : d + 1);
+        if (d < v) g[y * W + x] = d;
+    }
+}
+
+// pass 2, one thread per row: D(x) = min_q (x - q)^2 + g(q)^2 by the lower envelope of
+// parabolas (Felzenszwalb-Huttenlocher), in exact integer arithmetic; kFar columns have no
+// feature.  Scratch per row: v (W ints), z (W + 1 ints as doubles' stand-in: rationals compared
+// by cross-multiplication).
+__global__ void cm_edt_rows_kernel(const int* __restrict__ g, int64_t H, int64_t W, int* __restrict__ D,
+                                   int* __restrict__ vbuf) {
+    const int64_t y = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (y >= H) return;
+    const int* gr = g + y * W;
+    int* v = vbuf + y * W;  // parabola apexes of the envelope
+    int* out = D + y * W;
+    auto f = [&](int q) -> long long { const long long t = gr[q]; return t * t; };
+    // intersection abscissa of parabolas q1 < q2: s = ((f(q2) + q2^2) - (f(q1) + q1^2)) / (2 (q2 - q1))
+    int k = -1;
+    for (int q = 0; q < (int)W; ++q) {
+        if (gr[q] >= kFar) continue;
+        while (k >= 0) {
+            const int p = v[k];
+            if (k == 0) break;
+            const int pp = v[k - 1];
+            // remove p if the new parabola q overtakes p before p overtakes pp:
+            // s(pp, p) >= s(p, q)
+            const long long num1 = (f(p) + (long long)p * p) - (f(pp) + (long long)pp * pp), den1 = 2ll * (p - pp);
+            const long long num2 = (f(q) + (long long)q * q) - (f(p) + (long long)p * p), den2 = 2ll * (q - p);
+            if (num1 * den2 >= num2 * den1) --k;
+            else break;
+        }
+        v[++k] = q;
+    }
+    if (k < 0) {
+        for (int x = 0; x < (int)W; ++x) out[x] = INT32_MAX;
+        return;
+    }
+    int j = 0;
+    for (int x = 0; x < (int)W; ++x) {
+        // advance while the next parabola is lower at x
+        while (j < k) {
+            const long long a = (long long)(x - v[j]) * (x - v[j]) + f(v[j]);
+            const long long b = (long long)(x - v[j + 1]) * (x - v[j + 1]) + f(v[j + 1]);
+            if (b <= a) ++j;
+            else break;
+        }
+        const long long d = (long long)(x - v[j]) * (x - v[j]) + f(v[j]);
+        out[x] = d > INT32_MAX ? INT32_MAX : (int)d;
+    }
+}
+
+struct FeatEq {  // feat = (m[i] == val)
+    const unsigned char* m;
+    unsigned char val;
+    __device__ bool operator()(int64_t i) const { return m[i] == val; }
+};
+
+hipError_t cm_edt(const unsigned char* m, unsigned char val, int64_t H, int64_t W, int* g, int* D, int* vbuf,
+                  hipStream_t st) {
+    hipLaunchKernelGGL(cm_edt_cols_kernel<FeatEq>, dim3((unsigned)((W + 63) / 64)), dim3(64), 0, st, FeatEq{m, val}, H,
+                       W, g);
+    hipLaunchKernelGGL(cm_edt_rows_kernel, dim3((unsigned)((H + 63) / 64)), dim3(64), 0, st, g, H, W, D, vbuf);
+    return hipGetLastError();
+}
+
+// morphology from the squared EDT: dilate: out = D(to A) <= r^2; erode: out = A && D(to not A) > r^2
+__global__ void cm_morph_kernel(const unsigned char* __restrict__ A, const int* __restrict__ D, int64_t n, int r2,
+                                int erode, unsigned char* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = erode ? (unsigned char)(A[i] && D[i] > r2) : (unsigned char)(D[i] <= r2);
+}
+
+// Disk morphology needs distances only up to r: a radius-bounded separable transform, one
+// thread per pixel.  Pass V: gv(p) = min |dy| <= r with a feature at (y + dy, x), else r + 1.
+// Pass H: p is within r of a feature iff some |dx| <= r has dx^2 + gv(y, x + dx)^2 <= r^2
+// (the nearest feature q has |qy - py| <= r and |qx - px| <= r) -- exact, like the full EDT.
+__global__ void cm_bnd_cols_kernel(const unsigned char* __restrict__ A, int64_t H, int64_t W, int r,
+                                   unsigned char want, unsigned char* __restrict__ gv) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= H * W) return;
+    const int64_t y = i / W, x = i - (i / W) * W;
+    int d = r + 1;
+    for (int k = 0; k <= r; ++k) {
+        const bool up = y - k >= 0 && A[(y - k) * W + x] == want;
+        const bool dn = y + k < H && A[(y + k) * W + x] == want;
+        if (up || dn) { d = k; break; }
+    }
+    gv[i] = (unsigned char)d;
+}
+
+__global__ void cm_bnd_rows_kernel(const unsigned char* __restrict__ A, const unsigned char* __restrict__ gv, int64_t H,
+                                   int64_t W, int r, int erode, unsigned char* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= H * W) return;
+    const int64_t y = i / W, x = i - (i / W) * W;
+    const int r2 = r * r;
+    bool near = false;
+    for (int k = 0; k <= r && !near; ++k) {
+        const int k2 = k * k;
+        if (x - k >= 0) { const int g = gv[y * W + x - k]; near |= g <= r && k2 + g * g <= r2; }
+        if (x + k < W) { const int g = gv[y * W + x + k]; near |= g <= r && k2 + g * g <= r2; }
+    }
+    out[i] = erode ? (unsigned char)(A[i] && !near) : (unsigned char)near;
+}
+
+hipError_t cm_morph(const unsigned char* A, int64_t H, int64_t W, int r, bool erode, unsigned char* out, int* g, int* D,
+                    int* vbuf, hipStream_t st) {
+    (void)D;
+    (void)vbuf;
+    const int64_t n = H * W;
+    if (r > 250) {  // beyond the uint8 bounded form: the full EDT
+        hipError_t e = cm_edt(A, erode ? 0 : 1, H, W, g, D, vbuf, st);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(cm_morph_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A, D, n, r * r,
+                           erode ? 1 : 0, out);
+        return hipGetLastError();
+    }
+    unsigned char* gv = reinterpret_cast<unsigned char*>(g);
+    const unsigned grid = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(cm_bnd_cols_kernel, dim3(grid), dim3(256), 0, st, A, H, W, r, (unsigned char)(erode ? 0 : 1), gv);
+    hipLaunchKernelGGL(cm_bnd_rows_kernel, dim3(grid), dim3(256), 0, st, A, gv, H, W, r, erode ? 1 : 0, out);
+    return hipGetLastError();
+}
+
+// ---- image_filling (:82-94) around a reachability solve ---------------------------------
+// cost for the flood fill: 1 on pixels equal to the seed value m[0], +inf elsewhere
+__global__ void cm_fill_cost_kernel(const unsigned char* __restrict__ m, int64_t n, float* __restrict__ c) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    c[i] = m[i] == m[0] ? 1.f : __builtin_inff();
+}
+// filled = seed pixel's component set to 1; out = m | (~filled - 254) (uint8): seed 0 -> holes
+// (zeros not reached) become 1; seed 1 -> every pixel 1 (the reference's arithmetic)
+__global__ void cm_fill_apply_kernel(unsigned char* __restrict__ m, const float* __restrict__ T, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const unsigned char seed = m[0];  // read before any write: m[0] is never changed by this kernel
+    const unsigned char filled = (m[i] == seed && T[i] != __builtin_inff()) ? 1 : m[i];
+    const unsigned char inv = (unsigned char)((unsigned char)~filled - 254);
+    m[i] = m[i] | inv;
+}
+
+hipError_t cm_fill_cost(const unsigned char* m, int64_t n, float* c, hipStream_t st) {
+    hipLaunchKernelGGL(cm_fill_cost_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, m, n, c);
+    return hipGetLastError();
+}
+hipError_t cm_fill_apply(unsigned char* m, const float* T, int64_t n, hipStream_t st) {
+    hipLaunchKernelGGL(cm_fill_apply_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, m, T, n);
+    return hipGetLastError();
+}
+
+__global__ void cm_border_kernel(unsigned char* __restrict__ m, int64_t H, int64_t W, unsigned char v) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < W) {
+        m[i] = v;
+        m[(H - 1) * W + i] = v;
+    }
+    if (i < H) {
+        m[i * W] = v;
+        m[i * W + W - 1] = v;
+    }
+}
+
+// ---- cost (:1187-1205) ---------------------------------------------------------------------
+// dist = res * sqrt(D); atomic max of dist (non-negative doubles: bit order = value order)
+__global__ void cm_dist_kernel(const int* __restrict__ D, int64_t n, double res, double* __restrict__ dist,
+                               unsigned long long* maxbits) {
+    unsigned long long best = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const double d = res * __builtin_sqrt((double)D[i]);
+        dist[i] = d;
+        const unsigned long long b = (unsigned long long)__double_as_longlong(d);
+        best = b > best ? b : best;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long v = __shfl_xor(best, o);
+        best = v > best ? v : best;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMax(maxbits, best);
+}
+
+// od = dil * (1 - dist / max) (:1196), written into dist; atomic min over od > 0
+__global__ void cm_ramp_kernel(const unsigned char* __restrict__ dil, double* __restrict__ dist, int64_t n,
+                               const unsigned long long* __restrict__ maxbits, unsigned long long* minbits) {
+    const double mx = __longlong_as_double((long long)*maxbits);
+    unsigned long long best = ~0ull;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const double od = (double)dil[i] * (1 - dist[i] / mx);
+        dist[i] = od;
+        if (od > 0) {
+            const unsigned long long b = (unsigned long long)__double_as_longlong(od);
+            best = b < best ? b : best;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long v = __shfl_xor(best, o);
+        best = v < best ? v : best;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMin(minbits, best);
+}
+
+// base = 1 + (300 obst + (od - min[od > 0]) * gradient) (:1187, :1197-1205), [y][x]
+__global__ void cm_base_kernel(const unsigned char* __restrict__ obst, const double* __restrict__ od, int64_t n,
+                               const unsigned long long* __restrict__ minbits, double high, double gradient,
+                               double* __restrict__ base) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double v = od[i];
+    if (v > 0) v = v - __longlong_as_double((long long)*minbits);
+    base[i] = 1 + ((double)obst[i] * high + v * gradient);
+}
+
+// 50 x 50 box blur with fill value 300 (:1208-1210): window [-25, +24] on both axes (scipy
+// 'same' for an even kernel), separable: rows with fill 300, then columns with fill 50 * 300.
+// The reference's cMap is the transpose of `base`; the window treats both axes alike, so the
+// blur of base equals the transpose of the reference's blurred cMap.
+constexpr int kBox = 50, kBoxLo = 25, kBoxHi = kBox - 1 - kBoxLo;
+
+__global__ void cm_box_rows_kernel(const double* __restrict__ in, int64_t H, int64_t W, double fill,
+                                   double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= H * W) return;
+    const int64_t y = i / W, x = i - (i / W) * W;
+    double s = 0;
+    for (int k = -kBoxLo; k <= kBoxHi; ++k) {
+        const int64_t xx = x + k;
+        s += (xx >= 0 && xx < W) ? in[y * W + xx] : fill;
+    }
+    out[i] = s;
+}
+
+__global__ void cm_box_cols_kernel(const double* __restrict__ in, int64_t H, int64_t W, double fill, double scale,
+                                   double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= H * W) return;
+    const int64_t y = i / W, x = i - (i / W) * W;
+    double s = 0;
+    for (int k = -kBoxLo; k <= kBoxHi; ++k) {
+        const int64_t yy = y + k;
+        s += (yy >= 0 && yy < H) ? in[yy * W + x] : fill;
+    }
+    const bool border = y == 0 || x == 0 || y == H - 1 || x == W - 1;  // :1213-1216
+    out[i] = border ? __builtin_inf() : s * scale;
+}
+
+// ------------------------------------------------------------------------- host launchers
+hipError_t cm_normals(const double* Z, int64_t H, int64_t W, double size, unsigned long long* zmin, double slope_max,
+                      unsigned char* obst, double* Nx, double* Ny, double* Nz, hipStream_t st) {
+    const int64_t n = H * W;
+    hipError_t e = hipMemsetAsync(zmin, 0xff, sizeof(unsigned long long), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(cm_min_kernel, dim3((unsigned)std::min<int64_t>(1024, (n + 255) / 256)), dim3(256), 0, st, Z, n,
+                       zmin);
+    hipLaunchKernelGGL(cm_normals_kernel, dim3((unsigned)((n + kCmThreads - 1) / kCmThreads)), dim3(kCmThreads), 0, st,
+                       Z, H, W, size, zmin, slope_max, obst, Nx, Ny, Nz);
+    return hipGetLastError();
+}
+
+hipError_t cm_border(unsigned char* m, int64_t H, int64_t W, unsigned char v, hipStream_t st) {
+    const int64_t n = H > W ? H : W;
+    hipLaunchKernelGGL(cm_border_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, m, H, W, v);
+    return hipGetLastError();
+}
+
+hipError_t cm_cost(const unsigned char* obst, const unsigned char* dil, const int* Dobst, int64_t H, int64_t W,
+                   double res, double high, double gradient, double* work, double* tmp, double* cost,
+                   unsigned long long* red, hipStream_t st) {
+    const int64_t n = H * W;
+    const unsigned grid_red = (unsigned)std::min<int64_t>(1024, (n + 255) / 256), grid = (unsigned)((n + 255) / 256);
+    hipError_t e = hipMemsetAsync(red, 0, sizeof(unsigned long long), st);  // max
+    if (e == hipSuccess) e = hipMemsetAsync(red + 1, 0xff, sizeof(unsigned long long), st);  // min
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(cm_dist_kernel, dim3(grid_red), dim3(256), 0, st, Dobst, n, res, work, red);
+    hipLaunchKernelGGL(cm_ramp_kernel, dim3(grid_red), dim3(256), 0, st, dil, work, n, red, red + 1);
+    hipLaunchKernelGGL(cm_base_kernel, dim3(grid), dim3(256), 0, st, obst, work, n, red + 1, high, gradient, tmp);
+    hipLaunchKernelGGL(cm_box_rows_kernel, dim3(grid), dim3(256), 0, st, tmp, H, W, 300.0, work);
+    hipLaunchKernelGGL(cm_box_cols_kernel, dim3(grid), dim3(256), 0, st, work, H, W, 300.0 * kBox,
+                       1.0 / (kBox * kBox), cost);
+    return hipGetLastError();
+}
+
+}  // namespace eik

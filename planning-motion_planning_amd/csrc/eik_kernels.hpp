@@ -102,6 +102,20 @@ struct Gdm3dArgs {
 };
 hipError_t gdm3d(const Gdm3dArgs& a, bool f64, hipStream_t st);
 
+// Cost-raster builder (costmap.hip), f64 DEM -> f64 cost, uint8 obstacle masks.
+hipError_t cm_normals(const double* Z, int64_t H, int64_t W, double size, unsigned long long* zmin, double slope_max,
+                      unsigned char* obst, double* Nx, double* Ny, double* Nz, hipStream_t st);
+hipError_t cm_morph(const unsigned char* A, int64_t H, int64_t W, int r, bool erode, unsigned char* out, int* g, int* D,
+                    int* vbuf, hipStream_t st);
+hipError_t cm_edt(const unsigned char* m, unsigned char val, int64_t H, int64_t W, int* g, int* D, int* vbuf,
+                  hipStream_t st);
+hipError_t cm_fill_cost(const unsigned char* m, int64_t n, float* c, hipStream_t st);
+hipError_t cm_fill_apply(unsigned char* m, const float* T, int64_t n, hipStream_t st);
+hipError_t cm_border(unsigned char* m, int64_t H, int64_t W, unsigned char v, hipStream_t st);
+hipError_t cm_cost(const unsigned char* obst, const unsigned char* dil, const int* Dobst, int64_t H, int64_t W,
+                   double res, double high, double gradient, double* work, double* tmp, double* cost,
+                   unsigned long long* red, hipStream_t st);
+
 // Full-field inf-aware normalised gradient (computeGradient(T, point=[]), FastMarching.py:242-300)
 hipError_t gradient2d(const double* T, int64_t H, int64_t W, double* gnx, double* gny, hipStream_t st);
 

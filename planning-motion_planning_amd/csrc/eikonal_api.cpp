@@ -65,6 +65,8 @@ struct eik_ctx {
     eik_stats last{};
     eik_fim2d* cached = nullptr;  // solver reused by the host-buffer entry points
     eik_fim2d* cached_l = nullptr;  // queue state of the layered 3D solver (fim2dl.hip)
+    eik_fim2d* cached_fill = nullptr;  // reachability solver of the cost builder's hole filling
+    DevBuf cm_u8, cm_i32, cm_f32, cm_f64;  // cost-builder scratch
     int resident_l[5] = {0, 0, 0, 0, 0};  // co-resident workgroups of fim2dl_persist_kernel<nl>
     DevBuf cost, T, T2, goals, work, misc;
     DevBuf l3, c3, m3, v3;             // 3D solver scratch (lists, counts, marks, visits)
@@ -148,6 +150,7 @@ void eik_destroy(eik_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->cached) eik_fim2d_destroy(c->cached);
     if (c->cached_l) eik_fim2d_destroy(c->cached_l);
+    if (c->cached_fill) eik_fim2d_destroy(c->cached_fill);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -855,6 +858,128 @@ int eik_gradient2d_f64(eik_ctx* c, const double* T, int64_t H, int64_t W, double
     HIPCHK(c, gradient2d((const double*)c->T2.p, H, W, gx, gx + n, c->stream));
     HIPCHK(c, hipMemcpyAsync(gnx, gx, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(gny, gx + n, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return EIK_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ cost-raster builder
+// image_filling (:82-94) of the device mask m in place: reachability of the pixels equal to
+// m[0] from (0, 0) (the 4-connected flood fill) by the block-FIM solver on cost 1 / +inf.
+static int cm_fill(eik_ctx* c, unsigned char* m, int64_t H, int64_t W, float* fcost, float* fT, hipStream_t st) {
+    eik_fim2d* f = c->cached_fill;
+    if (!f || f->H != H || f->W != W) {
+        if (f) eik_fim2d_destroy(f);
+        c->cached_fill = nullptr;
+        int rc = eik_fim2d_create(c, 1, H, W, EIK_F32, &f);
+        if (rc) return rc;
+        c->cached_fill = f;
+    }
+    HIPCHK(c, cm_fill_cost(m, H * W, fcost, st));
+    const int64_t goal[2] = {0, 0};
+    const eik_stats keep = c->last;  // the builder's internal solves do not count as the caller's
+    int rc = eik_fim2d_solve(f, fcost, fT, goal, st);
+    c->last = keep;
+    if (rc) return rc;
+    HIPCHK(c, cm_fill_apply(m, fT, H * W, st));
+    return EIK_OK;
+}
+
+extern "C" {
+
+int eik_costmap_dev(eik_ctx* c, const double* d_Z, int64_t H, int64_t W, double res, double size,
+                    const eik_costmap_params* params, double* d_cost, uint8_t* d_obst, void* stream) {
+    if (!c || !d_Z || !d_cost || H < 3 || W < 3 || !(res > 0) || !(size > 0))
+        return c ? set_err(c, EIK_ERR_ARG, "bad cost-map arguments") : EIK_ERR_ARG;
+    const eik_costmap_params p = params ? *params : eik_costmap_params{0.20, 0.9, 1.0, 10.0, 300.0};
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t n = H * W;
+    // scratch: 3 masks, 3 int planes (column distances, squared EDT, envelope apexes), 2 f32 (fill
+    // cost, fill T), 2 f64 planes, reduction words
+    HIPCHK(c, c->cm_u8.ensure(3 * n + 64));
+    HIPCHK(c, c->cm_i32.ensure(sizeof(int) * 3 * n));
+    HIPCHK(c, c->cm_f32.ensure(sizeof(float) * 2 * n));
+    HIPCHK(c, c->cm_f64.ensure(sizeof(double) * 2 * n + 64));
+    unsigned char* obst = d_obst ? d_obst : (unsigned char*)c->cm_u8.p;
+    unsigned char* tmp = (unsigned char*)c->cm_u8.p + n;
+    unsigned char* dil = (unsigned char*)c->cm_u8.p + 2 * n;
+    int* g = (int*)c->cm_i32.p;
+    int* D = g + n;
+    int* vbuf = g + 2 * n;
+    float* fcost = (float*)c->cm_f32.p;
+    float* fT = fcost + n;
+    double* work = (double*)c->cm_f64.p;
+    double* tmpd = work + n;
+    unsigned long long* red = (unsigned long long*)(tmpd + n);
+    const int r1 = 10;                                              // :1167
+    const int r2 = (int)std::nearbyint((p.diagonal / 2) / res);     // :1172-1173
+    const int r3 = (int)std::nearbyint(p.expansion / res);          // :1190-1191
+    HIPCHK(c, cm_normals(d_Z, H, W, size, red, p.slope_max, obst, nullptr, nullptr, nullptr, st));  // :1104-1160
+    int rc = cm_fill(c, obst, H, W, fcost, fT, st);                 // :1163-1164
+    if (rc) return rc;
+    HIPCHK(c, cm_morph(obst, H, W, r1, true, tmp, g, D, vbuf, st));  // :1168
+    HIPCHK(c, cm_morph(tmp, H, W, r1, false, obst, g, D, vbuf, st)); // :1169
+    HIPCHK(c, cm_morph(obst, H, W, r2, false, tmp, g, D, vbuf, st)); // :1175
+    rc = cm_fill(c, tmp, H, W, fcost, fT, st);                      // :1176
+    if (rc) return rc;
+    HIPCHK(c, cm_morph(tmp, H, W, r2, true, obst, g, D, vbuf, st));  // :1177
+    HIPCHK(c, cm_border(obst, H, W, 1, st));                         // :1180-1184
+    HIPCHK(c, cm_morph(obst, H, W, r3, false, dil, g, D, vbuf, st)); // :1192
+    HIPCHK(c, cm_edt(obst, 1, H, W, g, D, vbuf, st));                // :1194 (distance to obstacles)
+    HIPCHK(c, cm_cost(obst, dil, D, H, W, res, p.high, p.gradient, work, tmpd, d_cost, red, st));  // :1187-1216
+    return EIK_OK;
+}
+
+int eik_costmap_f64(eik_ctx* c, const double* Z, int64_t H, int64_t W, double res, double size,
+                    const eik_costmap_params* params, double* cost_out, uint8_t* obst_out) {
+    if (!c || !Z || !cost_out) return c ? set_err(c, EIK_ERR_ARG, "NULL argument") : EIK_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t n = H * W;
+    HIPCHK(c, c->T2.ensure(sizeof(double) * 2 * n + n));
+    double* dZ = (double*)c->T2.p;
+    double* dC = dZ + n;
+    uint8_t* dO = (uint8_t*)(dC + n);
+    HIPCHK(c, hipMemcpyAsync(dZ, Z, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    int rc = eik_costmap_dev(c, dZ, H, W, res, size, params, dC, dO, c->stream);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(cost_out, dC, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+    if (obst_out) HIPCHK(c, hipMemcpyAsync(obst_out, dO, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return EIK_OK;
+}
+
+int eik_surface_normal_f64(eik_ctx* c, const double* Z, int64_t H, int64_t W, double size, double* Nx, double* Ny,
+                           double* Nz) {
+    if (!c || !Z || !Nx || !Ny || !Nz || H < 3 || W < 3 || !(size > 0))
+        return c ? set_err(c, EIK_ERR_ARG, "bad surface_normal arguments") : EIK_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t n = H * W;
+    HIPCHK(c, c->T2.ensure(sizeof(double) * 4 * n + 64));
+    double* dZ = (double*)c->T2.p;
+    unsigned long long* red = (unsigned long long*)(dZ + 4 * n);
+    HIPCHK(c, hipMemcpyAsync(dZ, Z, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, cm_normals(dZ, H, W, size, red, 0.0, nullptr, dZ + n, dZ + 2 * n, dZ + 3 * n, c->stream));
+    HIPCHK(c, hipMemcpyAsync(Nx, dZ + n, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(Ny, dZ + 2 * n, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(Nz, dZ + 3 * n, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return EIK_OK;
+}
+
+int eik_image_fill_u8(eik_ctx* c, const uint8_t* im, int64_t H, int64_t W, uint8_t* out) {
+    if (!c || !im || !out || H < 1 || W < 1) return c ? set_err(c, EIK_ERR_ARG, "bad image_filling arguments") : EIK_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t n = H * W;
+    HIPCHK(c, c->cm_u8.ensure(3 * n + 64));
+    HIPCHK(c, c->cm_f32.ensure(sizeof(float) * 2 * n));
+    unsigned char* m = (unsigned char*)c->cm_u8.p;
+    HIPCHK(c, hipMemcpyAsync(m, im, n, hipMemcpyHostToDevice, c->stream));
+    float* fcost = (float*)c->cm_f32.p;
+    int rc = cm_fill(c, m, H, W, fcost, fcost + n, c->stream);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(out, m, n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return EIK_OK;
 }

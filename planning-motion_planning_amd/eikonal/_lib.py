@@ -22,6 +22,13 @@ _f32p = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
 _f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
 _i64p = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
 _u32p = np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS")
+_u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
+
+
+class CostmapParams(C.Structure):
+    """eik_costmap_params (include/eikonal.h): the cost builder's constants."""
+    _fields_ = [("slope_max", C.c_double), ("diagonal", C.c_double), ("expansion", C.c_double),
+                ("gradient", C.c_double), ("high", C.c_double)]
 
 
 class EikStats(C.Structure):
@@ -103,6 +110,10 @@ def lib():
                                      P(C.c_int)]
         L.eik_fim3d_solve.argtypes = [vp, vp, vp, i64, i64, i64, C.c_int, _i64p, vp]
         L.eik_path3d_dev.argtypes = [vp, vp, C.c_int, i64, i64, i64, _f64p, _f64p, C.c_double, vp, i64, vp, vp, vp]
+        L.eik_costmap_f64.argtypes = [vp, _f64p, i64, i64, C.c_double, C.c_double, P(CostmapParams), _f64p, vp]
+        L.eik_costmap_dev.argtypes = [vp, vp, i64, i64, C.c_double, C.c_double, P(CostmapParams), vp, vp, vp]
+        L.eik_surface_normal_f64.argtypes = [vp, _f64p, i64, i64, C.c_double, _f64p, _f64p, _f64p]
+        L.eik_image_fill_u8.argtypes = [vp, _u8p, i64, i64, _u8p]
         _lib = L
         return L
 
@@ -113,7 +124,7 @@ EXPORTED = [
     "eik_gradient2d_f64", "eik_fim2d_create", "eik_fim2d_destroy", "eik_fim2d_set_ghosts", "eik_fim2d_start",
     "eik_fim2d_iterate", "eik_fim2d_solve", "eik_fim2d_pack_edges", "eik_fim2d_merge_ghost", "eik_fim2d_active",
     "eik_fim2d_stats", "eik_path2d_dev", "eik_tmap3d_f32", "eik_tmap3d_f64", "eik_path3d_f64", "eik_fim3d_solve",
-    "eik_path3d_dev",
+    "eik_path3d_dev", "eik_costmap_f64", "eik_costmap_dev", "eik_surface_normal_f64", "eik_image_fill_u8",
 ]
 
 
@@ -206,6 +217,31 @@ class Context:
                                        np.asarray(end, np.float64)[:3].copy(), float(tau), out, cap, C.byref(n),
                                        C.byref(st)))
         return out[: n.value].copy(), st.value
+
+    def costmap(self, Z, resolution, size, params=None):
+        """Coupled_motion_planner.py:1101-1216 on the GPU: (cost [y][x] = the reference's cMap.T,
+        obstacle map [y][x] uint8)."""
+        Z = np.ascontiguousarray(Z, dtype=np.float64)
+        H, W = Z.shape
+        cost = np.empty_like(Z)
+        obst = np.empty((H, W), np.uint8)
+        p = C.byref(params) if params is not None else None
+        self._chk(lib().eik_costmap_f64(self._h, Z, H, W, float(resolution), float(size), p, cost, obst.ctypes.data))
+        return cost, obst
+
+    def surface_normal(self, Z, size):
+        Z = np.ascontiguousarray(Z, dtype=np.float64)
+        H, W = Z.shape
+        nx, ny, nz = np.empty_like(Z), np.empty_like(Z), np.empty_like(Z)
+        self._chk(lib().eik_surface_normal_f64(self._h, Z, H, W, float(size), nx, ny, nz))
+        return nx, ny, nz
+
+    def image_fill(self, im):
+        im = np.ascontiguousarray(im, dtype=np.uint8)
+        H, W = im.shape
+        out = np.empty_like(im)
+        self._chk(lib().eik_image_fill_u8(self._h, im, H, W, out))
+        return out
 
     def gradient2d(self, T):
         T = np.ascontiguousarray(T, dtype=np.float64)
