@@ -187,6 +187,94 @@ __global__ void cm_edt_rows_kernel(const int* __restrict__ g, int64_t H, int64_t
     }
 }
 
+// pass 1, segmented (parallel over 64-row segments of every column): per segment the first and
+// last feature rows; per column a carry scan over the segments (nearest feature row above and
+// below each segment); per segment the two sweeps seeded with the carries.
+constexpr int kSeg = 64;
+
+template <typename F>
+__global__ void cm_seg_summary_kernel(F feat, int64_t H, int64_t W, int* __restrict__ first, int* __restrict__ last) {
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t sg = blockIdx.y;
+    if (x >= W) return;
+    const int64_t y0 = sg * kSeg, y1 = y0 + kSeg < H ? y0 + kSeg : H;
+    int f = -1, l = -1;
+    for (int64_t y = y0; y < y1; ++y)
+        if (feat(y * W + x)) {
+            if (f < 0) f = (int)y;
+            l = (int)y;
+        }
+    first[sg * W + x] = f;
+    last[sg * W + x] = l;
+}
+
+__global__ void cm_seg_carry_kernel(int64_t nseg, int64_t W, int* __restrict__ first, int* __restrict__ last) {
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= W) return;
+    // in place: last[s] <- last feature row before segment s; first[s] <- first feature row after it
+    int run = -1;
+    for (int64_t sg = 0; sg < nseg; ++sg) {
+        const int l = last[sg * W + x];
+        last[sg * W + x] = run;
+        if (l >= 0) run = l;
+    }
+    run = -1;
+    for (int64_t sg = nseg - 1; sg >= 0; --sg) {
+        const int f = first[sg * W + x];
+        first[sg * W + x] = run;
+        if (f >= 0) run = f;
+    }
+}
+
+template <typename F>
+__global__ void cm_seg_fill_kernel(F feat, int64_t H, int64_t W, const int* __restrict__ below,
+                                   const int* __restrict__ above, int* __restrict__ g) {
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t sg = blockIdx.y;
+    if (x >= W) return;
+    const int64_t y0 = sg * kSeg, y1 = y0 + kSeg < H ? y0 + kSeg : H;
+    int up = above[sg * W + x];
+    for (int64_t y = y0; y < y1; ++y) {
+        if (feat(y * W + x)) up = (int)y;
+        g[y * W + x] = up >= 0 ? (int)y - up : kFar;
+    }
+    int dn = below[sg * W + x];
+    for (int64_t y = y1 - 1; y >= y0; --y) {
+        if (feat(y * W + x)) dn = (int)y;
+        if (dn >= 0 && dn - (int)y < g[y * W + x]) g[y * W + x] = dn - (int)y;
+    }
+}
+
+// pass 2, one workgroup per row (rows <= kEdtRowMax wide): the row's column distances staged in
+// LDS; each pixel scans outward from its own column while k^2 < best -- the nearest feature's
+// column offset k satisfies k^2 <= D(x), so the scan is exact and costs about the distance to
+// the nearest feature (terrain rasters: tens of columns).
+constexpr int kEdtRowMax = 8192;
+
+__global__ __launch_bounds__(256) void cm_edt_rows_lds_kernel(const int* __restrict__ g, int64_t H, int64_t W,
+                                                              int* __restrict__ D) {
+    __shared__ int gs[kEdtRowMax];
+    const int64_t y = blockIdx.x;
+    const int w = (int)W;
+    for (int x = threadIdx.x; x < w; x += blockDim.x) gs[x] = g[y * W + x];
+    __syncthreads();
+    for (int x = threadIdx.x; x < w; x += blockDim.x) {
+        long long best = gs[x] >= kFar ? (long long)1 << 62 : (long long)gs[x] * gs[x];
+        for (int k = 1; (long long)k * k < best && (x - k >= 0 || x + k < w); ++k) {
+            const long long k2 = (long long)k * k;
+            if (x - k >= 0 && gs[x - k] < kFar) {
+                const long long v = k2 + (long long)gs[x - k] * gs[x - k];
+                best = v < best ? v : best;
+            }
+            if (x + k < w && gs[x + k] < kFar) {
+                const long long v = k2 + (long long)gs[x + k] * gs[x + k];
+                best = v < best ? v : best;
+            }
+        }
+        D[y * W + x] = best > INT32_MAX ? INT32_MAX : (int)best;
+    }
+}
+
 struct FeatEq {  // feat = (m[i] == val)
     const unsigned char* m;
     unsigned char val;
@@ -195,9 +283,22 @@ struct FeatEq {  // feat = (m[i] == val)
 
 hipError_t cm_edt(const unsigned char* m, unsigned char val, int64_t H, int64_t W, int* g, int* D, int* vbuf,
                   hipStream_t st) {
-    hipLaunchKernelGGL(cm_edt_cols_kernel<FeatEq>, dim3((unsigned)((W + 63) / 64)), dim3(64), 0, st, FeatEq{m, val}, H,
-                       W, g);
-    hipLaunchKernelGGL(cm_edt_rows_kernel, dim3((unsigned)((H + 63) / 64)), dim3(64), 0, st, g, H, W, D, vbuf);
+    const int64_t nseg = (H + kSeg - 1) / kSeg;
+    if (2 * nseg * W <= H * W) {  // segment summaries fit in the envelope scratch (vbuf, H * W ints)
+        int* first = vbuf;
+        int* last = vbuf + nseg * W;
+        const dim3 grid((unsigned)((W + 255) / 256), (unsigned)nseg);
+        hipLaunchKernelGGL(cm_seg_summary_kernel<FeatEq>, grid, dim3(256), 0, st, FeatEq{m, val}, H, W, first, last);
+        hipLaunchKernelGGL(cm_seg_carry_kernel, dim3((unsigned)((W + 255) / 256)), dim3(256), 0, st, nseg, W, first, last);
+        hipLaunchKernelGGL(cm_seg_fill_kernel<FeatEq>, grid, dim3(256), 0, st, FeatEq{m, val}, H, W, first, last, g);
+    } else {
+        hipLaunchKernelGGL(cm_edt_cols_kernel<FeatEq>, dim3((unsigned)((W + 63) / 64)), dim3(64), 0, st,
+                           FeatEq{m, val}, H, W, g);
+    }
+    if (W <= kEdtRowMax)
+        hipLaunchKernelGGL(cm_edt_rows_lds_kernel, dim3((unsigned)H), dim3(256), 0, st, g, H, W, D);
+    else
+        hipLaunchKernelGGL(cm_edt_rows_kernel, dim3((unsigned)((H + 63) / 64)), dim3(64), 0, st, g, H, W, D, vbuf);
     return hipGetLastError();
 }
 
