@@ -7,13 +7,15 @@
 //
 // All stages are HBM-bound elementwise / stencil / line passes.  Morphology with the
 // reference's disk structuring element (d <= r on integer offsets, structural_disk :96-105)
-// is computed EXACTLY through the squared Euclidean distance transform: dilate(A, disk r)(p) =
+// is computed EXACTLY from squared Euclidean distances: dilate(A, disk r)(p) =
 // [dist^2(p, A) <= r^2], erode(A, disk r)(p) = A(p) and [dist^2(p, not A) > r^2] (pixels outside
-// the image take no part, as cv2's default morphology border).  The EDT is the separable exact
-// one (column distances, then the lower envelope of parabolas per row), in int32 -- the same
-// squared distances scipy.ndimage.distance_transform_edt takes the sqrt of (:1194).  The flood
-// fill of image_filling (:82-94, cv2.floodFill 4-connected from (0, 0)) is reachability, i.e.
-// the block-FIM solver itself with cost 1 on the seed's value and +inf elsewhere (host side).
+// the image take no part, as cv2's default morphology border) -- by a radius-bounded separable
+// transform (only distances <= r matter).  The distance ramp needs the full exact EDT (its
+// maximum normalises the ramp, :1196): column distances by 64-row segments with a carry scan,
+// then per row an outward scan over LDS-staged column distances, in integers -- the squared
+// distances scipy.ndimage.distance_transform_edt takes the sqrt of (:1194).  The flood fill of
+// image_filling (:82-94, cv2.floodFill 4-connected from (0, 0)) is reachability, i.e. the
+// block-FIM solver itself with cost 1 on the seed's value and +inf elsewhere (host side).
 //
 // Floating point: IEEE f64 without contraction, the reference's operation order where it is
 // defined (stencils: two non-zero taps, exact halvings; normals; ramp); the box blur sums in a
