@@ -205,6 +205,14 @@ int eik_surface_normal_f64(eik_ctx* ctx, const double* Z, int64_t H, int64_t W, 
 /* image_filling(im) :82-94 (cv2.floodFill from (0, 0), 4-connected) on a 0/1 uint8 image */
 int eik_image_fill_u8(eik_ctx* ctx, const uint8_t* im, int64_t H, int64_t W, uint8_t* out);
 
+/* ---- DEM ingest, host only: no GPU, no context --------------------
+ * Coupled_motion_planner.py:1098-1099 reads PRL_DEM.txt as comma-separated rows with a Python
+ * float() per value.  eik_load_dem_txt parses the same text with host threads (nthreads <= 0:
+ * all cores), bit-identical values (correctly rounded parsing).  out == NULL: only H, W.
+ * Errors: EIK_ERR_ARG, message from eik_io_last_error(). */
+int eik_load_dem_txt(const char* path, double* out, int64_t cap, int64_t* H, int64_t* W, int nthreads);
+const char* eik_io_last_error(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -8,6 +8,7 @@ cannot be imported here (it needs OpenCV):
   structural_disk(r)                    :96-105  -> uint8 disk (host, as the reference)
   cost_map(Zs, resolution, size)        :1101-1216 -> (cMap, obstMap) exactly as main() holds
                                                     them before FM.biComputeTmap(cMap.T, ...)
+  load_dem(mapDirectory)                :1098-1099 -> Zs, the DEM text parsed by host threads
 All GPU work goes through libeikonal.so (include/eikonal.h: eik_costmap_*); no CPU fallback.
 """
 import math
@@ -15,6 +16,12 @@ import math
 import numpy as np
 
 from eikonal import _lib as L
+
+
+def load_dem(mapDirectory):
+    """Coupled_motion_planner.py:1098-1099: Zs from <mapDirectory>PRL_DEM.txt (comma-separated
+    rows), parsed by libeikonal's host threads; values identical to float() per entry."""
+    return L.load_dem_txt(str(mapDirectory) + "PRL_DEM.txt")
 
 
 def _ctx():

@@ -114,6 +114,8 @@ def lib():
         L.eik_costmap_dev.argtypes = [vp, vp, i64, i64, C.c_double, C.c_double, P(CostmapParams), vp, vp, vp]
         L.eik_surface_normal_f64.argtypes = [vp, _f64p, i64, i64, C.c_double, _f64p, _f64p, _f64p]
         L.eik_image_fill_u8.argtypes = [vp, _u8p, i64, i64, _u8p]
+        L.eik_load_dem_txt.argtypes = [C.c_char_p, vp, i64, P(i64), P(i64), C.c_int]
+        L.eik_io_last_error.restype = C.c_char_p
         _lib = L
         return L
 
@@ -125,7 +127,22 @@ EXPORTED = [
     "eik_fim2d_iterate", "eik_fim2d_solve", "eik_fim2d_pack_edges", "eik_fim2d_merge_ghost", "eik_fim2d_active",
     "eik_fim2d_stats", "eik_path2d_dev", "eik_tmap3d_f32", "eik_tmap3d_f64", "eik_path3d_f64", "eik_fim3d_solve",
     "eik_path3d_dev", "eik_costmap_f64", "eik_costmap_dev", "eik_surface_normal_f64", "eik_image_fill_u8",
+    "eik_load_dem_txt", "eik_io_last_error",
 ]
+
+
+def load_dem_txt(path, nthreads=0):
+    """Coupled_motion_planner.py:1098-1099 (comma-separated DEM text) -> float64 (H, W), parsed
+    by host threads in libeikonal (no GPU)."""
+    L = lib()
+    H, W = i64(0), i64(0)
+    p = os.fsencode(path)
+    if L.eik_load_dem_txt(p, None, 0, C.byref(H), C.byref(W), int(nthreads)) != EIK_OK:
+        raise ValueError(L.eik_io_last_error().decode())
+    out = np.empty((H.value, W.value), np.float64)
+    if L.eik_load_dem_txt(p, out.ctypes.data, out.size, C.byref(H), C.byref(W), int(nthreads)) != EIK_OK:
+        raise ValueError(L.eik_io_last_error().decode())
+    return out
 
 
 class Context:
