@@ -49,7 +49,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--block", type=int, default=4096, help="per-rank block side (cells)")
-    ap.add_argument("--exchange-every", type=int, default=8)
+    ap.add_argument("--exchange-every", type=int, default=8, help="--dd rounds: outer iterations per exchange")
+    ap.add_argument("--dd", choices=["live", "rounds"], default="live",
+                    help="N > 1: live persistent launches + IPC halo rounds, or relaunch-per-round over RCCL")
     ap.add_argument("--sync-every", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-path", action="store_true")
@@ -62,10 +64,18 @@ def main():
     world = env_int("WORLD_SIZE", 1)
     rank = env_int("RANK", 0)
     local_rank = env_int("LOCAL_RANK", 0)
+    # rehearsal knob (one-GPU box): every rank on cuda:0, gloo world group, the launches' grids
+    # split so they are co-resident.  Timing under it is not a scaling measurement.
+    shared = os.environ.get("EIK_BENCH_SHARED_GPU") == "1"
+    if shared:
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     px, py = dd.SPLITS[world]
     H, W = args.block * py, args.block * px
     blk = dd.Block(H, W, px, py, rank)
@@ -76,20 +86,54 @@ def main():
     stream = torch.cuda.current_stream(dev)
     ctx = eikonal.Context(local_rank)
     ctx.set_option(L.OPT_SYNC_EVERY, args.sync_every)
+    if shared and world > 1:
+        ctx.set_option(L.OPT_GRID, max(2, 2 * torch.cuda.get_device_properties(dev).multi_processor_count // world))
     fim = eikonal.Fim2d(ctx, 1, blk.h, blk.w, L.EIK_F32)
     lgoal = blk.local_goal(*goal_g)
 
+    dd_mode = args.dd if world > 1 else None
     if world > 1:
         send, recv, ghost = dd.make_strips(blk, torch.float32, dev, float("inf"))
+        ctrl = dd.control_group()
+        halo, live_err, vote = None, None, None
+        if dd_mode == "live":  # every rank must agree, or all fall back to rounds
+            try:
+                halo = dd.IpcHalo(ctx, blk, 4, group=ctrl)
+            except Exception as e:
+                live_err = repr(e)
+            if env_int("LOCAL_WORLD_SIZE", world) == world and not live_err:
+                try:  # one node: the per-round vote through shared memory, not gloo/TCP
+                    vote = dd.NodeVote(group=ctrl)
+                except Exception as e:
+                    live_err = repr(e)
+            ok = torch.tensor([0 if live_err else 1], dtype=torch.int64)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=ctrl)
+            if ok.item() == 0:
+                dd_mode = "rounds"
+        live_local = dd.LiveGpuLocal(fim, ghost)
         local = dd.GpuLocal(fim, ghost)
 
+        dd_rounds = []
+
         def step():
-            local.start(cost, T, lgoal, stream.cuda_stream)
-            dd.solve(local, blk, send, recv, exchange_every=args.exchange_every)
+            if dd_mode == "live":
+                live_local.start(cost, T, lgoal, stream.cuda_stream)
+                dd_rounds.append(dd.solve_live(live_local, blk, halo, group=ctrl, vote=vote))
+            else:
+                local.start(cost, T, lgoal, stream.cuda_stream)
+                dd_rounds.append(dd.solve(local, blk, send, recv, exchange_every=args.exchange_every))
     else:
         def step():
             fim.solve(cost.data_ptr(), T.data_ptr(), [lgoal], stream.cuda_stream)
 
+    if dd_mode == "live":
+        ctx.set_option(L.OPT_QTIMEOUT, 5.0)  # a stuck live round ends in an error, not a hang
+        try:
+            step()
+        except Exception as e:  # raised on every rank alike (dd.solve_live's error carry)
+            live_err = repr(e)
+            dd_mode = "rounds"
+            ctx.set_option(L.OPT_QTIMEOUT, 30.0)
     for _ in range(args.warmup):
         step()
 
@@ -116,8 +160,8 @@ def main():
         el = time.perf_counter() - t0
         ctx.set_option(L.OPT_TIMING, 0)
         if world > 1:
-            tt = torch.tensor([el], device=dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            tt = torch.tensor([el], dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=ctrl)
             el = tt.item()
         return el, visits, passes, sweep_ms, iters
 
@@ -173,12 +217,20 @@ def main():
         "data": "synthetic (fractal DEM seed 42 -> planner cost recipe, eikonal/terrain.py)",
         "config": {
             "workload": ("C2: 4096x4096 DEM-derived cost raster, single goal, FIM on 1 MI355X" if world == 1 else
-                         f"C4-weak: {H}x{W} DEM-derived raster, {px}x{py} blocks of {args.block}^2 with RCCL halo"),
+                         f"C4-weak: {H}x{W} DEM-derived raster, {px}x{py} blocks of {args.block}^2, halo: "
+                         + ("live persistent launches + IPC peer stores" if dd_mode == "live" else "RCCL rounds")),
             "H": H, "W": W, "split": f"{px}x{py}", "goal": list(goal_g), "tile": 64,
             "parallelism": "single-gpu" if world == 1 else f"domain-decomposition {px}x{py}",
         },
         "roofline": roof,
     }
+    if world > 1:
+        out["config"]["dd_mode"] = dd_mode + (" (shm vote)" if dd_mode == "live" and vote is not None else "")
+        rr = dd_rounds[-args.steps:]
+        out["config"]["dd_rounds_per_solve"] = round(sum(rr) / max(len(rr), 1), 1)
+        out["config"]["dd_us_per_round"] = round(ms_per_step * 1e3 / max(sum(rr) / max(len(rr), 1), 1), 1)
+        if live_err:
+            out["config"]["dd_live_error"] = live_err[:200]
 
     if rank == 0 and world == 1 and not args.no_path:
         out.update(ms_to_path(cost, ctx, fim, dev, stream, goal_g))

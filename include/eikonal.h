@@ -163,6 +163,40 @@ int eik_fim2d_active(eik_fim2d* fim, int64_t* active);
 /* statistics of the current/last solve (synchronises the stream to read the visit counter) */
 int eik_fim2d_stats(eik_fim2d* fim, eik_stats* out);
 
+/* Live domain decomposition (no reference counterpart: the multi-GPU split of SURVEY.md §8(e)).
+ * eik_fim2d_launch(fim, 1) starts ONE persistent launch on the bound stream and returns at once.
+ * Its last workgroup is a halo agent serving a pinned host mailbox while the others solve; the
+ * launch keeps serving its tile FIFO -- idle included -- until eik_fim2d_release.  Per round:
+ *   live_pack(p)   the agent snapshots "tiles pending or busy", then stores the four edges of T
+ *                  into send[p][side] (the neighbours' receive strips, e.g. eik_ipc_open'ed)
+ *   (host barrier: every rank has packed)
+ *   live_merge(p)  the agent min-merges recv[p][side] into the ghosts and queues the edge tiles
+ *                  whose ghost dropped; *active = the pack's snapshot, *changed = ghosts lowered
+ * The raster is converged when, in one round, every rank reports active == 0 and changed == 0.
+ * eik_fim2d_live_bind sets the strips (index parity * 4 + side, NULL = no neighbour) before the
+ * launch.  live = 0 is one ordinary persistent launch without the trailing synchronisation. */
+int eik_fim2d_live_bind(eik_fim2d* fim, void* const send[8], void* const recv[8]);
+int eik_fim2d_launch(eik_fim2d* fim, int live);
+int eik_fim2d_live_pack(eik_fim2d* fim, int parity);
+int eik_fim2d_live_merge(eik_fim2d* fim, int parity, int64_t* active, int64_t* changed);
+/* end the live launch: wait for it on the bound stream; *active = tiles left (0 when converged) */
+int eik_fim2d_release(eik_fim2d* fim, int64_t* active);
+
+/* Sum of one integer over the `world` ranks of one node, through a shared-memory segment of
+ * 64 * world bytes (zeroed before first use); round = 1, 2, ... on every rank in step.  Returns
+ * EIK_ERR_HIP after timeout_s without the others.  (Per-round vote of the live decomposition.) */
+int eik_node_allreduce(void* shm, int rank, int world, uint64_t round, int64_t value, int64_t* sum, double timeout_s);
+/* the segment: POSIX shm `name` of `bytes` (create != 0: new and zeroed), mapped at *addr */
+int eik_node_shm_open(const char* name, int64_t bytes, int create, void** addr);
+int eik_node_shm_close(void* addr, int64_t bytes);
+int eik_node_shm_unlink(const char* name);
+
+/* Device buffers shared between the processes of one node (hipIpc handles, 64 bytes). */
+int eik_ipc_alloc(eik_ctx* ctx, int64_t bytes, void** d_ptr, unsigned char handle[64]);
+int eik_ipc_free(eik_ctx* ctx, void* d_ptr);
+int eik_ipc_open(eik_ctx* ctx, const unsigned char handle[64], void** d_ptr);
+int eik_ipc_close(eik_ctx* ctx, void* d_ptr);
+
 /* getPathGDM on a device-resident field; out/n_out/status are device pointers. */
 int eik_path2d_dev(eik_ctx* ctx, const void* d_T, int dtype, int64_t H, int64_t W, const double init[2],
                    const double end[2], double tau, double* d_out, int64_t cap, int64_t* d_n_out, int* d_status,

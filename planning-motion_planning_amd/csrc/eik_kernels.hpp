@@ -38,6 +38,26 @@ struct Fim2dArgs {
     // layered solver (fim2dl.hip): cell (y, x) holds ls consecutive values, layers z0.. solved
     int64_t ls;            // layer stride (1 for the 2D solver)
     int z0;                // first solved layer
+    // live domain decomposition (eik_fim2d_launch with live != 0): the persistent launch stays up
+    // -- its last workgroup is the halo agent serving the host's commands -- and ends when
+    // *qhold != 0
+    unsigned* qhold;       // nullptr: end when no tile is pending or busy
+    struct LiveBox* live;  // pinned host mailbox of the halo agent (live launches only)
+};
+
+// Host <-> halo-agent mailbox (pinned, coherent host memory).  The host writes cmd, then seq
+// (release); the agent runs the command and writes its results, then done = seq (release).
+constexpr unsigned kLivePack = 1, kLiveMerge = 2, kLiveRelease = 3;
+struct LiveBox {
+    unsigned seq;        // host: sequence number of the posted command
+    unsigned cmd;        // host: op | parity << 8
+    unsigned done;       // agent: seq of the last completed command
+    unsigned active;     // agent: tiles pending or busy at the last pack (snapshot BEFORE reading T)
+    unsigned changed;    // agent: ghost cells the last merge lowered
+    unsigned error;      // agent: queue error bits
+    unsigned pad[2];
+    void* send[2][4];    // host: edge targets by parity and side (a neighbour's receive strips)
+    const void* recv[2][4];  // host: this block's receive strips by parity and side
 };
 constexpr int kModeList = 0, kModePersistent = 1;
 constexpr size_t kQueueCtlBytes = 256;

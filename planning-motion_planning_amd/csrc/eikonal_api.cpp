@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -91,6 +92,10 @@ struct eik_fim2d {
     double sweep_ms = 0.0, solve_ms = 0.0;
     bool started = false;
     int persist_grid = 0;                // co-resident workgroups of the persistent kernel
+    // live domain decomposition: hold word on the device, mailbox of the halo agent on the host
+    DevBuf hold;
+    LiveBox* box = nullptr;              // pinned, coherent
+    bool live_on = false;
 };
 
 static int set_err(eik_ctx* c, int code, const char* fmt, ...) {
@@ -257,6 +262,7 @@ void eik_fim2d_destroy(eik_fim2d* f) {
     if (f->h_q) (void)hipHostFree(f->h_q);
     if (f->ev_start) (void)hipEventDestroy(f->ev_start);
     if (f->ev_stop) (void)hipEventDestroy(f->ev_stop);
+    if (f->box) (void)hipHostFree(f->box);
     for (auto ev : f->ev_pool) (void)hipEventDestroy(ev);
     delete f;
 }
@@ -431,6 +437,173 @@ int eik_fim2d_merge_ghost(eik_fim2d* f, int side, const void* recv) {
     if (!f || !f->started || side < 0 || side > 3 || !recv || !f->a.ghost[side]) return EIK_ERR_ARG;
     f->a.iter = (unsigned)f->iterations;  // enqueue for the next sweep launch
     HIPCHK(f->ctx, fim2d_merge_ghost(f->a, f->f64, side, recv, side < 2 ? f->W : f->H, f->stream));
+    return EIK_OK;
+}
+
+// ------------------------------------------------------------- live domain decomposition
+static int live_box(eik_fim2d* f) {
+    if (f->box) return EIK_OK;
+    const hipError_t e = hipHostMalloc((void**)&f->box, sizeof(LiveBox), hipHostMallocCoherent);
+    if (e != hipSuccess) {
+        f->box = nullptr;
+        return set_err(f->ctx, EIK_ERR_NOMEM, "live mailbox: %s", hipGetErrorString(e));
+    }
+    memset(f->box, 0, sizeof(LiveBox));
+    return EIK_OK;
+}
+
+int eik_fim2d_live_bind(eik_fim2d* f, void* const send[8], void* const recv[8]) {
+    if (!f || !send || !recv) return EIK_ERR_ARG;
+    if (f->live_on) return set_err(f->ctx, EIK_ERR_ARG, "cannot rebind strips during a live launch");
+    int rc = live_box(f);
+    if (rc) return rc;
+    for (int p = 0; p < 2; ++p)
+        for (int s = 0; s < 4; ++s) {
+            f->box->send[p][s] = send[p * 4 + s];
+            f->box->recv[p][s] = recv[p * 4 + s];
+        }
+    return EIK_OK;
+}
+
+// post one command to the halo agent and wait for it (bounded by the queue timeout)
+static int live_cmd(eik_fim2d* f, unsigned op, unsigned par) {
+    eik_ctx* c = f->ctx;
+    LiveBox* b = f->box;
+    const unsigned seq = __atomic_load_n(&b->seq, __ATOMIC_RELAXED) + 1u;
+    __atomic_store_n(&b->cmd, op | (par & 1u) << 8, __ATOMIC_RELAXED);
+    __atomic_store_n(&b->seq, seq, __ATOMIC_RELEASE);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spin = 0; __atomic_load_n(&b->done, __ATOMIC_ACQUIRE) != seq; ++spin) {
+        if ((spin & 1023u) == 1023u) {
+            const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            if (el > c->qtimeout_s + 1.0)
+                return set_err(c, EIK_ERR_HIP, "live solve: the halo agent did not answer within %.1f s", el);
+            if (__atomic_load_n(&b->error, __ATOMIC_RELAXED) & 1u) break;
+            // the launch ended early (fault, or every workgroup left): nothing will answer
+            if (hipStreamQuery(f->stream) == hipSuccess)
+                return set_err(c, EIK_ERR_HIP, "live solve: the persistent launch is no longer running");
+        }
+        __builtin_ia32_pause();
+    }
+    const unsigned err = __atomic_load_n(&b->error, __ATOMIC_RELAXED);
+    if (err & 1u)
+        return set_err(c, EIK_ERR_HIP, "live solve: a queue wait exceeded %.1f s (EIK_OPT_QTIMEOUT)", c->qtimeout_s);
+    if (err & 2u)
+        return set_err(c, EIK_ERR_NOCONVERGE, "no convergence within %llu tile visits (negative costs?)",
+                       (unsigned long long)f->a.qbudget);
+    return EIK_OK;
+}
+
+int eik_fim2d_launch(eik_fim2d* f, int live) {
+    if (!f || !f->started) return EIK_ERR_ARG;
+    eik_ctx* c = f->ctx;
+    if (f->live_on) return set_err(c, EIK_ERR_ARG, "a live launch is still running (eik_fim2d_release)");
+    if (f->a.mode != kModePersistent)
+        return set_err(c, EIK_ERR_ARG, "eik_fim2d_launch needs the persistent mode (EIK_OPT_MODE)");
+    HIPCHK(c, hipSetDevice(c->device));
+    const int grid = c->grid > 0 ? c->grid : 4 * c->cu_count;
+    if (f->persist_grid == 0) f->persist_grid = fim2d_persist_resident(f->f64, c->cu_count);
+    Fim2dArgs a = f->a;
+    if (live) {
+        int rc = live_box(f);
+        if (rc) return rc;
+        hipError_t e = f->hold.ensure(64);
+        if (e != hipSuccess) return set_err(c, EIK_ERR_NOMEM, "live hold word: %s", hipGetErrorString(e));
+        HIPCHK(c, hipMemsetAsync(f->hold.p, 0, 64, f->stream));
+        f->box->seq = f->box->done = 0;
+        f->box->error = 0;
+        a.qhold = (unsigned*)f->hold.p;
+        a.live = f->box;
+    }
+    if (c->timing) {
+        while (f->ev_pool.size() < f->ev_used + 2) {
+            hipEvent_t ev;
+            HIPCHK(c, hipEventCreate(&ev));
+            f->ev_pool.push_back(ev);
+        }
+        HIPCHK(c, hipEventRecord(f->ev_pool[f->ev_used++], f->stream));
+    }
+    // live: the last workgroup is the halo agent; all must be co-resident (grid <= resident)
+    const int g = std::max(live ? 2 : 1, std::min(grid, f->persist_grid));
+    HIPCHK(c, fim2d_persist(a, f->f64, g, f->stream));
+    if (c->timing) HIPCHK(c, hipEventRecord(f->ev_pool[f->ev_used++], f->stream));
+    f->live_on = live != 0;
+    ++f->iterations;
+    return EIK_OK;
+}
+
+int eik_fim2d_live_pack(eik_fim2d* f, int par) {
+    if (!f || !f->live_on) return EIK_ERR_ARG;
+    return live_cmd(f, kLivePack, (unsigned)par);
+}
+
+int eik_fim2d_live_merge(eik_fim2d* f, int par, int64_t* active, int64_t* changed) {
+    if (!f || !f->live_on) return EIK_ERR_ARG;
+    int rc = live_cmd(f, kLiveMerge, (unsigned)par);
+    if (rc) return rc;
+    ++f->host_syncs;
+    if (active) *active = __atomic_load_n(&f->box->active, __ATOMIC_RELAXED);
+    if (changed) *changed = __atomic_load_n(&f->box->changed, __ATOMIC_RELAXED);
+    return EIK_OK;
+}
+
+int eik_fim2d_release(eik_fim2d* f, int64_t* active) {
+    if (!f || !f->live_on) return EIK_ERR_ARG;
+    eik_ctx* c = f->ctx;
+    f->live_on = false;
+    const int rc_cmd = live_cmd(f, kLiveRelease, 0);
+    HIPCHK(c, hipMemcpyAsync(f->h_q, f->qctl.p, kQueueCtlBytes, hipMemcpyDeviceToHost, f->stream));
+    HIPCHK(c, hipStreamSynchronize(f->stream));
+    ++f->host_syncs;
+    if (c->timing) drain_timing(f);
+    if (rc_cmd) return rc_cmd;
+    const unsigned err = f->h_q[192 / 4];
+    if (err & 1u)
+        return set_err(c, EIK_ERR_HIP, "live solve: a queue wait exceeded %.1f s (EIK_OPT_QTIMEOUT)", c->qtimeout_s);
+    if (err & 2u)
+        return set_err(c, EIK_ERR_NOCONVERGE, "no convergence within %llu tile visits (negative costs?)",
+                       (unsigned long long)f->a.qbudget);
+    if (active) *active = f->h_q[128 / 4];
+    return EIK_OK;
+}
+
+// ---------------------------------------------------------------- inter-process buffers
+int eik_ipc_alloc(eik_ctx* c, int64_t bytes, void** d_ptr, unsigned char handle[64]) {
+    if (!c || !d_ptr || !handle || bytes <= 0) return EIK_ERR_ARG;
+    static_assert(sizeof(hipIpcMemHandle_t) <= 64, "IPC handle size");
+    HIPCHK(c, hipSetDevice(c->device));
+    void* p = nullptr;
+    HIPCHK(c, hipMalloc(&p, (size_t)bytes));
+    hipIpcMemHandle_t h;
+    const hipError_t e = hipIpcGetMemHandle(&h, p);
+    if (e != hipSuccess) {
+        (void)hipFree(p);
+        return set_err(c, EIK_ERR_HIP, "hipIpcGetMemHandle: %s", hipGetErrorString(e));
+    }
+    memset(handle, 0, 64);
+    memcpy(handle, &h, sizeof h);
+    *d_ptr = p;
+    return EIK_OK;
+}
+
+int eik_ipc_free(eik_ctx* c, void* d_ptr) {
+    if (!c) return EIK_ERR_ARG;
+    if (d_ptr) HIPCHK(c, hipFree(d_ptr));
+    return EIK_OK;
+}
+
+int eik_ipc_open(eik_ctx* c, const unsigned char handle[64], void** d_ptr) {
+    if (!c || !handle || !d_ptr) return EIK_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    hipIpcMemHandle_t h;
+    memcpy(&h, handle, sizeof h);
+    HIPCHK(c, hipIpcOpenMemHandle(d_ptr, h, hipIpcMemLazyEnablePeerAccess));
+    return EIK_OK;
+}
+
+int eik_ipc_close(eik_ctx* c, void* d_ptr) {
+    if (!c) return EIK_ERR_ARG;
+    if (d_ptr) HIPCHK(c, hipIpcCloseMemHandle(d_ptr));
     return EIK_OK;
 }
 

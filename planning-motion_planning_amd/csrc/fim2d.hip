@@ -374,9 +374,103 @@ __global__ __launch_bounds__(kThreads) void fim2d_sweep_kernel(Fim2dArgs a) {
     }
 }
 
+// Live DD halo agent: the last workgroup of a live launch.  It serves the host's mailbox while
+// the other workgroups solve: PACK (snapshot the queue's activity, then store the four edges of T
+// into the neighbours' receive strips -- peer memory over xGMI), MERGE (min-merge the received
+// strips into the ghosts, queue the edge tiles whose ghost dropped) and RELEASE (end the launch).
+// One command in flight; every wait is bounded by qtimeout.
+template <typename R>
+__device__ void live_agent(const Fim2dArgs& a, unsigned* sh) {
+    LiveBox* box = a.live;
+    const int tid = threadIdx.x;
+    unsigned last = 0;
+    for (;;) {
+        if (tid == 0) {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            unsigned s;
+            for (;;) {
+                s = __hip_atomic_load(&box->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (s != last) break;
+                if (__hip_atomic_load(a.qerror, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
+                    __builtin_amdgcn_s_memrealtime() - t0 > a.qtimeout) {
+                    atomicOr(a.qerror, 1u);
+                    s = ~0u;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(4);
+            }
+            sh[0] = s;
+            sh[1] = s == ~0u ? 0u : __hip_atomic_load(&box->cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            sh[2] = (unsigned)__hip_atomic_load(a.qactive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sh[3] = 0u;
+        }
+        __syncthreads();
+        const unsigned s = sh[0], op = sh[1] & 0xffu, par = (sh[1] >> 8) & 1u;
+        if (s == ~0u) {  // timed out: make the solvers leave too
+            if (tid == 0) __hip_atomic_store(a.qhold, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        last = s;
+        if (op == kLivePack) {  // the snapshot (sh[2]) was taken before any T load below
+            const R* T = static_cast<const R*>(a.T);
+            R* tg[4];
+            for (int k = 0; k < 4; ++k) tg[k] = static_cast<R*>(box->send[par][k]);
+            for (int64_t i = tid; i < a.W; i += blockDim.x) {
+                if (tg[0]) st_scoped(tg[0] + i, ld_agent(T + i), __HIP_MEMORY_SCOPE_SYSTEM);
+                if (tg[1]) st_scoped(tg[1] + i, ld_agent(T + (a.H - 1) * a.W + i), __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            for (int64_t i = tid; i < a.H; i += blockDim.x) {
+                if (tg[2]) st_scoped(tg[2] + i, ld_agent(T + i * a.W), __HIP_MEMORY_SCOPE_SYSTEM);
+                if (tg[3]) st_scoped(tg[3] + i, ld_agent(T + i * a.W + a.W - 1), __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: peer stores complete
+        } else if (op == kLiveMerge) {
+            for (int side = 0; side < 4; ++side) {
+                const R* rv = static_cast<const R*>(box->recv[par][side]);
+                R* g = static_cast<R*>(const_cast<void*>(a.ghost[side]));
+                if (!rv || !g) continue;
+                const int64_t len = side < 2 ? a.W : a.H;
+                for (int64_t i = tid; i < len; i += blockDim.x) {
+                    const R v = ld_system(rv + i);
+                    if (v < ld_agent(g + i)) {
+                        st_scoped(g + i, v, __HIP_MEMORY_SCOPE_AGENT);
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                        atomicAdd(&sh[3], 1u);
+                        int ty, tx;
+                        if (side < 2) {
+                            tx = (int)(i / kTile);
+                            ty = side == 0 ? 0 : a.nty - 1;
+                        } else {
+                            ty = (int)(i / kTile);
+                            tx = side == 2 ? 0 : a.ntx - 1;
+                        }
+                        qpush(a, ty * a.ntx + tx, kFromN << side);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            if (op == kLivePack) __hip_atomic_store(&box->active, sh[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (op == kLiveMerge) __hip_atomic_store(&box->changed, sh[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (op == kLiveRelease) __hip_atomic_store(a.qhold, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&box->error, __hip_atomic_load(a.qerror, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&box->done, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        if (op == kLiveRelease) return;
+        __syncthreads();  // sh[] is rewritten by the next command
+    }
+}
+
 template <typename R>
 __global__ __launch_bounds__(kThreads) void fim2d_persist_kernel(Fim2dArgs a) {
     __shared__ TileLds<R> L;
+    if (a.live && blockIdx.x == gridDim.x - 1) {
+        __shared__ unsigned sh[4];
+        live_agent<R>(a, sh);
+        return;
+    }
     init_guard_rows(L);
     const R keep = (R)a.keep;
     int tile = -1;
@@ -460,14 +554,17 @@ __global__ void fim2d_qrewind_kernel(Fim2dArgs a) { *a.qhead = *a.qtail; }
 
 // Domain decomposition: ghost = min(ghost, recv) and activate every edge tile next to a ghost
 // cell that decreased (for list iteration `iter`, or into the FIFO).  side: 0 N 1 S 2 W 3 E.
+// The strip may have been written by a peer GPU (system-scope loads); during a live launch the
+// ghost store is made visible (agent scope, released) before the tile is queued.
 template <typename R>
 __global__ void fim2d_merge_ghost_kernel(Fim2dArgs a, int side, const R* __restrict__ recv, int64_t len) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= len) return;
     R* g = static_cast<R*>(const_cast<void*>(a.ghost[side]));
-    const R v = recv[i];
+    const R v = ld_system(recv + i);
     if (v < g[i]) {
-        g[i] = v;
+        st_scoped(g + i, v, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         int ty, tx;
         if (side < 2) {
             tx = (int)(i / kTile);
@@ -480,19 +577,20 @@ __global__ void fim2d_merge_ghost_kernel(Fim2dArgs a, int side, const R* __restr
     }
 }
 
-// Copy this subdomain's edge rows/columns of T into contiguous send strips.
+// Copy this subdomain's edge rows/columns of T into contiguous send strips -- local buffers or a
+// peer GPU's receive strips (system-scope stores).  T may be in flight (live launch): agent loads.
 template <typename R>
 __global__ void fim2d_pack_edges_kernel(Fim2dArgs a, R* __restrict__ n, R* __restrict__ s, R* __restrict__ w,
                                         R* __restrict__ e) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const R* T = static_cast<const R*>(a.T);
     if (i < a.W) {
-        if (n) n[i] = T[i];
-        if (s) s[i] = T[(a.H - 1) * a.W + i];
+        if (n) st_scoped(n + i, ld_agent(T + i), __HIP_MEMORY_SCOPE_SYSTEM);
+        if (s) st_scoped(s + i, ld_agent(T + (a.H - 1) * a.W + i), __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if (i < a.H) {
-        if (w) w[i] = T[i * a.W];
-        if (e) e[i] = T[i * a.W + a.W - 1];
+        if (w) st_scoped(w + i, ld_agent(T + i * a.W), __HIP_MEMORY_SCOPE_SYSTEM);
+        if (e) st_scoped(e + i, ld_agent(T + i * a.W + a.W - 1), __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 

@@ -124,15 +124,58 @@ struct TMem<R, true> {
     }
 };
 
+// Scoped loads / stores of one value (float or double) through its bit pattern.
+template <typename R>
+__device__ __forceinline__ R ld_agent(const R* p) {
+    if constexpr (sizeof(R) == 4) {
+        return __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT));
+    } else {
+        return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
+                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+}
+template <typename R>
+__device__ __forceinline__ R ld_system(const R* p) {
+    if constexpr (sizeof(R) == 4) {
+        return __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_SYSTEM));
+    } else {
+        return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
+                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    }
+}
+template <typename R>
+__device__ __forceinline__ void st_scoped(R* p, R v, int scope) {
+    if constexpr (sizeof(R) == 4) {
+        if (scope == __HIP_MEMORY_SCOPE_SYSTEM)
+            __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        else
+            __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+        if (scope == __HIP_MEMORY_SCOPE_SYSTEM)
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        else
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 template <typename R, bool COH>
 __device__ __forceinline__ R load_T(const Fim2dArgs& a, const TMem<R, COH>& T, int64_t gy, int64_t gx) {
     constexpr R INF = Real<R>::inf();
     if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) return T.ld(gy * a.W + gx);
-    // ghost strips only change between launches (merge kernel): plain loads
-    if (gy == -1 && gx >= 0 && gx < a.W) return a.ghost[0] ? static_cast<const R*>(a.ghost[0])[gx] : INF;
-    if (gy == a.H && gx >= 0 && gx < a.W) return a.ghost[1] ? static_cast<const R*>(a.ghost[1])[gx] : INF;
-    if (gx == -1 && gy >= 0 && gy < a.H) return a.ghost[2] ? static_cast<const R*>(a.ghost[2])[gy] : INF;
-    if (gx == a.W && gy >= 0 && gy < a.H) return a.ghost[3] ? static_cast<const R*>(a.ghost[3])[gy] : INF;
+    // ghost strips: the merge kernel lowers them between list launches, or DURING a live
+    // persistent launch -- there they are read like T (agent-scope loads, L1 bypassed)
+    auto g = [&](int side, int64_t i) -> R {
+        const R* p = static_cast<const R*>(a.ghost[side]);
+        if (!p) return INF;
+        return COH ? ld_agent(p + i) : p[i];
+    };
+    if (gy == -1 && gx >= 0 && gx < a.W) return g(0, gx);
+    if (gy == a.H && gx >= 0 && gx < a.W) return g(1, gx);
+    if (gx == -1 && gy >= 0 && gy < a.H) return g(2, gy);
+    if (gx == a.W && gy >= 0 && gy < a.H) return g(3, gy);
     return INF;
 }
 
@@ -219,7 +262,10 @@ __device__ __forceinline__ int qgrab(const Fim2dArgs& a, unsigned& trig) {
             return tile;
         }
         if ((spin & 7u) == 7u) {
-            if (__hip_atomic_load(a.qactive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return -1;
+            // live DD: idle is not the end -- a halo merge may queue tiles until the host releases
+            if (a.qhold ? __hip_atomic_load(a.qhold, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u
+                        : __hip_atomic_load(a.qactive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+                return -1;
             if (__hip_atomic_load(a.qerror, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return -1;
             if (__builtin_amdgcn_s_memrealtime() - t0 > a.qtimeout) {  // never hang
                 atomicOr(a.qerror, 1u);

@@ -116,6 +116,19 @@ def lib():
         L.eik_image_fill_u8.argtypes = [vp, _u8p, i64, i64, _u8p]
         L.eik_load_dem_txt.argtypes = [C.c_char_p, vp, i64, P(i64), P(i64), C.c_int]
         L.eik_io_last_error.restype = C.c_char_p
+        L.eik_fim2d_live_bind.argtypes = [vp, vp * 8, vp * 8]
+        L.eik_fim2d_launch.argtypes = [vp, C.c_int]
+        L.eik_fim2d_live_pack.argtypes = [vp, C.c_int]
+        L.eik_fim2d_live_merge.argtypes = [vp, C.c_int, P(i64), P(i64)]
+        L.eik_fim2d_release.argtypes = [vp, P(i64)]
+        L.eik_node_allreduce.argtypes = [vp, C.c_int, C.c_int, C.c_uint64, i64, P(i64), C.c_double]
+        L.eik_node_shm_open.argtypes = [C.c_char_p, i64, C.c_int, P(vp)]
+        L.eik_node_shm_close.argtypes = [vp, i64]
+        L.eik_node_shm_unlink.argtypes = [C.c_char_p]
+        L.eik_ipc_alloc.argtypes = [vp, i64, P(vp), C.c_char_p]
+        L.eik_ipc_free.argtypes = [vp, vp]
+        L.eik_ipc_open.argtypes = [vp, C.c_char_p, P(vp)]
+        L.eik_ipc_close.argtypes = [vp, vp]
         _lib = L
         return L
 
@@ -127,7 +140,9 @@ EXPORTED = [
     "eik_fim2d_iterate", "eik_fim2d_solve", "eik_fim2d_pack_edges", "eik_fim2d_merge_ghost", "eik_fim2d_active",
     "eik_fim2d_stats", "eik_path2d_dev", "eik_tmap3d_f32", "eik_tmap3d_f64", "eik_path3d_f64", "eik_fim3d_solve",
     "eik_path3d_dev", "eik_costmap_f64", "eik_costmap_dev", "eik_surface_normal_f64", "eik_image_fill_u8",
-    "eik_load_dem_txt", "eik_io_last_error",
+    "eik_load_dem_txt", "eik_io_last_error", "eik_fim2d_live_bind", "eik_fim2d_launch", "eik_fim2d_live_pack",
+    "eik_fim2d_live_merge", "eik_fim2d_release", "eik_node_allreduce", "eik_node_shm_open",
+    "eik_node_shm_close", "eik_node_shm_unlink", "eik_ipc_alloc", "eik_ipc_free", "eik_ipc_open", "eik_ipc_close",
 ]
 
 
@@ -321,6 +336,55 @@ class Fim2d:
         self.ctx._chk(lib().eik_fim2d_stats(self._h, C.byref(s)))
         return s.as_dict()
 
+    # live domain decomposition (eik_fim2d_live_bind / launch / live_pack / live_merge / release)
+    def live_bind(self, send, recv):
+        """send, recv: [parity][side] device addresses (int) or None"""
+        S = (vp * 8)(*[send[p][s] for p in range(2) for s in range(4)])
+        R = (vp * 8)(*[recv[p][s] for p in range(2) for s in range(4)])
+        self.ctx._chk(lib().eik_fim2d_live_bind(self._h, S, R))
+
+    def launch(self, live=True):
+        self.ctx._chk(lib().eik_fim2d_launch(self._h, 1 if live else 0))
+
+    def live_pack(self, parity):
+        self.ctx._chk(lib().eik_fim2d_live_pack(self._h, int(parity)))
+
+    def live_merge(self, parity):
+        a, c = i64(0), i64(0)
+        self.ctx._chk(lib().eik_fim2d_live_merge(self._h, int(parity), C.byref(a), C.byref(c)))
+        return a.value, c.value
+
+    def release(self):
+        a = i64(0)
+        self.ctx._chk(lib().eik_fim2d_release(self._h, C.byref(a)))
+        return a.value
+
+
+class IpcBuffer:
+    """A device buffer other processes of the node can map (eik_ipc_alloc / eik_ipc_open)."""
+
+    def __init__(self, ctx, nbytes):
+        self.ctx = ctx
+        p = vp()
+        h = C.create_string_buffer(64)
+        ctx._chk(lib().eik_ipc_alloc(ctx._h, int(nbytes), C.byref(p), h))
+        self.ptr, self.handle, self.nbytes = p.value, h.raw, int(nbytes)
+
+    def close(self):
+        if getattr(self, "ptr", None):
+            lib().eik_ipc_free(self.ctx._h, self.ptr)
+            self.ptr = None
+
+
+def ipc_open(ctx, handle):
+    p = vp()
+    ctx._chk(lib().eik_ipc_open(ctx._h, C.create_string_buffer(bytes(handle), 64), C.byref(p)))
+    return p.value
+
+
+def ipc_close(ctx, ptr):
+    ctx._chk(lib().eik_ipc_close(ctx._h, ptr))
+
 
 _default = {}
 
@@ -333,3 +397,28 @@ def default_context(device=0):
         c = Context(device)
         _default[key] = c
     return c
+
+
+def node_shm_open(name, nbytes, create):
+    p = vp()
+    rc = lib().eik_node_shm_open(name.encode(), int(nbytes), 1 if create else 0, C.byref(p))
+    if rc != EIK_OK:
+        raise EikError(rc, f"shared memory segment {name!r} could not be {'created' if create else 'opened'}")
+    return p.value
+
+
+def node_shm_close(addr, nbytes):
+    lib().eik_node_shm_close(addr, int(nbytes))
+
+
+def node_shm_unlink(name):
+    lib().eik_node_shm_unlink(name.encode())
+
+
+def node_allreduce(addr, rank, world, rnd, value, timeout_s=60.0):
+    """eik_node_allreduce over a shared-memory segment at host address addr."""
+    out = i64(0)
+    rc = lib().eik_node_allreduce(addr, int(rank), int(world), int(rnd), int(value), C.byref(out), float(timeout_s))
+    if rc != EIK_OK:
+        raise EikError(rc, "node all-reduce timed out (a rank stopped voting)")
+    return out.value

@@ -11,7 +11,18 @@ out-of-block neighbours are GHOST strips, and every `exchange_every` outer itera
 Updates are monotone min-merges, so stale ghosts only delay convergence, never change the
 fixed point.  The local solver is duck-typed (eikonal.Fim2d on the GPU; a numpy solver in the
 CPU tests) with start / iterate / pack_edges / merge_ghost / active.
+
+solve_live is the GPU-native schedule (the default of bench.py at N > 1): ONE persistent launch
+per rank stays up for the whole solve, serving its tile FIFO, while the host runs halo rounds
+beside it on a side stream -- the front crosses a rank boundary within one round (~0.1-0.3 ms)
+instead of waiting for the neighbour's whole local solve.  Edges go straight into the
+neighbours' receive strips (IpcHalo: peer stores over xGMI into hipIpc-shared memory,
+double-buffered by round parity); one small vote per round -- a shared-memory all-reduce
+(NodeVote) on one node, else a gloo all-reduce -- is both the barrier for those stores and the
+convergence test.
 """
+import datetime
+
 import torch
 import torch.distributed as dist
 
@@ -121,3 +132,178 @@ class GpuLocal:
     def active(self):
         self.last_active = self.fim.active()
         return self.last_active
+
+
+# ------------------------------------------------------------------------- live schedule
+OPP = {N_: S_, S_: N_, W_: E_, E_: W_}
+ERR_MARK = 1 << 40  # carried through the all-reduce when a rank's solve failed
+
+
+def control_group(timeout_s=120):
+    """A gloo group for the per-round control all-reduce (CPU tensors, no GPU kernel)."""
+    if dist.get_backend() == "gloo":
+        return None
+    return dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=timeout_s))
+
+
+class NodeVote:
+    """Per-round sum vote through shared memory (eik_node_allreduce): every rank on one node.
+    Rank 0 creates the segment, the others attach; the name travels over `group`."""
+
+    def __init__(self, group=None, timeout_s=60.0):
+        import uuid
+
+        from . import _lib as L
+
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        self.nbytes = 64 * self.world
+        name = [f"/eik_dd_{uuid.uuid4().hex[:12]}" if self.rank == 0 else None]
+        dist.broadcast_object_list(name, src=0, group=group)
+        if self.rank == 0:
+            self.addr = L.node_shm_open(name[0], self.nbytes, True)
+        dist.barrier(group=group)
+        if self.rank != 0:
+            self.addr = L.node_shm_open(name[0], self.nbytes, False)
+        dist.barrier(group=group)
+        if self.rank == 0:
+            L.node_shm_unlink(name[0])  # every rank is attached: the name can go (no leak on a crash)
+        self.round, self.timeout_s, self._L = 0, timeout_s, L
+
+    def __call__(self, value):
+        self.round += 1
+        return self._L.node_allreduce(self.addr, self.rank, self.world, self.round, value, self.timeout_s)
+
+    def close(self):
+        if self.addr:
+            self._L.node_shm_close(self.addr, self.nbytes)
+            self.addr = None
+
+
+def solve_live(local, block, halo, group=None, max_rounds=1000000, vote=None):
+    """Drive one live solve to global convergence; returns the number of halo rounds.
+
+    Round r (parity p = r & 1):  send (snapshot A_r: tiles pending or busy; then pack this rank's
+    edges into the neighbours' strips of parity p)  ->  all-reduce of C_{r-1} (barrier for those
+    stores; C = A + ghost cells lowered)  ->  merge the strips of parity p (C_r).
+    C_{r-1} == 0 on every rank means: in round r-1 no tile was pending or busy anywhere when the
+    edges were packed, and merging them lowered no ghost -- T was frozen from that snapshot on,
+    so it is the global fixed point.  Stores of parity p land only after every rank has merged
+    parity p of round r-2 (it has passed the all-reduce of round r-1)."""
+    local.launch(halo)
+    carry, rounds, ok, err = 1, 0, False, None
+    try:
+        while rounds < max_rounds:
+            rounds += 1
+            par = rounds & 1
+            if err is None:
+                try:
+                    halo.send(local, par)
+                except Exception as e:  # keep the collective schedule: the others must learn of it
+                    err, carry = e, ERR_MARK
+            if vote is not None:
+                tot = vote(carry)
+            else:
+                t = torch.tensor([carry], dtype=torch.int64)
+                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+                tot = int(t.item())
+            if tot >= ERR_MARK:
+                raise RuntimeError("live domain-decomposed solve failed on a rank") from err
+            if tot == 0:
+                ok = True
+                return rounds
+            try:
+                a, c = halo.merge(local, par)
+                carry = a + c
+            except Exception as e:
+                err, carry = e, ERR_MARK
+        raise RuntimeError("live domain-decomposed solve did not converge")
+    finally:
+        left = local.release()
+        if ok and left != 0:
+            raise RuntimeError(f"live solve released with {left} tiles still active")
+
+
+class P2PHalo:
+    """Halo transport over torch.distributed P2P (gloo on CPU, RCCL on GPU): pack into local send
+    strips, exchange, receive into the strip set of the round's parity.  The local solver exposes
+    begin / pack_edges / sync / merge_ghost / end (tests/dd_cpu.py)."""
+
+    def __init__(self, block, dtype, device, group=None):
+        self.block, self.group = block, group
+        self.send_strips, r0, _ = make_strips(block, dtype, device, float("inf"))
+        _, r1, _ = make_strips(block, dtype, device, float("inf"))
+        self._recv = (r0, r1)
+
+    def send(self, local, par):
+        local.begin()
+        local.pack_edges(*self.send_strips)
+        local.sync()
+        exchange(self.block, self.send_strips, self._recv[par], self.group)
+
+    def merge(self, local, par):
+        for s in range(4):
+            if self.block.nb[s] is not None:
+                local.merge_ghost(s, self._recv[par][s])
+        return local.end()
+
+
+class IpcHalo:
+    """Receive strips in hipIpc-shared device memory; the halo agent of a rank's live launch
+    stores its edges directly into its neighbours' strips (peer stores over xGMI).  Strip
+    (parity p, side s) of a block with sides h x w sits at byte ((p * 4 + s) * max(h, w)) * elem."""
+
+    def __init__(self, ctx, block, elem_bytes, group=None):
+        from . import _lib as L
+
+        self.ctx, self.block, self.elem = ctx, block, elem_bytes
+        slot = max(block.h, block.w) * elem_bytes
+        self.buf = L.IpcBuffer(ctx, 8 * slot)
+        self.base, self.slot = self.buf.ptr, slot
+        handles = [None] * dist.get_world_size(group)
+        dist.all_gather_object(handles, self.buf.handle, group=group)
+        self.peers = {}
+        self.targets = ([None] * 4, [None] * 4)
+        self.recvs = ([None] * 4, [None] * 4)
+        for s in range(4):
+            nb = block.nb[s]
+            if nb is None:
+                continue
+            if nb not in self.peers:
+                self.peers[nb] = L.ipc_open(ctx, handles[nb])
+            pb = Block(block.H, block.W, block.px, block.py, nb)
+            pslot = max(pb.h, pb.w) * elem_bytes
+            for par in (0, 1):
+                self.targets[par][s] = self.peers[nb] + (par * 4 + OPP[s]) * pslot
+                self.recvs[par][s] = self.base + (par * 4 + s) * slot
+
+    def send(self, local, par):
+        local.live_pack(par)
+
+    def merge(self, local, par):
+        return local.live_merge(par)
+
+    def close(self):
+        from . import _lib as L
+
+        for p in self.peers.values():
+            L.ipc_close(self.ctx, p)
+        self.peers = {}
+        self.buf.close()
+
+
+class LiveGpuLocal(GpuLocal):
+    """solve_live adapter over eikonal.Fim2d (persistent mode): one launch stays up per solve; its
+    halo agent packs and merges on the host's command (halo.targets / halo.recvs strips)."""
+
+    def launch(self, halo):
+        self.fim.live_bind(halo.targets, halo.recvs)
+        self.fim.launch(live=True)
+
+    def live_pack(self, par):
+        self.fim.live_pack(par)
+
+    def live_merge(self, par):
+        return self.fim.live_merge(par)
+
+    def release(self):
+        return self.fim.release()

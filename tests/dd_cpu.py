@@ -1,7 +1,8 @@
 """CPU local solver for the domain-decomposition tests (TEST INFRASTRUCTURE, numpy).
 
-Implements the duck-typed local-solver protocol of eikonal/dd.py (start / iterate /
-pack_edges / merge_ghost / active) with a vectorised Jacobi Godunov iteration on one block
+Implements the duck-typed local-solver protocols of eikonal/dd.py (start / iterate /
+pack_edges / merge_ghost / active for dd.solve; launch / begin / sync / end / release for
+dd.solve_live over dd.P2PHalo) with a vectorised Jacobi Godunov iteration on one block
 plus its ghost strips, so the rank-exchange logic of dd.solve can be exercised with the gloo
 backend on CPU.  The GPU path plugs eikonal.Fim2d into the same driver (dd.GpuLocal).
 """
@@ -43,18 +44,46 @@ class CpuLocal:
                 P[sl] = self.ghosts[side].numpy()
         return P
 
+    def _sweep(self):
+        """one Jacobi sweep; returns whether T changed"""
+        P = self._padded()
+        a = np.minimum(P[1:-1, :-2], P[1:-1, 2:])
+        b = np.minimum(P[:-2, 1:-1], P[2:, 1:-1])
+        nv = np.minimum(self.T, godunov(a, b, self.cost))
+        if np.array_equal(nv, self.T):
+            return False
+        self.T = nv
+        return True
+
     def iterate(self, k):
         if not self.dirty:
             return
-        while True:
-            P = self._padded()
-            a = np.minimum(P[1:-1, :-2], P[1:-1, 2:])
-            b = np.minimum(P[:-2, 1:-1], P[2:, 1:-1])
-            nv = np.minimum(self.T, godunov(a, b, self.cost))
-            if np.array_equal(nv, self.T):
-                break
-            self.T = nv
+        while self._sweep():
+            pass
         self.dirty = False
+
+    # live protocol (dd.solve_live): the "concurrently running kernel" advances live_sweeps
+    # Jacobi sweeps per round, so fronts cross blocks mid-solve as on the GPU
+    live_sweeps = 3
+
+    def launch(self, halo=None):
+        self.changed, self.snap = 0, 1
+
+    def begin(self):
+        for _ in range(self.live_sweeps):
+            if not self.dirty:
+                break
+            self.dirty = self._sweep()
+        self.snap, self.changed = int(self.dirty), 0
+
+    def sync(self):
+        pass
+
+    def end(self):
+        return self.snap, self.changed
+
+    def release(self):
+        return int(self.dirty)
 
     def pack_edges(self, n, s, w, e):
         for t, v in ((n, self.T[0]), (s, self.T[-1]), (w, self.T[:, 0]), (e, self.T[:, -1])):
@@ -64,8 +93,10 @@ class CpuLocal:
     def merge_ghost(self, side, recv):
         g = self.ghosts[side]
         m = torch.minimum(g, recv)
-        if bool((m < g).any()):
+        n = int((m < g).sum())
+        if n:
             self.dirty = True
+            self.changed = getattr(self, "changed", 0) + n
         g.copy_(m)
 
     def active(self):

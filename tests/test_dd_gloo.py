@@ -1,5 +1,6 @@
-"""Multi-rank domain decomposition on CPU (gloo): the halo-exchange driver eikonal/dd.py, run
-with 2 and 4 ranks on blocks of one raster, must converge to the single-domain solution (the
+"""Multi-rank domain decomposition on CPU (gloo): the halo-exchange drivers of eikonal/dd.py
+(dd.solve rounds and the dd.solve_live protocol over P2PHalo), run with 2 and 4 ranks on blocks
+of one raster, must converge to the single-domain solution (the
 oracle FMM field, <= 1e-9 abs: same Godunov fixed point).  The GPU bench plugs the HIP solver
 into the same driver over RCCL."""
 import os
@@ -31,7 +32,7 @@ def _cost(H, W, seed):
     return c
 
 
-def _worker(rank, world, port, H, W, goal, seed, q):
+def _worker(rank, world, port, H, W, goal, seed, q, live=False):
     from dd_cpu import CpuLocal
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -43,14 +44,24 @@ def _worker(rank, world, port, H, W, goal, seed, q):
     send, recv, ghost = dd.make_strips(blk, torch.float64, "cpu", float("inf"))
     loc = CpuLocal(cost, ghost)
     loc.start(blk.local_goal(*goal))
-    rounds = dd.solve(loc, blk, send, recv, exchange_every=4)
+    if live:
+        vote = dd.NodeVote() if live == "node" else None
+        halo = dd.P2PHalo(blk, torch.float64, "cpu")
+        rounds = dd.solve_live(loc, blk, halo, group=dd.control_group(), vote=vote)
+        if vote is not None:  # a second solve on the same vote (round numbers carry on)
+            loc.start(blk.local_goal(*goal))
+            assert dd.solve_live(loc, blk, halo, vote=vote) == rounds
+            vote.close()
+    else:
+        rounds = dd.solve(loc, blk, send, recv, exchange_every=4)
     q.put((rank, blk.y0, blk.y1, blk.x0, blk.x1, loc.T, rounds))
     dist.barrier()
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("live", [False, True, "node"])
 @pytest.mark.parametrize("world", [2, 4])
-def test_dd_matches_single_domain(world):
+def test_dd_matches_single_domain(world, live):
     H, W, seed = 48, 70, 3
     goal = (9, 30)
     c = _cost(H, W, seed)
@@ -58,7 +69,7 @@ def test_dd_matches_single_domain(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, H, W, goal, seed, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, H, W, goal, seed, q, live)) for r in range(world)]
     for p in procs:
         p.start()
     parts = [q.get(timeout=120) for _ in range(world)]
