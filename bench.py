@@ -170,6 +170,8 @@ def main():
     # 2) the same K steps again with a hipEvent pair around every sweep launch (roofline)
     el_i, visits, passes, sweep_ms, iters = (0.0, 0, 0, 0.0, 0) if args.no_timing else timed(True)
 
+    if world > 1:  # the halo transport delivered every final edge (a wrong field cannot pass)
+        dd_ok = dd.halo_consistent(blk, T, ghost, group=ctrl)
     value = H * W * args.steps / el / 1e9
     ms_per_step = el / args.steps * 1e3
 
@@ -226,6 +228,7 @@ def main():
     }
     if world > 1:
         out["config"]["dd_mode"] = dd_mode + (" (shm vote)" if dd_mode == "live" and vote is not None else "")
+        out["config"]["dd_halo_consistent"] = dd_ok
         rr = dd_rounds[-args.steps:]
         out["config"]["dd_rounds_per_solve"] = round(sum(rr) / max(len(rr), 1), 1)
         out["config"]["dd_us_per_round"] = round(ms_per_step * 1e3 / max(sum(rr) / max(len(rr), 1), 1), 1)

@@ -425,6 +425,8 @@ __device__ void live_agent(const Fim2dArgs& a, unsigned* sh) {
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: peer stores complete
         } else if (op == kLiveMerge) {
+            // the strips were stored by peer GPUs: drop any stale cached copy before reading
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
             for (int side = 0; side < 4; ++side) {
                 const R* rv = static_cast<const R*>(box->recv[par][side]);
                 R* g = static_cast<R*>(const_cast<void*>(a.ghost[side]));

@@ -307,3 +307,18 @@ class LiveGpuLocal(GpuLocal):
 
     def release(self):
         return self.fim.release()
+
+
+def halo_consistent(block, T, ghosts, group=None):
+    """After a converged solve every ghost strip equals the neighbour's final edge of T exactly
+    (the last round packed the final edges and merged them).  Checks the halo transport end to
+    end over `group` (CPU tensors); returns True on every rank iff it holds on all."""
+    h, w = T.shape
+    edges = [T[0, :], T[h - 1, :], T[:, 0], T[:, w - 1]]
+    send = [edges[s].detach().cpu().contiguous() if block.nb[s] is not None else None for s in range(4)]
+    recv = [torch.empty_like(send[s]) if send[s] is not None else None for s in range(4)]
+    exchange(block, send, recv, group)
+    ok = all(torch.equal(recv[s], ghosts[s].detach().cpu()) for s in range(4) if block.nb[s] is not None)
+    t = torch.tensor([1 if ok else 0], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(t.item())

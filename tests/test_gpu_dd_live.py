@@ -131,6 +131,7 @@ def _ipc_worker(rank, world, port, H, W, goal, seed, q, f64):
             loc.start(c, T, blk.local_goal(*goal), torch.cuda.current_stream(dev).cuda_stream)
             rounds = dd.solve_live(loc, blk, halo, vote=vote)
             torch.cuda.synchronize()
+            assert dd.halo_consistent(blk, T, ghost)
             res.append(T.cpu().double().numpy())
         dist.barrier()
         halo.close()

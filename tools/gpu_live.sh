@@ -18,3 +18,7 @@ tail -2 gpurun_out/live_bench4.log
 timeout -k 10 300 python bench.py --no-extra --no-cpu-baseline --steps 20 > gpurun_out/live_bench1.log 2>&1 \
     || { tail -40 gpurun_out/live_bench1.log; exit 1; }
 tail -1 gpurun_out/live_bench1.log
+EIK_BENCH_SHARED_GPU=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+    --master-addr 127.0.0.1 --master-port 29613 bench.py --gpus 2 --steps 10 --warmup 2 \
+    > gpurun_out/live_bench2_4096.log 2>&1 || { tail -40 gpurun_out/live_bench2_4096.log; exit 1; }
+tail -1 gpurun_out/live_bench2_4096.log
