@@ -13,7 +13,7 @@ N = 4096
 cost = terrain.cost_block(0, 0, N, N, N, N, seed=42, device=dev).contiguous()
 fim = eikonal.Fim2d(ctx, 1, N, N, L.EIK_F32)
 T = torch.empty_like(cost)
-for mode, delta in ((L.MODE_PERSISTENT, 0), (L.MODE_LIST, 0), (L.MODE_LIST, 3000), (L.MODE_LIST, 1000), (L.MODE_LIST, 300), (L.MODE_LIST, 100)):
+for mode, delta in ((L.MODE_PERSISTENT, 0), (L.MODE_LIST, 0), (L.MODE_LIST, 100000), (L.MODE_LIST, 30000), (L.MODE_LIST, 10000), (L.MODE_LIST, 3000), (L.MODE_LIST, 1000), (L.MODE_LIST, 300)):
     ctx.set_option(L.OPT_MODE, mode)
     ctx.set_option(L.OPT_DELTA, delta)
     for _ in range(2):
@@ -29,3 +29,5 @@ for mode, delta in ((L.MODE_PERSISTENT, 0), (L.MODE_LIST, 0), (L.MODE_LIST, 3000
     print(f"mode={mode} delta={delta}: {el:.3f} ms  launches={st['iterations']} visits={st['tile_visits']} "
           f"inplace={st['inplace_passes']}", flush=True)
 print("Tmax", float(T[torch.isfinite(T)].max()))
+Tf = T[torch.isfinite(T)]
+print(f"T max {Tf.max().item():.1f} median {Tf.median().item():.1f}  cost median {cost[torch.isfinite(cost)].median().item():.2f}")

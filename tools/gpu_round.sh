@@ -4,7 +4,7 @@
 export TMPDIR=/tmp
 R=${ROUND:-r01}
 O=gpurun_out
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > $O/t_all.log 2>&1 || { echo "tests rc=$?"; tail -n 30 $O/t_all.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/t_all.log 2>&1 || { echo "tests rc=$?"; tail -n 30 $O/t_all.log; exit 1; }
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke rc=$?"; exit 1; }
 timeout -k 10 600 python bench.py > $O/bench_$R.json 2> $O/bench_$R.err || { echo "bench rc=$?"; tail -n 20 $O/bench_$R.err; exit 1; }
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_$R -o prof -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline > $O/prof_$R.out 2> $O/prof_$R.err || { echo "prof rc=$?"; exit 1; }
