@@ -245,6 +245,7 @@ def main():
             "C3": bench_batch(ctx, dev, stream, args.extra_steps),
             "C5": bench_layers(ctx, dev, stream, cost, goal_g, args.extra_steps),
             "costmap": bench_costmap(ctx, dev, stream, args.extra_steps, goal_g),
+            "C4_1gpu": bench_c4(ctx, dev, stream, max(2, args.extra_steps // 2)),
         }
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -322,6 +323,26 @@ def bench_batch(ctx, dev, stream, steps, B=128, N=1024):
     torch.cuda.empty_cache()
     return {"workload": f"configs[2]: batch {B} x {N}x{N} terrain maps (seeds 1000..{1000 + B - 1}), one goal each",
             "value": round(B * N * N / sec / 1e9, 4), "unit": "Gcells/s", "ms_per_step": round(sec * 1e3, 4),
+            "steps": steps, "tile_visits_per_solve": st["tile_visits"], "inplace_passes_per_solve": st["inplace_passes"],
+            "reached_fraction": round(reach, 4)}
+
+
+def bench_c4(ctx, dev, stream, steps, N=16384):
+    """configs[3] on ONE GPU: the 16384^2 DEM-derived raster (terrain seed 7), goal at the centre,
+    solved whole (1 GiB cost + 1 GiB T in HBM).  The N = 4 / 8 driver runs measure the split
+    versions; this line is the single-GPU reference point of the same raster size."""
+    cost = terrain.cost_block(0, 0, N, N, N, N, seed=7, device=dev).contiguous()
+    T = torch.empty_like(cost)
+    fim = eikonal.Fim2d(ctx, 1, N, N, L.EIK_F32)
+    goal = (N // 2, N // 2)
+    sec = timed_loop(lambda: fim.solve(cost.data_ptr(), T.data_ptr(), [goal], stream.cuda_stream), steps)
+    st = fim.stats()
+    reach = float(torch.isfinite(T).float().mean())
+    fim.close()
+    del cost, T
+    torch.cuda.empty_cache()
+    return {"workload": f"configs[3] at 1 GPU: {N}x{N} DEM-derived raster (seed 7), single goal at the centre, 1x1",
+            "value": round(N * N / sec / 1e9, 4), "unit": "Gcells/s", "ms_per_step": round(sec * 1e3, 4),
             "steps": steps, "tile_visits_per_solve": st["tile_visits"], "inplace_passes_per_solve": st["inplace_passes"],
             "reached_fraction": round(reach, 4)}
 

@@ -99,6 +99,32 @@ __device__ __forceinline__ double godunov2_fast(double a, double b, double c) {
     return __builtin_fma(0.5, d + __builtin_sqrt(q), lo);
 }
 
+// Sweep step with the shortest dependency chain from the upstream values (a, b) to the result:
+//   d = min(|a - b|, c)      one v_sub + one v_min with the |.| source modifier (the legacy form
+//                            needs min + max + sub + unsigned min);
+//   q = 2c^2 - d^2           one fma against c2x2 = 2c^2, computed off the chain from the
+//                            prefetched cost (one rounding instead of two);
+//   w = lo + (d + sqrt(q))/2
+// Special values as godunov2_fast: a = b = +inf gives |a - b| = NaN, which v_min turns into c,
+// and w = +inf; c = +inf with one finite side gives NaN (no update).  v_min_f32 is written in
+// asm so that no NaN canonicalisation is inserted (IEEE minNum: a NaN operand yields the other).
+__device__ __forceinline__ float godunov2_chain(float a, float b, float c, float c2x2) {
+    const float lo = umin(a, b);
+    const float diff = a - b;
+    float d;
+    asm("v_min_f32 %0, |%1|, %2" : "=v"(d) : "v"(diff), "v"(c));
+    const float q = __builtin_fmaf(-d, d, c2x2);
+    return __builtin_fmaf(0.5f, d + __builtin_amdgcn_sqrtf(q), lo);
+}
+__device__ __forceinline__ double godunov2_chain(double a, double b, double c, double c2x2) {
+    const double lo = umin(a, b);
+    const double diff = a - b;
+    double d;
+    asm("v_min_f64 %0, |%1|, %2" : "=v"(d) : "v"(diff), "v"(c));
+    const double q = __builtin_fma(-d, d, c2x2);
+    return __builtin_fma(0.5, d + __builtin_sqrt(q), lo);
+}
+
 // Whole-wave shift by one lane (lane i <- lane i-1) on the DPP path: v_mov_b32_dpp wave_shr:1.
 // Keeps the Gauss-Seidel dependency of the skewed sweep in registers (no LDS round trip).
 __device__ __forceinline__ float wave_shr1(float v) {
@@ -118,6 +144,19 @@ __device__ __forceinline__ double wave_shr1(double v) {
     const unsigned long long u = __double_as_longlong(v);
     const int lo = __builtin_amdgcn_update_dpp(0, (int)(u & 0xffffffffu), 0x138, 0xF, 0xF, false);
     const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), 0x138, 0xF, 0xF, false);
+    return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+// Whole-wave shift by one lane with the identity of an unsigned min in lane 0 (UINT_MAX, i.e. a
+// NaN pattern above every value): umin(wave_shr1_umin_id(x), y) is one v_min_u32_dpp once the
+// DPP combiner folds the move into its user, and lane 0 gets y.
+__device__ __forceinline__ float wave_shr1_umin_id(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(-1, __float_as_int(v), 0x138, 0xF, 0xF, false));
+}
+__device__ __forceinline__ double wave_shr1_umin_id(double v) {
+    const unsigned long long u = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(-1, (int)(u & 0xffffffffu), 0x138, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(-1, (int)(u >> 32), 0x138, 0xF, 0xF, false);
     return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 

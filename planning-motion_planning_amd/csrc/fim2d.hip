@@ -96,8 +96,12 @@ __device__ __forceinline__ bool sweep_quadrant(R* __restrict__ Ts, int lane, R k
     for (int s = 0; s < 2 * kTile; s += D) {
 #pragma unroll
         for (int u = 0; u < D; ++u) {
-            const R upx = wave_shr1(cur, q_upx[u]);  // lane 0: halo column
-            const R w = godunov2_fast(umin(upx, q_dnx[u]), umin(cur, q_dny[u]), q_c[u]);
+            // x side: lane 0 takes the halo column; lanes 1.. take lane l-1's fresh value (DPP)
+            // -- the prefetched LDS value of that cell is a valid, possibly stale, upper bound, so
+            // one v_min3 serves both cases; the chain to w is godunov2_chain's (see there)
+            const R xs = umin(q_upx[u], q_dnx[u]);
+            const R c2x2 = R(2) * (q_c[u] * q_c[u]);
+            const R w = godunov2_chain(umin(wave_shr1_umin_id(cur), xs), umin(cur, q_dny[u]), q_c[u], c2x2);
             lds_min(reinterpret_cast<R*>(base + q_o[u]), w);
             if constexpr (TRACK) changed |= w < q_old[u] * keep;
             cur = umin(w, q_old[u]);  // NaN (both-inf case) sorts above every value: keeps old
