@@ -431,12 +431,29 @@ def bench_costmap(ctx, dev, stream, steps, goal, N=4096, res=0.05):
     sec2 = timed_loop(dem_to_path, steps)
     obst_frac = float(obst.float().mean())
     fim.close()
+    # main()'s whole step 1 (:1097-1258) through one ABI call from the host
+    # DEM -- cost raster, both fronts in fp64 as the reference, device join, two path kernels, host
+    # assembly (pageable H2D of the DEM included)
+    sys.path.insert(0, os.path.join(ROOT, "planning-motion_planning_amd"))
+    import planner
+    Zh = Z.cpu().numpy()
+    q = planner.query(res * (g[0] + 1), res * (g[1] + 1), res * (256 + 1), res * (256 + 1), 0.0, res, res * N)
+    rp = {}
+
+    def step1():
+        rp["r"] = ctx.rover_path(Zh, q)
+
+    sec3 = timed_loop(step1, max(2, steps // 2))
     return {"workload": f"cost raster of the planner (Coupled_motion_planner.py:1101-1216) from a {N}x{N} DEM "
                         f"(terrain seed 42, res {res} m), f64",
             "value": round(N * N / sec / 1e9, 4), "unit": "Gcells/s", "ms_per_step": round(sec * 1e3, 3),
             "steps": steps, "obstacle_fraction": round(obst_frac, 4),
             "ms_dem_to_path_device": round(sec2 * 1e3, 3), "path_points": int(n_d.item()),
-            "path_status": int(st_d.item())}
+            "path_status": int(st_d.item()),
+            "planner_step1": {"workload": "Coupled_motion_planner.py:1097-1258 via eik_rover_path_f64: host DEM -> "
+                                          "cost raster -> biComputeTmap (2 x fp64 fronts) -> 2 GDM paths -> roverPath",
+                              "ms": round(sec3 * 1e3, 3), "waypoints": int(len(rp["r"][0])),
+                              "node_join": [int(v) for v in rp["r"][2]]}}
 
 
 def cpu_baseline(cost, goal):

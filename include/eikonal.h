@@ -239,6 +239,39 @@ int eik_surface_normal_f64(eik_ctx* ctx, const double* Z, int64_t H, int64_t W, 
 /* image_filling(im) :82-94 (cv2.floodFill from (0, 0), 4-connected) on a 0/1 uint8 image */
 int eik_image_fill_u8(eik_ctx* ctx, const uint8_t* im, int64_t H, int64_t W, uint8_t* out);
 
+/* ---- rover path of the planner -----------------------------------
+ * Coupled_motion_planner.py main(), step 1 (:1097-1258): DEM -> cost raster (eik_costmap_*) ->
+ * biComputeTmap(cMap.T, sample node, rover node) -> getPathGDM from nodeJoin to each end ->
+ * roverPath = [flipud(pathS); pathG[1:]] in metres (res * (p + 1)), waypoints within 0.1 m of the
+ * rover or the sample dropped, z = zp + Zs[round(y / res), round(x / res)], heading =
+ * [initialHeading, atan2(dy, dx)...].  Nodes: pxm = int(round(xm / res - 1)) etc. (:1107-1117,
+ * Python's round: half to even).  Defaults of the reference: zp 0.07 (:1132), tau 0.5 (:1225). */
+typedef struct {
+    double xm, ym;            /* sample position (m), :1107-1108                                 */
+    double xr, yr;            /* rover position (m), :1115-1116                                  */
+    double initial_heading;   /* rad, :1254                                                      */
+    double resolution, size;  /* DEM spacing (m) and side (m) as main()'s arguments              */
+    double zp;                /* height of the rover reference system above the floor, :1132     */
+    double tau;               /* GDM step (cells), :1225-1226                                    */
+} eik_rover_query;
+
+/* Host-only tail of step 1 (no GPU, no context): from the two GDM paths (K x 2 cell coordinates,
+ * pathS from nodeJoin to the rover node, pathG from nodeJoin to the sample node) and the DEM Z
+ * (H x W, raw heights: the min shift of :1101 is applied here) to path_xyz (cap x 3, metres) and
+ * heading (cap).  *n_out = rows written; EIK_ERR_ARG if cap is too small or a waypoint falls
+ * outside Z (the reference raises IndexError there). */
+int eik_rover_assemble(const double* pathS, int64_t nS, const double* pathG, int64_t nG, const double* Z, int64_t H,
+                       int64_t W, const eik_rover_query* q, double* path_xyz, double* heading, int64_t cap,
+                       int64_t* n_out);
+
+/* The whole of step 1 on the GPU: cost raster, both fronts as one 2-map fp64 batch, the device
+ * join, the two path kernels, then eik_rover_assemble on the host.  Z: H x W host DEM.  join
+ * (nullable) receives nodeJoin; cost_out (nullable, H x W [y][x]) the cost raster.
+ * EIK_ERR_UNREACHABLE when the rover cannot reach the sample. */
+int eik_rover_path_f64(eik_ctx* ctx, const double* Z, int64_t H, int64_t W, const eik_rover_query* q,
+                       const eik_costmap_params* params, double* path_xyz, double* heading, int64_t cap,
+                       int64_t* n_out, uint32_t join[2], double* cost_out);
+
 /* ---- DEM ingest, host only: no GPU, no context --------------------
  * Coupled_motion_planner.py:1098-1099 reads PRL_DEM.txt as comma-separated rows with a Python
  * float() per value.  eik_load_dem_txt parses the same text with host threads (nthreads <= 0:

@@ -1157,4 +1157,83 @@ int eik_image_fill_u8(eik_ctx* c, const uint8_t* im, int64_t H, int64_t W, uint8
     return EIK_OK;
 }
 
+// ------------------------------------------------------- rover path (planner step 1, :1097-1258)
+int eik_rover_path_f64(eik_ctx* c, const double* Z, int64_t H, int64_t W, const eik_rover_query* q,
+                       const eik_costmap_params* params, double* path_xyz, double* heading, int64_t cap,
+                       int64_t* n_out, uint32_t join[2], double* cost_out) {
+    if (!c || !Z || !q || !path_xyz || !heading || !n_out || H < 3 || W < 3 || !(q->resolution > 0) ||
+        !(q->size > 0) || !(q->tau > 0))
+        return c ? set_err(c, EIK_ERR_ARG, "bad rover-path arguments") : EIK_ERR_ARG;
+    const int64_t n = H * W;
+    if (n >= (1ll << 29)) return set_err(c, EIK_ERR_ARG, "bidirectional join supports < 2^29 cells");
+    // nodes: int(round(v / res - 1)), Python's round = half to even   :1107-1117
+    const double res = q->resolution;
+    const int64_t g[4] = {(int64_t)std::nearbyint(q->xm / res - 1), (int64_t)std::nearbyint(q->ym / res - 1),
+                          (int64_t)std::nearbyint(q->xr / res - 1), (int64_t)std::nearbyint(q->yr / res - 1)};
+    for (int k = 0; k < 2; ++k)
+        if (g[2 * k] < 0 || g[2 * k + 1] < 0 || g[2 * k] >= W || g[2 * k + 1] >= H)
+            return set_err(c, EIK_ERR_ARG, "%s node (%ld, %ld) outside the %ldx%ld DEM", k ? "rover" : "sample",
+                           (long)g[2 * k], (long)g[2 * k + 1], (long)H, (long)W);
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    const int64_t steps = (int64_t)std::nearbyint(15000.0 / q->tau);  // FastMarching.py:173
+    const int64_t pcap = steps + 4;
+    const size_t pbytes = sizeof(double) * 2 * 2 * pcap + 64;
+    HIPCHK(c, c->T2.ensure(std::max(sizeof(double) * n, pbytes)));  // Z, then (Z consumed) the paths
+    HIPCHK(c, c->cost.ensure(sizeof(double) * 2 * n));
+    HIPCHK(c, c->T.ensure(sizeof(double) * 2 * n));
+    double* dZ = (double*)c->T2.p;
+    double* dcost = (double*)c->cost.p;
+    double* dT = (double*)c->T.p;
+    HIPCHK(c, hipMemcpyAsync(dZ, Z, sizeof(double) * n, hipMemcpyHostToDevice, st));
+    int rc = eik_costmap_dev(c, dZ, H, W, res, q->size, params, dcost, nullptr, st);  // :1101-1216
+    if (rc) return rc;
+    // biComputeTmap(cMap.T, goal = sample node, start = rover node)   :1222; both fronts, one batch
+    HIPCHK(c, hipMemcpyAsync(dcost + n, dcost, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
+    if (cost_out) HIPCHK(c, hipMemcpyAsync(cost_out, dcost, sizeof(double) * n, hipMemcpyDeviceToHost, st));
+    eik_fim2d* f = nullptr;
+    rc = get_solver(c, 2, H, W, EIK_F64, &f);
+    if (rc) return rc;
+    rc = eik_fim2d_solve(f, dcost, dT, g, st);
+    if (rc) return rc;
+    const size_t wb = bidir_join_work_bytes(n);
+    HIPCHK(c, c->work.ensure(wb));
+    HIPCHK(c, c->misc.ensure(64));
+    HIPCHK(c, bidir_join(dT, dT + n, n, c->work.p, c->work.bytes, (unsigned long long*)c->misc.p, st));
+    unsigned long long best = 0;
+    HIPCHK(c, hipMemcpyAsync(&best, c->misc.p, sizeof best, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    if (best == ~0ull) return set_err(c, EIK_ERR_UNREACHABLE, "the rover cannot reach the sample");
+    const int64_t node = (int64_t)(best & ((1ull << 29) - 1));
+    const double jn[2] = {(double)(node % W), (double)(node / W)};
+    if (join) {
+        join[0] = (uint32_t)(node % W);
+        join[1] = (uint32_t)(node / W);
+    }
+    // pathG = getPathGDM(TmapG, nodeJoin, goal, tau), pathS = getPathGDM(TmapS, nodeJoin, start, tau)   :1225-1226
+    double* dP = (double*)c->T2.p;  // [pathG | pathS], then n_out[2], status[2]
+    int64_t* dn = (int64_t*)(dP + 2 * 2 * pcap);
+    int* dst = (int*)(dn + 2);
+    const double eg[2] = {(double)g[0], (double)g[1]}, es[2] = {(double)g[2], (double)g[3]};
+    rc = eik_path2d_dev(c, dT, EIK_F64, H, W, jn, eg, q->tau, dP, pcap, dn, dst, st);
+    if (rc) return rc;
+    rc = eik_path2d_dev(c, dT + n, EIK_F64, H, W, jn, es, q->tau, dP + 2 * pcap, pcap, dn + 1, dst + 1, st);
+    if (rc) return rc;
+    int64_t hn[2];
+    int hs[2];
+    HIPCHK(c, hipMemcpyAsync(hn, dn, sizeof hn, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(hs, dst, sizeof hs, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    if (hs[0] == EIK_PATH_ERROR || hs[1] == EIK_PATH_ERROR)
+        return set_err(c, EIK_ERR_ARG, "getPathGDM failed (the reference raises): NaN point or out of range");
+    std::vector<double> pg((size_t)(2 * hn[0])), ps((size_t)(2 * hn[1]));
+    HIPCHK(c, hipMemcpyAsync(pg.data(), dP, sizeof(double) * 2 * hn[0], hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(ps.data(), dP + 2 * pcap, sizeof(double) * 2 * hn[1], hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    rc = eik_rover_assemble(ps.data(), hn[1], pg.data(), hn[0], Z, H, W, q, path_xyz, heading, cap, n_out);
+    if (rc) return set_err(c, rc, *n_out > cap ? "path buffer too small (%ld rows needed)" : "waypoint outside the DEM",
+                           (long)*n_out);
+    return EIK_OK;
+}
+
 }  // extern "C"

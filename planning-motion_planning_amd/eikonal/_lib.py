@@ -31,6 +31,13 @@ class CostmapParams(C.Structure):
                 ("gradient", C.c_double), ("high", C.c_double)]
 
 
+class RoverQuery(C.Structure):
+    """eik_rover_query (include/eikonal.h): main()'s step-1 arguments (Coupled_motion_planner.py:1092)."""
+    _fields_ = [("xm", C.c_double), ("ym", C.c_double), ("xr", C.c_double), ("yr", C.c_double),
+                ("initial_heading", C.c_double), ("resolution", C.c_double), ("size", C.c_double),
+                ("zp", C.c_double), ("tau", C.c_double)]
+
+
 class EikStats(C.Structure):
     _fields_ = [("iterations", i64), ("tile_visits", i64), ("host_syncs", i64), ("solve_ms", C.c_double),
                 ("sweep_ms", C.c_double), ("bytes_alg", C.c_double), ("inplace_passes", i64)]
@@ -129,6 +136,10 @@ def lib():
         L.eik_ipc_free.argtypes = [vp, vp]
         L.eik_ipc_open.argtypes = [vp, C.c_char_p, P(vp)]
         L.eik_ipc_close.argtypes = [vp, vp]
+        L.eik_rover_assemble.argtypes = [_f64p, i64, _f64p, i64, _f64p, i64, i64, P(RoverQuery), _f64p, _f64p, i64,
+                                         P(i64)]
+        L.eik_rover_path_f64.argtypes = [vp, _f64p, i64, i64, P(RoverQuery), P(CostmapParams), _f64p, _f64p, i64,
+                                         P(i64), _u32p, vp]
         _lib = L
         return L
 
@@ -143,7 +154,25 @@ EXPORTED = [
     "eik_load_dem_txt", "eik_io_last_error", "eik_fim2d_live_bind", "eik_fim2d_launch", "eik_fim2d_live_pack",
     "eik_fim2d_live_merge", "eik_fim2d_release", "eik_node_allreduce", "eik_node_shm_open",
     "eik_node_shm_close", "eik_node_shm_unlink", "eik_ipc_alloc", "eik_ipc_free", "eik_ipc_open", "eik_ipc_close",
+    "eik_rover_assemble", "eik_rover_path_f64",
 ]
+
+
+def rover_assemble(pathS, pathG, Z, query, cap=None):
+    """Host tail of the planner's step 1 (Coupled_motion_planner.py:1228-1252), no GPU:
+    (roverPath (N, 3) metres, heading (N,))."""
+    pathS = np.ascontiguousarray(pathS, np.float64)
+    pathG = np.ascontiguousarray(pathG, np.float64)
+    Z = np.ascontiguousarray(Z, np.float64)
+    cap = cap or len(pathS) + len(pathG)
+    out = np.empty((cap, 3))
+    hd = np.empty(cap)
+    n = i64(0)
+    rc = lib().eik_rover_assemble(pathS, len(pathS), pathG, len(pathG), Z, Z.shape[0], Z.shape[1], C.byref(query),
+                                  out, hd, cap, C.byref(n))
+    if rc != EIK_OK:
+        raise IndexError(f"rover path: waypoint outside the DEM or buffer too small (rc {rc}, {n.value} rows)")
+    return out[: n.value].copy(), hd[: n.value].copy()
 
 
 def load_dem_txt(path, nthreads=0):
@@ -260,6 +289,23 @@ class Context:
         p = C.byref(params) if params is not None else None
         self._chk(lib().eik_costmap_f64(self._h, Z, H, W, float(resolution), float(size), p, cost, obst.ctypes.data))
         return cost, obst
+
+    def rover_path(self, Z, query, params=None, want_cost=False):
+        """Planner step 1 on the GPU (Coupled_motion_planner.py:1097-1258): DEM -> (roverPath (N, 3),
+        heading (N,), nodeJoin uint32 (2,)[, cost raster [y][x]])."""
+        Z = np.ascontiguousarray(Z, dtype=np.float64)
+        H, W = Z.shape
+        cap = 2 * int(round(15000 / query.tau)) + 8
+        out = np.empty((cap, 3))
+        hd = np.empty(cap)
+        n = i64(0)
+        join = np.zeros(2, np.uint32)
+        cost = np.empty_like(Z) if want_cost else None
+        p = C.byref(params) if params is not None else None
+        self._chk(lib().eik_rover_path_f64(self._h, Z, H, W, C.byref(query), p, out, hd, cap, C.byref(n), join,
+                                           cost.ctypes.data if want_cost else None))
+        res = (out[: n.value].copy(), hd[: n.value].copy(), join)
+        return res + (cost,) if want_cost else res
 
     def surface_normal(self, Z, size):
         Z = np.ascontiguousarray(Z, dtype=np.float64)
