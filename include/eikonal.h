@@ -272,6 +272,46 @@ int eik_rover_path_f64(eik_ctx* ctx, const double* Z, int64_t H, int64_t W, cons
                        const eik_costmap_params* params, double* path_xyz, double* heading, int64_t cap,
                        int64_t* n_out, uint32_t join[2], double* cost_out);
 
+/* ---- end-effector cost volume of the planner ---------------------
+ * Coupled_motion_planner.py main(), step 3 (:1462-1593): the arm's FM3D runs on
+ * Cmap = GetObstMap(...)[0] * TunnelCost(...) over a small square area around the sample.  The
+ * volume is [iy][ix][iz], sY x sX x sZ with sX == sY (the planner's area is square, :1519). */
+typedef struct {
+    int64_t sX, sY, sZ;              /* nodes per axis, :1528-1529                                 */
+    double resX, resY, resZ;         /* m per node, :1532-1534                                     */
+    double xm, ym;                   /* GetObstMap's sample test: columns with resX*i == xm or
+                                        resY*j == ym are skipped (:329; the planner passes the
+                                        global sample position)                                    */
+    double rlim, rO, rm;             /* TunnelCost(Rlim, rO, rm, ...), :1577 (Rlim, rO, rm :1121-1124) */
+    uint32_t final_wp[3];            /* sample node (x, y, z), :1574                                */
+    uint32_t initial_wp[3];          /* end-effector start node (x, y, z), :1573                    */
+} eik_arm_volume;
+
+/* GetObstMap(ZsMap, resX, resY, resZ, sX, sY, sZ, newObstMap, xm, ym) :319-358.  ZsMap, newObstMap:
+ * m x n (row j = y).  finalMap (2 / +inf), obstMap and groundMap (1 / +inf; nullable): sX*sY*sZ. */
+int eik_arm_obst_map_f64(eik_ctx* ctx, const double* ZsMap, const double* newObstMap, int64_t m, int64_t n,
+                         const eik_arm_volume* vol, double* finalMap, double* obstMap, double* groundMap);
+
+/* TunnelCost(rlim, rO, rm, gamma2D, sX, sY, sZ, resX, resY, resZ, finalBaseHeading, finalWayPointArm,
+ * initialWayPointArm) :505-725.  gamma2D, heading: npts x 3 (arm base positions in the area's frame,
+ * (roll, pitch, yaw) per point).  Cmap: sY*sX*sZ (10 / tunnel cost / +inf), bit-identical to the
+ * reference (tests/golden/arm.npz). */
+int eik_arm_tunnel_cost_f64(eik_ctx* ctx, const double* gamma2D, const double* heading, int64_t npts,
+                            const eik_arm_volume* vol, double* Cmap);
+
+/* :1562-1593 on the GPU: Cmap = finalMap * tunnel on the device -> FM3D.computeTmap(Cmap,
+ * finalWayPointArm, initialWayPointArm) -> FM3D.getPathGDM(T, initialWayPointArm, finalWayPointArm,
+ * tau) -> path (cap x 3 node coordinates, before the planner's scaling and smoothing, :1588-1598).
+ * cost_out / T_out (nullable): the volume and the arrival field, sY*sX*sZ. */
+int eik_arm_path_f64(eik_ctx* ctx, const double* ZsMap, const double* newObstMap, int64_t m, int64_t n,
+                     const double* gamma2D, const double* heading, int64_t npts, const eik_arm_volume* vol, double tau,
+                     double* path, int64_t cap, int64_t* n_out, int* status, double* cost_out, double* T_out);
+
+/* FastMarching3D.computeTmap on B independent volumes of one shape in ONE solve (candidate fetch
+ * poses): cost, T: B*H*W*L; goals: B x (x, y, z). */
+int eik_tmap3d_batch_f64(eik_ctx* ctx, const double* cost, int64_t B, int64_t H, int64_t W, int64_t L,
+                         const int64_t* goals, double* T);
+
 /* ---- DEM ingest, host only: no GPU, no context --------------------
  * Coupled_motion_planner.py:1098-1099 reads PRL_DEM.txt as comma-separated rows with a Python
  * float() per value.  eik_load_dem_txt parses the same text with host threads (nthreads <= 0:

@@ -90,8 +90,10 @@ struct Fim3dArgs {
     unsigned iter;
     int max_passes;        // relaxation passes per tile visit
     unsigned long long* visits;
+    int tpv;               // tiles per volume (B volumes: tile = volume * tpv + tile in volume)
 };
-hipError_t fim3d_init(const Fim3dArgs& a, bool f64, int64_t gx, int64_t gy, int64_t gz, hipStream_t st);
+// T = inf for B volumes, goal cell of volume b = d_goals[3b..3b+2] (x, y, z) set to 0 and listed
+hipError_t fim3d_init(const Fim3dArgs& a, bool f64, const int64_t* d_goals, int B, hipStream_t st);
 hipError_t fim3d_sweep(const Fim3dArgs& a, bool f64, int grid, hipStream_t st);
 void fim3d_tile_shape(int64_t L, int* tx, int* ty, int* tz);
 
@@ -138,5 +140,28 @@ hipError_t cm_cost(const unsigned char* obst, const unsigned char* dil, const in
 
 // Full-field inf-aware normalised gradient (computeGradient(T, point=[]), FastMarching.py:242-300)
 hipError_t gradient2d(const double* T, int64_t H, int64_t W, double* gnx, double* gny, hipStream_t st);
+
+// End-effector cost volume (arm.hip): GetObstMap + TunnelCost event painting.
+struct ArmArgs {
+    long long sX, sY, sZ;       // volume [iy][ix][iz], sY x sX x sZ (the planner's area is square)
+    double resX, resY, resZ, rlim, rad;
+    int nX, nZ, nK;
+    unsigned long long nA, nB, nC;  // events of the tunnel, the closing step, the half sphere
+    const double* toaA;         // [points][12]: rows 0..2 of the base transform (yaw - pi/2)
+    const double* toaB;         // [12] first point (closing step)
+    const double* toaC;         // [12] last point, no yaw offset (half sphere)
+    const double *tabI, *tabK, *norm, *valA;      // linspaces, per (i, k) norm and value
+    const double *ct, *st, *cs, *ss, *ks, *valC;  // half-sphere tables
+    long long fw[3], iw[3];     // sample / start nodes (x, y, z)
+    unsigned* first;            // [cells] lowest assign sequence number
+    unsigned char* closed;      // [cells]
+    double* tunnel;             // [cells] TunnelCost's Cmap
+    const double* fmap;         // [cells] GetObstMap's finalMap (for out)
+    double* out;                // nullable: fmap * tunnel
+};
+hipError_t arm_obst_map(const double* Zs, const double* obst, int64_t m, int64_t n, double resX, double resY,
+                        double resZ, int64_t sX, int64_t sY, int64_t sZ, double xm, double ym, double* fmap,
+                        double* omap, double* gmap, unsigned* bad, hipStream_t st);
+hipError_t arm_tunnel(const ArmArgs& a, hipStream_t st);
 
 }  // namespace eik

@@ -68,6 +68,7 @@ struct eik_ctx {
     eik_fim2d* cached_l = nullptr;  // queue state of the layered 3D solver (fim2dl.hip)
     eik_fim2d* cached_fill = nullptr;  // reachability solver of the cost builder's hole filling
     DevBuf cm_u8, cm_i32, cm_f32, cm_f64;  // cost-builder scratch
+    DevBuf arm;                            // end-effector volume scratch (arm.hip)
     int resident_l[5] = {0, 0, 0, 0, 0};  // co-resident workgroups of fim2dl_persist_kernel<nl>
     DevBuf cost, T, T2, goals, work, misc;
     DevBuf l3, c3, m3, v3;             // 3D solver scratch (lists, counts, marks, visits)
@@ -858,23 +859,10 @@ static int layered_plan(eik_ctx* c, const void* d_cost, int64_t H, int64_t W, in
     return EIK_OK;
 }
 
-int eik_fim3d_solve(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, int64_t W, int64_t L, int dtype,
-                    const int64_t goal[3], void* stream) {
-    if (!c || !d_cost || !d_T || !goal || H < 1 || W < 1 || L < 1)
-        return c ? set_err(c, EIK_ERR_ARG, "bad 3D arguments") : EIK_ERR_ARG;
-    if (goal[0] < 0 || goal[1] < 0 || goal[2] < 0 || goal[0] >= W || goal[1] >= H || goal[2] >= L)
-        return set_err(c, EIK_ERR_ARG, "goal (%ld,%ld,%ld) outside %ldx%ldx%ld", (long)goal[0], (long)goal[1],
-                       (long)goal[2], (long)H, (long)W, (long)L);
-    HIPCHK(c, hipSetDevice(c->device));
-    hipStream_t st = (hipStream_t)stream;
-    if (dtype == EIK_F32 && c->mode == kModePersistent && c->max_rounds == 1 && H * W * L * 4 < (int64_t)UINT32_MAX) {
-        int z0 = 0, nl = 0;
-        int rc = layered_plan(c, d_cost, H, W, L, st, &z0, &nl);
-        if (rc) return rc;
-        if (nl > 0 && goal[2] >= z0 && goal[2] < z0 + nl) {
-            return solve_layered(c, d_cost, d_T, H, W, L, z0, nl, goal, st);
-        }
-    }
+// B independent volumes of one shape (list mode; the tiles of all volumes share the lists).
+// goals: B x (x, y, z), host memory.
+static int fim3d_solve_batch(eik_ctx* c, const void* d_cost, void* d_T, int64_t B, int64_t H, int64_t W, int64_t L,
+                             int dtype, const int64_t* goals, hipStream_t st) {
     Fim3dArgs a{};
     a.cost = d_cost;
     a.T = d_T;
@@ -885,8 +873,10 @@ int eik_fim3d_solve(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, int64_
     a.ntx = (int)((W + a.tx - 1) / a.tx);
     a.nty = (int)((H + a.ty - 1) / a.ty);
     a.ntz = (int)((L + a.tz - 1) / a.tz);
-    const int64_t tiles = (int64_t)a.ntx * a.nty * a.ntz;
+    const int64_t tpv = (int64_t)a.ntx * a.nty * a.ntz;
+    const int64_t tiles = B * tpv;
     if (tiles >= (1ll << 31) - 8) return set_err(c, EIK_ERR_ARG, "too many 3D tiles");
+    a.tpv = (int)tpv;
     a.capacity = (int)tiles;
     a.max_passes = c->max_passes3;
     HIPCHK(c, c->l3.ensure(sizeof(int) * 3 * tiles));
@@ -902,7 +892,9 @@ int eik_fim3d_solve(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, int64_
     HIPCHK(c, hipEventCreate(&e1));
     HIPCHK(c, hipEventRecord(e0, st));
     HIPCHK(c, hipMemsetAsync(c->v3.p, 0, sizeof(unsigned long long), st));
-    HIPCHK(c, fim3d_init(a, dtype == EIK_F64, goal[0], goal[1], goal[2], st));
+    HIPCHK(c, c->goals.ensure(sizeof(int64_t) * 3 * B));
+    HIPCHK(c, hipMemcpyAsync(c->goals.p, goals, sizeof(int64_t) * 3 * B, hipMemcpyHostToDevice, st));
+    HIPCHK(c, fim3d_init(a, dtype == EIK_F64, (const int64_t*)c->goals.p, (int)B, st));
     int* h = nullptr;
     HIPCHK(c, hipHostMalloc((void**)&h, sizeof(int) * 2 + sizeof(unsigned long long)));
     const int grid = c->grid > 0 ? c->grid : 4 * c->cu_count;
@@ -939,6 +931,26 @@ int eik_fim3d_solve(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, int64_
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     return rc;
+}
+
+int eik_fim3d_solve(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, int64_t W, int64_t L, int dtype,
+                    const int64_t goal[3], void* stream) {
+    if (!c || !d_cost || !d_T || !goal || H < 1 || W < 1 || L < 1)
+        return c ? set_err(c, EIK_ERR_ARG, "bad 3D arguments") : EIK_ERR_ARG;
+    if (goal[0] < 0 || goal[1] < 0 || goal[2] < 0 || goal[0] >= W || goal[1] >= H || goal[2] >= L)
+        return set_err(c, EIK_ERR_ARG, "goal (%ld,%ld,%ld) outside %ldx%ldx%ld", (long)goal[0], (long)goal[1],
+                       (long)goal[2], (long)H, (long)W, (long)L);
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == EIK_F32 && c->mode == kModePersistent && c->max_rounds == 1 && H * W * L * 4 < (int64_t)UINT32_MAX) {
+        int z0 = 0, nl = 0;
+        int rc = layered_plan(c, d_cost, H, W, L, st, &z0, &nl);
+        if (rc) return rc;
+        if (nl > 0 && goal[2] >= z0 && goal[2] < z0 + nl) {
+            return solve_layered(c, d_cost, d_T, H, W, L, z0, nl, goal, st);
+        }
+    }
+    return fim3d_solve_batch(c, d_cost, d_T, 1, H, W, L, dtype, goal, st);
 }
 
 }  // extern "C"
@@ -1233,6 +1245,308 @@ int eik_rover_path_f64(eik_ctx* c, const double* Z, int64_t H, int64_t W, const 
     rc = eik_rover_assemble(ps.data(), hn[1], pg.data(), hn[0], Z, H, W, q, path_xyz, heading, cap, n_out);
     if (rc) return set_err(c, rc, *n_out > cap ? "path buffer too small (%ld rows needed)" : "waypoint outside the DEM",
                            (long)*n_out);
+    return EIK_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------- end-effector cost volume (planner step 3, :1462-1593)
+namespace {
+
+// The host side of arm.hip: the tables TunnelCost forms in Python floats (:515-519, :527-546,
+// :571-590, :621-631, :655-668, :683-703), in the reference's evaluation order.
+struct ArmTables {
+    std::vector<double> buf;  // toaA | toaB | toaC | I | K | norm | valA | ct | st | cs | ss | ks | valC
+    size_t oA = 0, oB = 0, oC = 0, oI = 0, oK = 0, oN = 0, oV = 0, oct = 0, ost = 0, ocs = 0, oss = 0, oks = 0, ovc = 0;
+    int nX = 0, nZ = 0, nK = 0;
+    double rad = 0;
+};
+
+void np_linspace(double a, double b, int64_t n, double* out) {
+#pragma clang fp contract(off)
+    if (n == 1) {
+        out[0] = a;
+        return;
+    }
+    const double div = (double)(n - 1), delta = b - a, step = delta / div;
+    for (int64_t i = 0; i < n; ++i) out[i] = step == 0 ? ((double)i / div) * delta + a : (double)i * step + a;
+    out[n - 1] = b;
+}
+
+void arm_toa(const double* h, const double* p, double yaw_off, double* t) {
+#pragma clang fp contract(off)
+    const double alpha = h[2] - yaw_off, beta = h[1], gamma = h[0];
+    const double ca = std::cos(alpha), cb = std::cos(beta), cg = std::cos(gamma);
+    const double sa = std::sin(alpha), sb = std::sin(beta), sg = std::sin(gamma);
+    const double r[12] = {ca * cb, ca * sb * sg - sa * cg, ca * sb * cg + sa * sg, p[0],
+                          sa * cb, sa * sb * sg + ca * cg, sa * sb * cg - ca * sg, p[1],
+                          -sb,     cb * sg,                cb * cg,                p[2]};
+    for (int i = 0; i < 12; ++i) t[i] = r[i];
+}
+
+void arm_tables(const double* gamma2D, const double* heading, int64_t npts, const eik_arm_volume& v, ArmTables& T) {
+#pragma clang fp contract(off)
+    const double gradient = 15.0;                                              // :512
+    const double tunnelRad = v.rlim + 2 * v.resX;                              // :515
+    T.nX = (int)(std::nearbyint(2 * tunnelRad / v.resX) + 1);                  // :516
+    T.nZ = (int)(std::nearbyint(2 * tunnelRad / v.resZ) + 1);                  // :517
+    T.nK = (int)std::nearbyint(T.nZ / 2.0) + 1;                                // :671
+    T.rad = v.rlim + 2 * v.resZ;                                               // :688-690
+    const size_t nik = (size_t)T.nX * T.nZ;
+    size_t o = 0;
+    T.oA = o; o += 12 * (size_t)npts;
+    T.oB = o; o += 12;
+    T.oC = o; o += 12;
+    T.oI = o; o += T.nX;
+    T.oK = o; o += T.nZ;
+    T.oN = o; o += nik;
+    T.oV = o; o += nik;
+    T.oct = o; o += 100;
+    T.ost = o; o += 100;
+    T.ocs = o; o += 90;
+    T.oss = o; o += 90;
+    T.oks = o; o += T.nK;
+    T.ovc = o; o += T.nK;
+    T.buf.assign(o, 0.0);
+    double* b = T.buf.data();
+    const double half_pi = 3.141592653589793 / 2;  // math.pi / 2
+    for (int64_t j = 0; j < npts; ++j) arm_toa(heading + 3 * j, gamma2D + 3 * j, half_pi, b + T.oA + 12 * j);
+    arm_toa(heading, gamma2D, half_pi, b + T.oB);                                          // :617-631
+    arm_toa(heading + 3 * (npts - 1), gamma2D + 3 * (npts - 1), 0.0, b + T.oC);            // :655-668
+    np_linspace(-tunnelRad, tunnelRad, T.nX, b + T.oI);                                     // :563
+    np_linspace(-tunnelRad, tunnelRad, T.nZ, b + T.oK);                                     // :564
+    const double c = (v.rO + v.rm) / 2;
+    for (int i = 0; i < T.nX; ++i)
+        for (int k = 0; k < T.nZ; ++k) {
+            const double I = b[T.oI + i], K = b[T.oK + k];
+            const double i2 = I * I, k2 = K * K;
+            const double norm = std::sqrt(i2 + k2);                                         // :578
+            const double d = norm - c;
+            const double t1 = gradient * (d * d) + 2;
+            const double u = ((I + v.rlim) + 2 * v.resZ);
+            b[T.oN + (size_t)i * T.nZ + k] = norm;
+            b[T.oV + (size_t)i * T.nZ + k] = t1 + 4 * u;                                   // :590
+        }
+    for (int ti = 0; ti < 100; ++ti) {                                                      // :674-676
+        const double theta = 3.141592653589793 * (-100 + 2 * ti) / 180;
+        b[T.oct + ti] = std::cos(theta);
+        b[T.ost + ti] = std::sin(theta);
+    }
+    for (int si = 0; si < 90; ++si) {                                                       // :679-681
+        const double sigma = 3.141592653589793 * (-90 + 2 * si) / 180;
+        b[T.ocs + si] = std::cos(sigma);
+        b[T.oss + si] = std::sin(sigma);
+    }
+    np_linspace(0.0, tunnelRad, T.nK, b + T.oks);                                           // :684
+    for (int k = 0; k < T.nK; ++k) {
+        const double d = b[T.oks + k] - c;
+        b[T.ovc + k] = gradient * (d * d) + 2;                                              // :703
+    }
+}
+
+}  // namespace
+
+// Build the volume on the device into d_cost (fmap * tunnel) and/or return the pieces.  d_fmap:
+// GetObstMap's finalMap (computed here when d_Z != nullptr); d_tunnel: TunnelCost's map.
+static int arm_volume_dev(eik_ctx* c, const double* d_Z, const double* d_obst, int64_t m, int64_t n,
+                          const double* gamma2D, const double* heading, int64_t npts, const eik_arm_volume* v,
+                          double* d_fmap, double* d_omap, double* d_gmap, double* d_tunnel, double* d_cost,
+                          hipStream_t st) {
+    const int64_t nc = v->sX * v->sY * v->sZ;
+    if (d_Z) {
+        HIPCHK(c, c->misc.ensure(64));
+        HIPCHK(c, hipMemsetAsync(c->misc.p, 0, sizeof(unsigned), st));
+        HIPCHK(c, arm_obst_map(d_Z, d_obst, m, n, v->resX, v->resY, v->resZ, v->sX, v->sY, v->sZ, v->xm, v->ym, d_fmap,
+                               d_omap, d_gmap, (unsigned*)c->misc.p, st));
+    }
+    if (!d_tunnel) return EIK_OK;
+    ArmTables T;
+    arm_tables(gamma2D, heading, npts, *v, T);
+    ArmArgs a{};
+    a.sX = v->sX;
+    a.sY = v->sY;
+    a.sZ = v->sZ;
+    a.resX = v->resX;
+    a.resY = v->resY;
+    a.resZ = v->resZ;
+    a.rlim = v->rlim;
+    a.rad = T.rad;
+    a.nX = T.nX;
+    a.nZ = T.nZ;
+    a.nK = T.nK;
+    a.nA = 2ull * (unsigned long long)npts * T.nX * T.nZ;
+    a.nB = (unsigned long long)T.nX * T.nZ;
+    a.nC = 100ull * 90ull * (unsigned long long)(T.nK + 1);
+    if (a.nA + a.nB + a.nC >= 0xffffffffull) return set_err(c, EIK_ERR_ARG, "too many tunnel events");
+    for (int k = 0; k < 3; ++k) {
+        a.fw[k] = v->final_wp[k];
+        a.iw[k] = v->initial_wp[k];
+    }
+    // scratch: tables | first (u32) | closed (u8)
+    const size_t tb = sizeof(double) * T.buf.size();
+    const size_t need = tb + sizeof(unsigned) * nc + nc + 256;
+    HIPCHK(c, c->arm.ensure(need));
+    char* p = (char*)c->arm.p;
+    HIPCHK(c, hipMemcpyAsync(p, T.buf.data(), tb, hipMemcpyHostToDevice, st));
+    const double* d = (const double*)p;
+    a.toaA = d + T.oA;
+    a.toaB = d + T.oB;
+    a.toaC = d + T.oC;
+    a.tabI = d + T.oI;
+    a.tabK = d + T.oK;
+    a.norm = d + T.oN;
+    a.valA = d + T.oV;
+    a.ct = d + T.oct;
+    a.st = d + T.ost;
+    a.cs = d + T.ocs;
+    a.ss = d + T.oss;
+    a.ks = d + T.oks;
+    a.valC = d + T.ovc;
+    a.first = (unsigned*)(p + ((tb + 255) & ~(size_t)255));
+    a.closed = (unsigned char*)(a.first + nc);
+    a.tunnel = d_tunnel;
+    a.fmap = d_fmap;
+    a.out = d_cost;
+    HIPCHK(c, arm_tunnel(a, st));
+    // the tables must outlive the kernels: T.buf is host memory copied above; wait before return
+    HIPCHK(c, hipStreamSynchronize(st));
+    if (d_Z) {
+        unsigned bad = 0;
+        HIPCHK(c, hipMemcpy(&bad, c->misc.p, sizeof bad, hipMemcpyDeviceToHost));
+        if (bad) return set_err(c, EIK_ERR_ARG, "GetObstMap: a surface index below -sZ (the reference raises IndexError)");
+    }
+    return EIK_OK;
+}
+
+static int arm_check(eik_ctx* c, const eik_arm_volume* v) {
+    if (!v || v->sX < 1 || v->sY < 1 || v->sZ < 1 || !(v->resX > 0) || !(v->resY > 0) || !(v->resZ > 0))
+        return set_err(c, EIK_ERR_ARG, "bad arm volume");
+    if (v->sX != v->sY) return set_err(c, EIK_ERR_ARG, "arm volume must be square in x, y (sX %ld != sY %ld)",
+                                       (long)v->sX, (long)v->sY);
+    return EIK_OK;
+}
+
+extern "C" {
+
+int eik_arm_obst_map_f64(eik_ctx* c, const double* Z, const double* obst, int64_t m, int64_t n,
+                         const eik_arm_volume* v, double* fmap, double* omap, double* gmap) {
+    if (!c || !Z || !obst || !fmap || m < 1 || n < 1) return c ? set_err(c, EIK_ERR_ARG, "NULL argument") : EIK_ERR_ARG;
+    int rc = arm_check(c, v);
+    if (rc) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    const int64_t nc = v->sX * v->sY * v->sZ, nz = m * n;
+    HIPCHK(c, c->T2.ensure(sizeof(double) * (2 * nz + 3 * nc)));
+    double* dZ = (double*)c->T2.p;
+    double* dO = dZ + nz;
+    double* dF = dO + nz;
+    double* dOm = omap ? dF + nc : nullptr;
+    double* dGm = gmap ? dF + 2 * nc : nullptr;
+    HIPCHK(c, hipMemcpyAsync(dZ, Z, sizeof(double) * nz, hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(dO, obst, sizeof(double) * nz, hipMemcpyHostToDevice, st));
+    rc = arm_volume_dev(c, dZ, dO, m, n, nullptr, nullptr, 0, v, dF, dOm, dGm, nullptr, nullptr, st);
+    if (rc) return rc;
+    unsigned bad = 0;
+    HIPCHK(c, hipMemcpyAsync(&bad, c->misc.p, sizeof bad, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(fmap, dF, sizeof(double) * nc, hipMemcpyDeviceToHost, st));
+    if (omap) HIPCHK(c, hipMemcpyAsync(omap, dOm, sizeof(double) * nc, hipMemcpyDeviceToHost, st));
+    if (gmap) HIPCHK(c, hipMemcpyAsync(gmap, dGm, sizeof(double) * nc, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    if (bad) return set_err(c, EIK_ERR_ARG, "GetObstMap: a surface index below -sZ (the reference raises IndexError)");
+    return EIK_OK;
+}
+
+int eik_arm_tunnel_cost_f64(eik_ctx* c, const double* gamma2D, const double* heading, int64_t npts,
+                            const eik_arm_volume* v, double* Cmap) {
+    if (!c || !gamma2D || !heading || !Cmap || npts < 1) return c ? set_err(c, EIK_ERR_ARG, "NULL argument") : EIK_ERR_ARG;
+    int rc = arm_check(c, v);
+    if (rc) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t nc = v->sX * v->sY * v->sZ;
+    HIPCHK(c, c->T2.ensure(sizeof(double) * nc));
+    double* dT = (double*)c->T2.p;
+    rc = arm_volume_dev(c, nullptr, nullptr, 0, 0, gamma2D, heading, npts, v, nullptr, nullptr, nullptr, dT, nullptr,
+                        c->stream);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(Cmap, dT, sizeof(double) * nc, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return EIK_OK;
+}
+
+int eik_arm_path_f64(eik_ctx* c, const double* Z, const double* obst, int64_t m, int64_t n, const double* gamma2D,
+                     const double* heading, int64_t npts, const eik_arm_volume* v, double tau, double* path,
+                     int64_t cap, int64_t* n_out, int* status, double* cost_out, double* T_out) {
+    if (!c || !Z || !obst || !gamma2D || !heading || !path || !n_out || !status || npts < 1 || m < 1 || n < 1 ||
+        !(tau > 0) || cap < 2)
+        return c ? set_err(c, EIK_ERR_ARG, "bad arm-path arguments") : EIK_ERR_ARG;
+    int rc = arm_check(c, v);
+    if (rc) return rc;
+    for (int k = 0; k < 3; ++k) {
+        const int64_t lim = k == 0 ? v->sX : k == 1 ? v->sY : v->sZ;
+        if ((int64_t)v->final_wp[k] >= lim || (int64_t)v->initial_wp[k] >= lim)
+            return set_err(c, EIK_ERR_ARG, "waypoint outside the %ldx%ldx%ld volume", (long)v->sX, (long)v->sY,
+                           (long)v->sZ);
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    const int64_t nc = v->sX * v->sY * v->sZ, nz = m * n;
+    const int64_t steps = (int64_t)std::nearbyint(15000.0 / tau);
+    const int64_t pcap = std::min<int64_t>(cap, steps + 4);
+    // Z | obst | fmap | tunnel | cost | T | path | n_out | status
+    HIPCHK(c, c->T2.ensure(sizeof(double) * (2 * nz + 4 * nc + 3 * pcap) + 64));
+    double* dZ = (double*)c->T2.p;
+    double* dO = dZ + nz;
+    double* dF = dO + nz;
+    double* dTun = dF + nc;
+    double* dC = dTun + nc;
+    double* dT = dC + nc;
+    double* dP = dT + nc;
+    int64_t* dn = (int64_t*)(dP + 3 * pcap);
+    int* dst = (int*)(dn + 1);
+    HIPCHK(c, hipMemcpyAsync(dZ, Z, sizeof(double) * nz, hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(dO, obst, sizeof(double) * nz, hipMemcpyHostToDevice, st));
+    rc = arm_volume_dev(c, dZ, dO, m, n, gamma2D, heading, npts, v, dF, nullptr, nullptr, dTun, dC, st);
+    if (rc) return rc;
+    // FM3D.computeTmap(Cmap, finalWayPointArm, initialWayPointArm) :1585; H = sY rows, W = sX columns
+    const int64_t goal[3] = {v->final_wp[0], v->final_wp[1], v->final_wp[2]};
+    rc = eik_fim3d_solve(c, dC, dT, v->sY, v->sX, v->sZ, EIK_F64, goal, st);
+    if (rc) return rc;
+    // FM3D.getPathGDM(Tmap3D, initialWayPointArm, finalWayPointArm, 0.5) :1588
+    const double init[3] = {(double)v->initial_wp[0], (double)v->initial_wp[1], (double)v->initial_wp[2]};
+    const double end[3] = {(double)v->final_wp[0], (double)v->final_wp[1], (double)v->final_wp[2]};
+    rc = eik_path3d_dev(c, dT, EIK_F64, v->sY, v->sX, v->sZ, init, end, tau, dP, pcap, dn, dst, st);
+    if (rc) return rc;
+    int64_t hn = 0;
+    HIPCHK(c, hipMemcpyAsync(&hn, dn, sizeof hn, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(status, dst, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    *n_out = hn;
+    HIPCHK(c, hipMemcpyAsync(path, dP, sizeof(double) * 3 * hn, hipMemcpyDeviceToHost, st));
+    if (cost_out) HIPCHK(c, hipMemcpyAsync(cost_out, dC, sizeof(double) * nc, hipMemcpyDeviceToHost, st));
+    if (T_out) HIPCHK(c, hipMemcpyAsync(T_out, dT, sizeof(double) * nc, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    return EIK_OK;
+}
+
+int eik_tmap3d_batch_f64(eik_ctx* c, const double* cost, int64_t B, int64_t H, int64_t W, int64_t L,
+                         const int64_t* goals, double* T) {
+    if (!c || !cost || !T || !goals || B < 1 || H < 1 || W < 1 || L < 1)
+        return c ? set_err(c, EIK_ERR_ARG, "bad 3D batch arguments") : EIK_ERR_ARG;
+    for (int64_t b = 0; b < B; ++b)
+        if (goals[3 * b] < 0 || goals[3 * b + 1] < 0 || goals[3 * b + 2] < 0 || goals[3 * b] >= W ||
+            goals[3 * b + 1] >= H || goals[3 * b + 2] >= L)
+            return set_err(c, EIK_ERR_ARG, "goal of volume %ld outside %ldx%ldx%ld", (long)b, (long)H, (long)W, (long)L);
+    const int64_t n = B * H * W * L;
+    int rc = check_cost(c, cost, n);
+    if (rc) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, c->cost.ensure(sizeof(double) * n));
+    HIPCHK(c, c->T.ensure(sizeof(double) * n));
+    HIPCHK(c, hipMemcpyAsync(c->cost.p, cost, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    rc = fim3d_solve_batch(c, c->cost.p, c->T.p, B, H, W, L, EIK_F64, goals, c->stream);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(T, c->T.p, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     return EIK_OK;
 }
 

@@ -67,10 +67,12 @@ __global__ __launch_bounds__(256) void fim3d_sweep_kernel(Fim3dArgs a) {
 
     for (int it = blockIdx.x; it < cnt; it += gridDim.x) {
         const int tile = a.lists[(int64_t)cur * a.capacity + it];
-        const int bz = tile % a.ntz, bxy = tile / a.ntz, bx = bxy % a.ntx, by = bxy / a.ntx;
+        const int vol = tile / a.tpv, rem = tile - vol * a.tpv;  // batch: volume, tile in volume
+        const int bz = rem % a.ntz, bxy = rem / a.ntz, bx = bxy % a.ntx, by = bxy / a.ntx;
         const int64_t x0 = (int64_t)bx * TX, y0 = (int64_t)by * TY, z0 = (int64_t)bz * TZ;
-        const R* __restrict__ cost = static_cast<const R*>(a.cost);
-        R* __restrict__ T = static_cast<R*>(a.T);
+        const int64_t voff = (int64_t)vol * a.H * a.W * a.L;
+        const R* __restrict__ cost = static_cast<const R*>(a.cost) + voff;
+        R* __restrict__ T = static_cast<R*>(a.T) + voff;
         if (tid == 0) {
             s_flags = 0;
             s_changed[0] = 0;
@@ -155,7 +157,7 @@ __global__ __launch_bounds__(256) void fim3d_sweep_kernel(Fim3dArgs a) {
         __syncthreads();
         if (tid == 0) {
             const unsigned f = s_flags;
-            const int base = bxy * a.ntz;
+            const int base = vol * a.tpv + bxy * a.ntz;
             if (last) enqueue3(a, tile, nxt, stamp);
             if ((f & 1u) && bx > 0) enqueue3(a, tile - a.ntz, nxt, stamp);
             if ((f & 2u) && bx + 1 < a.ntx) enqueue3(a, tile + a.ntz, nxt, stamp);
@@ -177,27 +179,33 @@ __global__ void fim3d_init_kernel(R* __restrict__ T, int64_t n, unsigned* __rest
 }
 
 template <typename R>
-__global__ void fim3d_seed_kernel(Fim3dArgs a, int64_t gx, int64_t gy, int64_t gz) {
-    a.counts[1] = 0;
-    a.counts[2] = 0;
-    static_cast<R*>(a.T)[(gy * a.W + gx) * a.L + gz] = R(0);
-    const int tile = ((int)(gy / a.ty) * a.ntx + (int)(gx / a.tx)) * a.ntz + (int)(gz / a.tz);
+__global__ void fim3d_seed_kernel(Fim3dArgs a, const int64_t* __restrict__ goals, int B) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b == 0) {
+        a.counts[1] = 0;
+        a.counts[2] = 0;
+        a.counts[0] = B;
+    }
+    if (b >= B) return;
+    const int64_t gx = goals[3 * b], gy = goals[3 * b + 1], gz = goals[3 * b + 2];
+    static_cast<R*>(a.T)[(int64_t)b * a.H * a.W * a.L + (gy * a.W + gx) * a.L + gz] = R(0);
+    const int tile = b * a.tpv + ((int)(gy / a.ty) * a.ntx + (int)(gx / a.tx)) * a.ntz + (int)(gz / a.tz);
     a.mark[tile] = 1;
-    a.lists[0] = tile;
-    a.counts[0] = 1;
+    a.lists[b] = tile;
 }
 
-hipError_t fim3d_init(const Fim3dArgs& a, bool f64, int64_t gx, int64_t gy, int64_t gz, hipStream_t st) {
-    const int64_t n = a.H * a.W * a.L;
+hipError_t fim3d_init(const Fim3dArgs& a, bool f64, const int64_t* d_goals, int B, hipStream_t st) {
+    const int64_t n = (int64_t)B * a.H * a.W * a.L;
     const int grid = (int)std::min<int64_t>(4096, (n + 255) / 256);
+    const int sg = (B + 255) / 256;
     if (f64) {
         hipLaunchKernelGGL(fim3d_init_kernel<double>, dim3(grid), dim3(256), 0, st, static_cast<double*>(a.T), n,
                            a.mark, (int64_t)a.capacity);
-        hipLaunchKernelGGL(fim3d_seed_kernel<double>, dim3(1), dim3(1), 0, st, a, gx, gy, gz);
+        hipLaunchKernelGGL(fim3d_seed_kernel<double>, dim3(sg), dim3(256), 0, st, a, d_goals, B);
     } else {
         hipLaunchKernelGGL(fim3d_init_kernel<float>, dim3(grid), dim3(256), 0, st, static_cast<float*>(a.T), n,
                            a.mark, (int64_t)a.capacity);
-        hipLaunchKernelGGL(fim3d_seed_kernel<float>, dim3(1), dim3(1), 0, st, a, gx, gy, gz);
+        hipLaunchKernelGGL(fim3d_seed_kernel<float>, dim3(sg), dim3(256), 0, st, a, d_goals, B);
     }
     return hipGetLastError();
 }

@@ -38,6 +38,13 @@ class RoverQuery(C.Structure):
                 ("zp", C.c_double), ("tau", C.c_double)]
 
 
+class ArmVolume(C.Structure):
+    """eik_arm_volume (include/eikonal.h): the end-effector volume of main() step 3."""
+    _fields_ = [("sX", i64), ("sY", i64), ("sZ", i64), ("resX", C.c_double), ("resY", C.c_double),
+                ("resZ", C.c_double), ("xm", C.c_double), ("ym", C.c_double), ("rlim", C.c_double),
+                ("rO", C.c_double), ("rm", C.c_double), ("final_wp", C.c_uint32 * 3), ("initial_wp", C.c_uint32 * 3)]
+
+
 class EikStats(C.Structure):
     _fields_ = [("iterations", i64), ("tile_visits", i64), ("host_syncs", i64), ("solve_ms", C.c_double),
                 ("sweep_ms", C.c_double), ("bytes_alg", C.c_double), ("inplace_passes", i64)]
@@ -140,6 +147,11 @@ def lib():
                                          P(i64)]
         L.eik_rover_path_f64.argtypes = [vp, _f64p, i64, i64, P(RoverQuery), P(CostmapParams), _f64p, _f64p, i64,
                                          P(i64), _u32p, vp]
+        L.eik_arm_obst_map_f64.argtypes = [vp, _f64p, _f64p, i64, i64, P(ArmVolume), _f64p, vp, vp]
+        L.eik_arm_tunnel_cost_f64.argtypes = [vp, _f64p, _f64p, i64, P(ArmVolume), _f64p]
+        L.eik_arm_path_f64.argtypes = [vp, _f64p, _f64p, i64, i64, _f64p, _f64p, i64, P(ArmVolume), C.c_double, _f64p,
+                                       i64, P(i64), P(C.c_int), vp, vp]
+        L.eik_tmap3d_batch_f64.argtypes = [vp, _f64p, i64, i64, i64, i64, _i64p, _f64p]
         _lib = L
         return L
 
@@ -154,7 +166,8 @@ EXPORTED = [
     "eik_load_dem_txt", "eik_io_last_error", "eik_fim2d_live_bind", "eik_fim2d_launch", "eik_fim2d_live_pack",
     "eik_fim2d_live_merge", "eik_fim2d_release", "eik_node_allreduce", "eik_node_shm_open",
     "eik_node_shm_close", "eik_node_shm_unlink", "eik_ipc_alloc", "eik_ipc_free", "eik_ipc_open", "eik_ipc_close",
-    "eik_rover_assemble", "eik_rover_path_f64",
+    "eik_rover_assemble", "eik_rover_path_f64", "eik_arm_obst_map_f64", "eik_arm_tunnel_cost_f64",
+    "eik_arm_path_f64", "eik_tmap3d_batch_f64",
 ]
 
 
@@ -306,6 +319,54 @@ class Context:
                                            cost.ctypes.data if want_cost else None))
         res = (out[: n.value].copy(), hd[: n.value].copy(), join)
         return res + (cost,) if want_cost else res
+
+    def arm_obst_map(self, ZsMap, newObstMap, vol, all_maps=True):
+        """GetObstMap (Coupled_motion_planner.py:319-358) -> (finalMap, obstMap, groundMap)."""
+        Z = np.ascontiguousarray(ZsMap, dtype=np.float64)
+        O = np.ascontiguousarray(newObstMap, dtype=np.float64)
+        shape = (vol.sX, vol.sY, vol.sZ)
+        f = np.empty(shape)
+        o = np.empty(shape) if all_maps else None
+        g = np.empty(shape) if all_maps else None
+        self._chk(lib().eik_arm_obst_map_f64(self._h, Z, O, Z.shape[0], Z.shape[1], C.byref(vol), f,
+                                             o.ctypes.data if all_maps else None, g.ctypes.data if all_maps else None))
+        return f, o, g
+
+    def arm_tunnel_cost(self, gamma2D, heading, vol):
+        """TunnelCost (Coupled_motion_planner.py:505-725) -> Cmap (sY, sX, sZ)."""
+        g = np.ascontiguousarray(gamma2D, dtype=np.float64)
+        h = np.ascontiguousarray(heading, dtype=np.float64)
+        out = np.empty((vol.sY, vol.sX, vol.sZ))
+        self._chk(lib().eik_arm_tunnel_cost_f64(self._h, g, h, g.shape[0], C.byref(vol), out))
+        return out
+
+    def arm_path(self, ZsMap, newObstMap, gamma2D, heading, vol, tau=0.5, want_fields=False):
+        """:1562-1593: cost volume -> FM3D field -> end-effector path (K, 3) node coordinates."""
+        Z = np.ascontiguousarray(ZsMap, dtype=np.float64)
+        O = np.ascontiguousarray(newObstMap, dtype=np.float64)
+        g = np.ascontiguousarray(gamma2D, dtype=np.float64)
+        h = np.ascontiguousarray(heading, dtype=np.float64)
+        cap = int(round(15000 / tau)) + 4
+        out = np.empty((cap, 3))
+        n, st = i64(0), C.c_int(0)
+        shape = (vol.sY, vol.sX, vol.sZ)
+        cost = np.empty(shape) if want_fields else None
+        T = np.empty(shape) if want_fields else None
+        self._chk(lib().eik_arm_path_f64(self._h, Z, O, Z.shape[0], Z.shape[1], g, h, g.shape[0], C.byref(vol),
+                                         float(tau), out, cap, C.byref(n), C.byref(st),
+                                         cost.ctypes.data if want_fields else None,
+                                         T.ctypes.data if want_fields else None))
+        res = (out[: n.value].copy(), st.value)
+        return res + (cost, T) if want_fields else res
+
+    def tmap3d_batch(self, cost, goals):
+        """FastMarching3D.computeTmap on B volumes (B, H, W, L) in one solve; goals (B, 3) (x, y, z)."""
+        cost = np.ascontiguousarray(cost, dtype=np.float64)
+        B, H, W, Lz = cost.shape
+        g = np.ascontiguousarray(goals, np.int64).reshape(-1)
+        T = np.empty_like(cost)
+        self._chk(lib().eik_tmap3d_batch_f64(self._h, cost, B, H, W, Lz, g, T))
+        return T
 
     def surface_normal(self, Z, size):
         Z = np.ascontiguousarray(Z, dtype=np.float64)

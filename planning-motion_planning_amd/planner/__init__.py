@@ -44,3 +44,40 @@ def assemble(pathS, pathG, Zs, xm, ym, xr, yr, initialHeading, resolution, size=
     """The host tail alone (:1228-1252): the two GDM paths -> (roverPath, heading).  No GPU."""
     q = query(xm, ym, xr, yr, initialHeading, resolution, size, zp, tau)
     return L.rover_assemble(pathS, pathG, Zs, q)
+
+
+# ------------------------------------------------------------------ step 3: the end-effector volume
+def volume(sX, sY, sZ, resX, resY, resZ, xm=0.0, ym=0.0, rlim=0.527, rO=(0.4241 + 0.1105) / 2, rm=0.1105,
+           finalWayPointArm=(0, 0, 0), initialWayPointArm=(0, 0, 0)):
+    """eik_arm_volume from main()'s variables (:1121-1124, :1528-1534, :1573-1574)."""
+    v = L.ArmVolume()
+    v.sX, v.sY, v.sZ = int(sX), int(sY), int(sZ)
+    v.resX, v.resY, v.resZ = float(resX), float(resY), float(resZ)
+    v.xm, v.ym = float(xm), float(ym)
+    v.rlim, v.rO, v.rm = float(rlim), float(rO), float(rm)
+    for k in range(3):
+        v.final_wp[k] = int(finalWayPointArm[k])
+        v.initial_wp[k] = int(initialWayPointArm[k])
+    return v
+
+
+def GetObstMap(ZsMap, resX, resY, resZ, sX, sY, sZ, newObstMap, xm, ym):
+    """Drop-in of Coupled_motion_planner.py:319-358 -> (finalMap, obstMap, groundMap) on the GPU."""
+    v = volume(sX, sY, sZ, resX, resY, resZ, xm, ym)
+    return _ctx().arm_obst_map(np.asarray(ZsMap, np.float64), np.asarray(newObstMap, np.float64), v)
+
+
+def TunnelCost(rlim, rO, rm, gamma2D, sX, sY, sZ, resX, resY, resZ, finalBaseHeading, finalWayPointArm,
+               initialWayPointArm):
+    """Drop-in of Coupled_motion_planner.py:505-725 -> Cmap (sY, sX, sZ) on the GPU, bit-identical."""
+    v = volume(sX, sY, sZ, resX, resY, resZ, rlim=rlim, rO=rO, rm=rm, finalWayPointArm=finalWayPointArm,
+               initialWayPointArm=initialWayPointArm)
+    return _ctx().arm_tunnel_cost(np.asarray(gamma2D, np.float64), np.asarray(finalBaseHeading, np.float64), v)
+
+
+def arm_path(ZsMap, newObstMap, effectorBasePath, effectorBaseHeading, sX, sY, sZ, resX, resY, resZ, xm, ym,
+             finalWayPointArm, initialWayPointArm, Rlim=0.527, rO=(0.4241 + 0.1105) / 2, rm=0.1105, tau=TAU):
+    """main() :1562-1588 as one device pipeline: Cmap = GetObstMap * TunnelCost, FM3D.computeTmap from
+    the sample node, FM3D.getPathGDM from the start node -> (gamma3D node coordinates (K, 3), status)."""
+    v = volume(sX, sY, sZ, resX, resY, resZ, xm, ym, Rlim, rO, rm, finalWayPointArm, initialWayPointArm)
+    return _ctx().arm_path(ZsMap, newObstMap, effectorBasePath, effectorBaseHeading, v, tau)
