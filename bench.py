@@ -246,6 +246,7 @@ def main():
             "C5": bench_layers(ctx, dev, stream, cost, goal_g, args.extra_steps),
             "costmap": bench_costmap(ctx, dev, stream, args.extra_steps, goal_g),
             "C4_1gpu": bench_c4(ctx, dev, stream, max(2, args.extra_steps // 2)),
+            "arm": bench_arm(ctx, args.extra_steps),
         }
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -345,6 +346,54 @@ def bench_c4(ctx, dev, stream, steps, N=16384):
             "value": round(N * N / sec / 1e9, 4), "unit": "Gcells/s", "ms_per_step": round(sec * 1e3, 4),
             "steps": steps, "tile_visits_per_solve": st["tile_visits"], "inplace_passes_per_solve": st["inplace_passes"],
             "reached_fraction": round(reach, 4)}
+
+
+def bench_arm(ctx, steps, half=30, m=40, K=16, res=0.05):
+    """SURVEY.md §8(f) rank 3, main() step 3 (:1462-1593): the end-effector volume of a 2h x 2h area
+    (GetObstMap * TunnelCost, eik_arm_path_f64 also solving FM3D and the 3D path), and K candidate
+    fetch poses' volumes solved as ONE batched FM3D (eik_tmap3d_batch_f64) against K single solves."""
+    import math
+    sys.path.insert(0, os.path.join(ROOT, "planning-motion_planning_amd"))
+    import planner
+    rng = np.random.default_rng(5)
+    n = 2 * half
+    yy, xx = np.mgrid[0:n, 0:n] * res
+    Z = 0.1 * np.sin(2.1 * xx) * np.cos(0.9 * yy + 0.3) + 0.03 * rng.standard_normal((n, n))
+    Z -= Z.min()
+    resX = res * (2 * n - 1) / (2 * n)
+    sZ = int(round((Z.max() + 0.5) / 0.02))
+    obst = (rng.random((n, n)) < 0.1).astype(np.float64)
+    p0, p1 = np.array([0.2, 0.35]) * n * resX, np.array([0.6, 0.5]) * n * resX
+    t = np.linspace(0, 1, m)[:, None]
+    base = np.zeros((m, 3))
+    base[:, :2] = p0 + t * (p1 - p0)
+    base[:, 2] = 0.25
+    heading = np.stack([np.zeros(m), np.zeros(m), np.full(m, math.atan2(*(p1 - p0)[::-1]))], 1)
+    fw = np.uint32(np.round([(p1[0] + 0.2) / resX, (p1[1] + 0.15) / resX, (Z.max() * 0.6 + 0.1) / 0.02]))
+    iw = np.uint32(np.round([(p0[0] + 0.15) / resX, (p0[1] + 0.1) / resX, 0.45 / 0.02]))
+    vol = planner.volume(n, n, sZ, resX, resX, 0.02, 1.0, 2.0, 0.527, 0.2673, 0.1105, fw, iw)
+    sec_t = timed_loop(lambda: ctx.arm_tunnel_cost(base, heading, vol), steps)
+    out = {}
+
+    def full():
+        out["r"] = ctx.arm_path(Z, obst, base, heading, vol, 0.5, want_fields=True)
+
+    sec_p = timed_loop(full, steps)
+    path, st, cost, _ = out["r"]
+    # K candidate fetch poses: the sample node moved around the last base point
+    goals = []
+    for k in range(K):
+        a = 2 * math.pi * k / K
+        goals.append([int(fw[0]) + round(4 * math.cos(a)), int(fw[1]) + round(4 * math.sin(a)), int(fw[2])])
+    costs = np.repeat(cost[None], K, 0)
+    for k, g in enumerate(goals):
+        costs[k, g[1], g[0], g[2]] = 1.0  # finite at every candidate node
+    sec_b = timed_loop(lambda: ctx.tmap3d_batch(costs, goals), steps)
+    sec_s = timed_loop(lambda: [ctx.tmap3d(costs[k], goals[k]) for k in range(K)], max(1, steps // 2))
+    return {"workload": f"configs-adjacent: end-effector volume {n}x{n}x{sZ} ({m} base points), f64",
+            "ms_tunnel_cost": round(sec_t * 1e3, 3), "ms_volume_fm3d_path": round(sec_p * 1e3, 3),
+            "path_points": int(len(path)), "path_status": int(st),
+            f"ms_batch{K}_fm3d": round(sec_b * 1e3, 3), f"ms_{K}_single_fm3d": round(sec_s * 1e3, 3)}
 
 
 def bench_layers(ctx, dev, stream, cost2d, goal, steps, Lz=3):
