@@ -78,8 +78,11 @@ typedef enum {
                                 FIFO of tiles; EIK_MODE_LIST: one launch per outer iteration   */
     EIK_OPT_QTIMEOUT = 7,    /* persistent mode: seconds a workgroup may wait on the FIFO before
                                 the solve fails with EIK_ERR_HIP instead of hanging (default 30) */
-    EIK_OPT_MAX_VISITS = 8   /* persistent mode: tile visits after which a solve fails with
+    EIK_OPT_MAX_VISITS = 8,  /* persistent mode: tile visits after which a solve fails with
                                 EIK_ERR_NOCONVERGE (0: default 1024 x tiles + 2^20)            */
+    EIK_OPT_PASSES = 9       /* persistent mode: sweep passes a visit may run in place while its
+                                tile keeps changing before it is re-queued (0, the default:
+                                8 for a single map, 2 for a batch of maps)                     */
 } eik_option;
 
 typedef enum { EIK_MODE_LIST = 0, EIK_MODE_PERSISTENT = 1 } eik_mode;

@@ -35,6 +35,7 @@ struct Fim2dArgs {
     unsigned* qstate;      // per tile: kPending | kBusy
     unsigned long long qtimeout;  // spin limit, s_memrealtime ticks (100 MHz)
     unsigned long long qbudget;   // tile-visit cap (negative costs never converge)
+    int max_passes;        // in-place sweep passes per persistent visit (EIK_OPT_PASSES)
     // layered solver (fim2dl.hip): cell (y, x) holds ls consecutive values, layers z0.. solved
     int64_t ls;            // layer stride (1 for the 2D solver)
     int z0;                // first solved layer

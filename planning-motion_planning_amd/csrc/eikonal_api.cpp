@@ -61,6 +61,7 @@ struct eik_ctx {
     int mode = kModePersistent;  // EIK_OPT_MODE
     double qtimeout_s = 30.0;    // EIK_OPT_QTIMEOUT: persistent-mode spin limit
     unsigned long long max_visits = 0;  // EIK_OPT_MAX_VISITS (0: per-solver default)
+    int passes = 0;              // EIK_OPT_PASSES: in-place passes per persistent visit (0: adaptive)
     int timing = 0;
     int grid = 0;
     eik_stats last{};
@@ -178,6 +179,7 @@ int eik_set_option(eik_ctx* c, int opt, double v) {
             break;
         case EIK_OPT_QTIMEOUT: c->qtimeout_s = v > 0 ? v : 30.0; break;
         case EIK_OPT_MAX_VISITS: c->max_visits = v > 0 ? (unsigned long long)v : 0ull; break;
+        case EIK_OPT_PASSES: c->passes = std::max(0, std::min(64, (int)v)); break;
         default: return set_err(c, EIK_ERR_ARG, "unknown option %d", opt);
     }
     return EIK_OK;
@@ -294,6 +296,10 @@ int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
     const bool fits = f->H * f->W * (f->f64 ? 8 : 4) < (int64_t)UINT32_MAX;
     f->a.mode = (c->mode == kModePersistent && fits && !(c->delta > 0)) ? kModePersistent : kModeList;
     f->a.qtimeout = (unsigned long long)(c->qtimeout_s * 1e8);  // s_memrealtime: 100 MHz
+    // in-place passes: a single map's solve is front-latency-bound (long in-place refinement of
+    // the front tiles pays), a batch is throughput-bound (hand the workgroup to tiles with fresher
+    // halos early): C2 2.07-2.09 ms at 8-16 vs 2.23 at 2; C3 6.86 ms at 2 vs 8.0 at 8
+    f->a.max_passes = c->passes > 0 ? c->passes : f->B > 1 ? 2 : 8;
     f->a.qbudget = c->max_visits ? c->max_visits : 1024ull * (unsigned long long)(f->B * f->a.tiles_per_map) + (1ull << 20);
     f->iterations = 0;
     f->host_syncs = 0;
@@ -801,6 +807,7 @@ static int solve_layered(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, i
     a.edge_dirty = nullptr;
     for (auto& g : a.ghost) g = nullptr;
     a.qtimeout = (unsigned long long)(c->qtimeout_s * 1e8);
+    a.max_passes = c->passes > 0 ? c->passes : 8;
     a.qbudget = c->max_visits ? c->max_visits : 1024ull * (unsigned long long)a.tiles_per_map + (1ull << 20);
     if (c->resident_l[nl] == 0) c->resident_l[nl] = fim2dl_persist_resident(nl, c->cu_count);
     const int grid = std::min(c->grid > 0 ? c->grid : 4 * c->cu_count, c->resident_l[nl]);

@@ -210,11 +210,11 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
     __syncthreads();
     EIK_PROBE(1);
 
-    // PERSISTENT mode revisits a tile that changed IN PLACE, up to kPasses times: its interior
-    // is already in LDS and nobody else writes it while it is busy, so a pass only refreshes the
-    // halo ring, activates the neighbours its last write-back improved, and sweeps again -- no
-    // restaging, no queue round trip.  (List mode: one pass; a changed tile re-lists itself.)
-    constexpr int kPasses = COH ? 8 : 1;
+    // PERSISTENT mode revisits a tile that changed IN PLACE, up to a.max_passes times
+    // (EIK_OPT_PASSES; by default 8 for one map, 2 for a batch): its interior is already in LDS
+    // and nobody else writes it while it is busy, so a pass only refreshes the halo ring,
+    // activates the neighbours its last write-back improved, and sweeps again -- no restaging,
+    // no queue round trip.  (List mode: one pass; a changed tile re-lists itself.)
     for (int pass = 0;; ++pass) {
         // ---- sweep rounds (quadrant directions concurrently, one per wave; `dirs` selects them)
         const bool sweep = (L.dirs >> wave) & 1u;
@@ -283,7 +283,7 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
                     }
                 }
             }
-            if constexpr (kPasses > 1) {
+            if (COH) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) told[4 * k + e] = nv[e];  // what memory holds now
             }
@@ -298,9 +298,9 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
         if (tid == 0) L.last = a.max_rounds == 1 ? -1 : (int)last_changed;  // -1: see flags bit 7
         if constexpr (COH) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
         __syncthreads();
-        if constexpr (kPasses > 1) {
+        if (COH) {
             const unsigned f = L.flags;  // uniform
-            if (!(f & 128u) || pass + 1 >= kPasses || a.max_rounds != 1) break;
+            if (!(f & 128u) || pass + 1 >= a.max_passes || a.max_rounds != 1) break;
             if (tid == 0 && a.visits) atomicAdd(a.visits + 1, 1ull);  // in-place passes (stats)
             activate_neighbours(a, tile, f, L.key, 0, 0u);  // lanes 0..4 (T already drained)
             Ts[h] = load_halo();

@@ -177,7 +177,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
     }
     __syncthreads();
 
-    constexpr int kPasses = COH ? 8 : 1;
+    const int kPasses = COH ? a.max_passes : 1;
     for (int pass = 0;; ++pass) {
         if ((L.dirs >> wave) & 1u) {
             if (wave == 0)      sweep_layered<NL, +1, +1>(Ts, lane);

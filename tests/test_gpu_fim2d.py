@@ -168,3 +168,31 @@ def test_stats_count_visits(ctx):
     ctx.tmap2d(c, [256, 256], dtype=np.float32)
     s = ctx.stats()
     assert s["tile_visits"] >= 64 and s["iterations"] >= 1 and s["solve_ms"] > 0
+
+
+@pytest.mark.parametrize("passes", [1, 2, 16])
+def test_pass_cap_option(passes):
+    """EIK_OPT_PASSES (in-place passes per persistent visit) changes the schedule, not the field:
+    a single map and a batch against the oracle at caps other than the defaults (8 / 2)."""
+    import eikonal
+    from eikonal import _lib as L
+
+    c = eikonal.Context(0)
+    try:
+        c.set_option(L.OPT_PASSES, passes)
+        rng = np.random.default_rng(11)
+        cost = rng.uniform(1, 10, (700, 900))
+        cost[rng.random(cost.shape) < 0.12] = np.inf
+        cost = cost.astype(np.float32).astype(np.float64)
+        goal = [300, 350]
+        cost[goal[1], goal[0]] = 1.0
+        check_field(c.tmap2d(cost, goal, dtype=np.float32), oracle_field(cost, goal), goal, False)
+        costs = rng.uniform(1, 8, (4, 150, 210)).astype(np.float32)
+        goals = np.array([[20, 30], [200, 140], [100, 75], [5, 149]], np.int64)
+        for b in range(4):
+            costs[b, goals[b, 1], goals[b, 0]] = 1.0
+        T = c.tmap2d_batch(costs, goals)
+        for b in range(4):
+            check_field(T[b], oracle_field(costs[b], goals[b]), goals[b], False)
+    finally:
+        c.close()

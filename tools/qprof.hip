@@ -35,7 +35,7 @@ int main(int argc, char** argv) {
     a.qactive = (int*)(q + 128); a.qerror = (unsigned*)(q + 192); a.mode = kModePersistent;
     unsigned qn = 4096; while (qn < 8u * tiles) qn <<= 1;
     a.qmask = qn - 1; CK(hipMalloc(&a.qslot, 4ull * qn)); CK(hipMalloc(&a.qstate, 4ull * tiles));
-    a.qtimeout = 1000000000ull; a.qbudget = 1ull << 40;
+    a.qtimeout = 1000000000ull; a.qbudget = 1ull << 40; a.max_passes = 8;
     a.ls = 1; a.z0 = 0;
     int64_t* goals; CK(hipMalloc(&goals, 16)); int64_t hg[2] = {N / 2, N / 2}; CK(hipMemcpy(goals, hg, 16, hipMemcpyHostToDevice));
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
