@@ -365,30 +365,42 @@ hipError_t gdm2d(const Gdm2dArgs& a, bool f64, hipStream_t st) {
 // ---------------------------------------------------------------- 3D path (FM3D)
 // np.gradient(T) along `axis` (0 y, 1 x, 2 z) at (j, i, k): central differences / 2 inside,
 // one-sided at the ends (numpy's edge_order=1), no inf awareness (FastMarching3D.py:200).
-template <typename R>
-__device__ __forceinline__ double npgrad(const R* __restrict__ T, int64_t H, int64_t W, int64_t L, int axis,
-                                         int64_t j, int64_t i, int64_t k) {
-    const int64_t len = axis == 0 ? H : axis == 1 ? W : L;
-    const int64_t p = axis == 0 ? j : axis == 1 ? i : k;
-    const int64_t st = axis == 0 ? W * L : axis == 1 ? L : 1;
-    const R* c = T + (j * W + i) * L + k;
-    if (p == 0) return ((double)c[st] - (double)c[0]) / 1.0;
-    if (p == len - 1) return ((double)c[0] - (double)c[-st]) / 1.0;
-    return ((double)c[st] - (double)c[-st]) / 2.0;
-}
+// The 3D walk is one wave with every lane running the same scalar step (LDS reads are
+// broadcasts, so no lane divergence).  T is read from an LDS window [WY][WX][WZ] (z fastest, the
+// volume's own order) that is recentred and reloaded by all 64 lanes when the 4x4x4 cube a step
+// needs (trilinear corners +-1 for np.gradient) leaves it; the integer-descent fallback reads
+// outside the window from global memory.  The last kRing path points are mirrored in LDS, so the
+// back-tracking of :231-249 does not wait on its own global stores.  The arithmetic, its order
+// and every branch are FastMarching3D.py's (bit-identical to the oracle's restatement).
+constexpr int kWin3Bytes = 48 * 1024;
+constexpr int kRing = 256;
 
-// FastMarching3D.interpolatePoint :275-314, interior branch (a7 coefficient as written, :290)
 template <typename R>
-__device__ double interp3(const R* __restrict__ T, int64_t H, int64_t W, int64_t L, int axis, double px, double py,
-                          double pz, bool& oob) {
-    const uint32_t i = (uint32_t)__builtin_trunc(px), j = (uint32_t)__builtin_trunc(py), k = (uint32_t)__builtin_trunc(pz);
-    oob = i + 1 >= (uint64_t)W || j + 1 >= (uint64_t)H || k + 1 >= (uint64_t)L;
-    if (oob) return 0.0;
-    const double a = px - i, b = py - j, c = pz - k;
-    const double m000 = npgrad(T, H, W, L, axis, j, i, k), m010 = npgrad(T, H, W, L, axis, j, i + 1, k);
-    const double m100 = npgrad(T, H, W, L, axis, j + 1, i, k), m001 = npgrad(T, H, W, L, axis, j, i, k + 1);
-    const double m110 = npgrad(T, H, W, L, axis, j + 1, i + 1, k), m011 = npgrad(T, H, W, L, axis, j, i + 1, k + 1);
-    const double m101 = npgrad(T, H, W, L, axis, j + 1, i, k + 1), m111 = npgrad(T, H, W, L, axis, j + 1, i + 1, k + 1);
+struct Win3 {
+    const R* __restrict__ T;
+    int64_t H, W, L;
+    const R* w;           // LDS window
+    int64_t y0, x0, z0;   // window origin
+    int WY, WX, WZ;
+    __device__ __forceinline__ bool inside(int64_t y, int64_t x, int64_t z) const {
+        return (uint64_t)(y - y0) < (uint64_t)WY && (uint64_t)(x - x0) < (uint64_t)WX && (uint64_t)(z - z0) < (uint64_t)WZ;
+    }
+    // T[y, x, z] (in range), from the window when it holds the cell
+    __device__ __forceinline__ double at(int64_t y, int64_t x, int64_t z) const {
+        if (inside(y, x, z)) return (double)w[((y - y0) * WX + (x - x0)) * WZ + (z - z0)];
+        return (double)T[(y * W + x) * L + z];
+    }
+    // window-only read (the step's cube is always inside the window)
+    __device__ __forceinline__ double atw(int64_t y, int64_t x, int64_t z) const {
+        return (double)w[((int)(y - y0) * WX + (int)(x - x0)) * WZ + (int)(z - z0)];
+    }
+};
+
+// FastMarching3D.interpolatePoint :275-314, interior branch (a7 coefficient as written, :290), on
+// the eight corner values m[4 dj + 2 di + dk] = m{dj}{di}{dk}
+__device__ __forceinline__ double tri3(const double* m, double a, double b, double c) {
+    const double m000 = m[0], m001 = m[1], m010 = m[2], m011 = m[3];
+    const double m100 = m[4], m101 = m[5], m110 = m[6], m111 = m[7];
     const double a0 = m000;
     const double a1 = m010 - m000;
     const double a2 = m100 - m000;
@@ -402,91 +414,196 @@ __device__ double interp3(const R* __restrict__ T, int64_t H, int64_t W, int64_t
 
 __device__ __forceinline__ double norm3(double a, double b, double c) { return __builtin_sqrt(a * a + b * b + c * c); }
 
+// The walk is ONE wave: its LDS accesses complete in issue order, so lanes exchange values through
+// LDS with only a compiler fence (and an LDS-count wait) -- a workgroup barrier would also wait
+// for the path's global stores.
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// window origin along one axis: the needed span [lo, hi] (clipped to the volume) centred in a
+// window of n cells that stays inside [0, len)
+__device__ __forceinline__ int64_t win_origin(int64_t lo, int64_t hi, int n, int64_t len) {
+    int64_t o = (lo + hi + 1) / 2 - n / 2;
+    if (o + n > len) o = len - n;
+    return o < 0 ? 0 : o;
+}
+
 template <typename R>
 __global__ __launch_bounds__(64) void gdm3d_kernel(Gdm3dArgs a) {
-    if (threadIdx.x != 0) return;
-    const R* __restrict__ T = static_cast<const R*>(a.T);
+    __shared__ __attribute__((aligned(16))) char wbuf[kWin3Bytes];
+    __shared__ double ring[kRing][3];
+    __shared__ double gsh[3][8], nsh[6];
+    __shared__ int nbad[6];
+    const int lane = threadIdx.x;
+    const bool lead = lane == 0;
+    Win3<R> v;
+    v.T = static_cast<const R*>(a.T);
+    v.H = a.H; v.W = a.W; v.L = a.L;
+    v.w = reinterpret_cast<const R*>(wbuf);
+    R* const wl = reinterpret_cast<R*>(wbuf);
+    {
+        constexpr int cells = kWin3Bytes / (int)sizeof(R);
+        v.WZ = (int)(a.L < 16 ? a.L : 16);
+        int s = 1;
+        while ((s + 1) * (s + 1) * v.WZ <= cells && s < 128) ++s;
+        v.WY = (int)(a.H < s ? a.H : s);
+        v.WX = (int)(a.W < s ? a.W : s);
+    }
+    v.y0 = v.x0 = v.z0 = -((int64_t)1 << 40);  // empty: the first step loads
     const int64_t H = a.H, W = a.W, L = a.L;
     double* out = a.out;
-    int64_t n = 1;
+    // path point q: the LDS ring while it holds it (the last kRing points), else global memory
+    auto pt = [&](int64_t q, int c) -> double { return ring[q % kRing][c]; };
+    auto put = [&](int64_t q, double x, double y, double z) {
+        out[3 * q] = x;  // every lane: same address and value (each lane reads back its own
+        out[3 * q + 1] = y;  // stores when back-tracking below the ring)
+        out[3 * q + 2] = z;
+        ring[q % kRing][0] = x;
+        ring[q % kRing][1] = y;
+        ring[q % kRing][2] = z;
+    };
+    int64_t n = 0, lo = 0;  // ring holds points [lo, n); below lo: global
+    auto point = [&](int64_t q, int c) -> double { return q >= lo ? pt(q, c) : out[3 * q + c]; };
+    put(0, a.init[0], a.init[1], a.init[2]);
+    n = 1;
     int status = kGdmDone;
-    out[0] = a.init[0];
-    out[1] = a.init[1];
-    out[2] = a.init[2];
     const double tau = a.tau;
     const int off[6][3] = {{0, -1, 0}, {0, 1, 0}, {-1, 0, 0}, {1, 0, 0}, {0, 0, -1}, {0, 0, 1}};
+    double gx = a.init[0], gy = a.init[1], gz = a.init[2];  // the last point, out[n - 1]
+    double ustep[6][3];  // (-off) / tau of the integer-descent moves (:244-252), divided once
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+        for (int c = 0; c < 3; ++c) ustep[q][c] = (double)(-off[q][c]) / tau;
     for (long k = 0; k < a.steps; ++k) {
-        const double* g = out + 3 * (n - 1);
-        bool o1, o2, o3;
-        double dx = interp3<R>(T, H, W, L, 1, g[0], g[1], g[2], o1);
-        double dy = interp3<R>(T, H, W, L, 0, g[0], g[1], g[2], o2);
-        double dz = interp3<R>(T, H, W, L, 2, g[0], g[1], g[2], o3);
-        if (o1 || o2 || o3) { status = kGdmError; break; }
+        const uint32_t i = (uint32_t)__builtin_trunc(gx), j = (uint32_t)__builtin_trunc(gy), kk = (uint32_t)__builtin_trunc(gz);
+        if (i + 1 >= (uint64_t)W || j + 1 >= (uint64_t)H || kk + 1 >= (uint64_t)L) { status = kGdmError; break; }
+        {  // the step's 4x4x4 cube (clipped to the volume) must be in the window
+            const int64_t ylo = j > 0 ? j - 1 : 0, yhi = j + 2 < H ? j + 2 : H - 1;
+            const int64_t xlo = i > 0 ? i - 1 : 0, xhi = i + 2 < W ? i + 2 : W - 1;
+            const int64_t zlo = kk > 0 ? kk - 1 : 0, zhi = kk + 2 < L ? kk + 2 : L - 1;
+            if (!v.inside(ylo, xlo, zlo) || !v.inside(yhi, xhi, zhi)) {
+                v.y0 = win_origin(ylo, yhi, v.WY, H);
+                v.x0 = win_origin(xlo, xhi, v.WX, W);
+                v.z0 = win_origin(zlo, zhi, v.WZ, L);
+                __syncthreads();  // every lane's reads of the old window are done
+                // lane c, c + 64, ...: (yy, xx, zz) advanced by carries, no divisions; 32 loads in
+                // flight per lane before their LDS stores
+                const int nc = v.WY * v.WX * v.WZ;
+                const int sz = 64 % v.WZ, sx = (64 / v.WZ) % v.WX, sy = (64 / v.WZ) / v.WX;
+                int zz = lane % v.WZ, xx = (lane / v.WZ) % v.WX, yy = (lane / v.WZ) / v.WX;
+                constexpr int kB = 32;
+                for (int c0 = lane; c0 < nc; c0 += 64 * kB) {
+                    R val[kB];
+#pragma unroll
+                    for (int u = 0; u < kB; ++u) {
+                        if (c0 + 64 * u < nc) val[u] = v.T[((v.y0 + yy) * W + v.x0 + xx) * L + v.z0 + zz];
+                        zz += sz;
+                        if (zz >= v.WZ) { zz -= v.WZ; ++xx; }
+                        xx += sx;
+                        if (xx >= v.WX) { xx -= v.WX; ++yy; }
+                        yy += sy;
+                    }
+#pragma unroll
+                    for (int u = 0; u < kB; ++u)
+                        if (c0 + 64 * u < nc) wl[c0 + 64 * u] = val[u];
+                }
+                __syncthreads();
+            }
+        }
+        // the 24 np.gradient samples (3 axes x 8 trilinear corners), one per lane, then every
+        // lane combines them (broadcast LDS reads)
+        if (lane < 24) {
+            const int axis = lane >> 3, cj = (lane >> 2) & 1, ci = (lane >> 1) & 1, ck = lane & 1;
+            const int64_t y = j + cj, x = i + ci, z = kk + ck;
+            const int64_t len = axis == 0 ? H : axis == 1 ? W : L;
+            const int64_t p = axis == 0 ? y : axis == 1 ? x : z;
+            const bool first = p == 0, last = !first && p == len - 1;
+            const int64_t dlo = first ? 0 : 1, dhi = last ? 0 : 1;
+            const double t_hi = v.atw(y + (axis == 0) * dhi, x + (axis == 1) * dhi, z + (axis == 2) * dhi);
+            const double t_lo = v.atw(y - (axis == 0) * dlo, x - (axis == 1) * dlo, z - (axis == 2) * dlo);
+            // (/ 1.0 at the ends, / 2.0 inside: both exact, as multiplications)
+            gsh[axis][lane & 7] = (t_hi - t_lo) * (first || last ? 1.0 : 0.5);
+        }
+        wave_lds_sync();
+        double dx = tri3(gsh[1], gx - i, gy - j, gz - kk);
+        double dy = tri3(gsh[0], gx - i, gy - j, gz - kk);
+        double dz = tri3(gsh[2], gx - i, gy - j, gz - kk);
         if (__builtin_isnan(dx) || __builtin_isnan(dy) || __builtin_isnan(dz)) {  // :212-253
-            int64_t nx = (int64_t)__builtin_rint(g[0]), ny = (int64_t)__builtin_rint(g[1]), nz = (int64_t)__builtin_rint(g[2]);
+            int64_t nx = (int64_t)__builtin_rint(gx), ny = (int64_t)__builtin_rint(gy), nz = (int64_t)__builtin_rint(gz);
             bool err = false;
             for (;;) {
                 if (nx < 0 || ny < 0 || nz < 0 || nx >= W || ny >= H || nz >= L) { err = true; break; }
-                if (!__builtin_isinf((double)T[(ny * W + nx) * L + nz])) break;
+                if (!__builtin_isinf(v.at(ny, nx, nz))) break;
                 --n;
                 if (n == 0) { err = true; break; }
-                const double* q = out + 3 * (n - 1);
-                nx = (int64_t)__builtin_rint(q[0]);
-                ny = (int64_t)__builtin_rint(q[1]);
-                nz = (int64_t)__builtin_rint(q[2]);
+                nx = (int64_t)__builtin_rint(point(n - 1, 0));
+                ny = (int64_t)__builtin_rint(point(n - 1, 1));
+                nz = (int64_t)__builtin_rint(point(n - 1, 2));
             }
             if (err) { status = kGdmError; break; }
-            while (n > 0 && norm3(out[3 * (n - 1)] - nx, out[3 * (n - 1) + 1] - ny, out[3 * (n - 1) + 2] - nz) < 1) --n;
+            while (n > 0 && norm3(point(n - 1, 0) - nx, point(n - 1, 1) - ny, point(n - 1, 2) - nz) < 1) --n;
             if (n >= a.cap) { status = kGdmError; break; }
-            out[3 * n] = (double)nx;
-            out[3 * n + 1] = (double)ny;
-            out[3 * n + 2] = (double)nz;
+            if (n < lo) lo = n;
+            put(n, (double)nx, (double)ny, (double)nz);
             ++n;
-            double curT = (double)T[(ny * W + nx) * L + nz];
-            for (int q = 0; q < 6; ++q) {
-                int64_t cx = nx + off[q][0], cy = ny + off[q][1], cz = nz + off[q][2];
+            // the six neighbours' T in parallel (lanes 0..5), then the reference's ordered scan
+            if (lane < 6) {
+                int64_t cx = nx + off[lane][0], cy = ny + off[lane][1], cz = nz + off[lane][2];
                 if (cx < 0) cx += W;  // python negative indices wrap
                 if (cy < 0) cy += H;
                 if (cz < 0) cz += L;
-                if (cx >= W || cy >= H || cz >= L) { err = true; break; }
-                const double tc = (double)T[(cy * W + cx) * L + cz];
+                const bool bad = cx >= W || cy >= H || cz >= L;
+                nsh[lane] = bad ? __builtin_nan("") : v.at(cy, cx, cz);
+                nbad[lane] = bad;
+            }
+            wave_lds_sync();
+            double curT = v.at(ny, nx, nz);
+            for (int q = 0; q < 6; ++q) {
+                if (nbad[q]) { err = true; break; }
+                const double tc = nsh[q];
                 if (tc < curT) {
                     curT = tc;
-                    dx = (double)(-off[q][0]) / tau;
-                    dy = (double)(-off[q][1]) / tau;
-                    dz = (double)(-off[q][2]) / tau;
+                    dx = ustep[q][0];
+                    dy = ustep[q][1];
+                    dz = ustep[q][2];
                 }
             }
+            wave_lds_sync();  // nsh / nbad are rewritten by the next step
             if (err) { status = kGdmError; break; }
+            gx = (double)nx;
+            gy = (double)ny;
+            gz = (double)nz;
         }
-        g = out + 3 * (n - 1);
         const double nrm = __builtin_sqrt(dx * dx + dy * dy + dz * dz);  // :255
         double ax, ay, az;
         if (nrm < 0.01) {
-            ax = g[0] - tau * (dx / nrm);
-            ay = g[1] - tau * (dy / nrm);
-            az = g[2] - tau * (dz / nrm);
+            ax = gx - tau * (dx / nrm);
+            ay = gy - tau * (dy / nrm);
+            az = gz - tau * (dz / nrm);
         } else {  // unnormalised step (:262-264)
-            ax = g[0] - tau * dx;
-            ay = g[1] - tau * dy;
-            az = g[2] - tau * dz;
+            ax = gx - tau * dx;
+            ay = gy - tau * dy;
+            az = gz - tau * dz;
         }
         if (n >= a.cap) { status = kGdmError; break; }
-        out[3 * n] = ax;
-        out[3 * n + 1] = ay;
-        out[3 * n + 2] = az;
+        put(n, ax, ay, az);
         ++n;
+        if (n - lo > kRing) lo = n - kRing;
+        gx = ax;
+        gy = ay;
+        gz = az;
         if (__builtin_isnan(ax) || __builtin_isnan(ay) || __builtin_isnan(az)) { status = kGdmError; break; }
         if (norm3(ax - a.end[0], ay - a.end[1], az - a.end[2]) < 1.5) break;  // :266-267
     }
-    if (status == kGdmDone && n < a.cap) {  // :269
-        out[3 * n] = a.end[0];
-        out[3 * n + 1] = a.end[1];
-        out[3 * n + 2] = a.end[2];
-        ++n;
+    if (lead) {
+        if (status == kGdmDone && n < a.cap) {  // :269
+            out[3 * n] = a.end[0];
+            out[3 * n + 1] = a.end[1];
+            out[3 * n + 2] = a.end[2];
+            ++n;
+        }
+        *a.n_out = n;
+        *a.status = status;
     }
-    *a.n_out = n;
-    *a.status = status;
 }
 
 hipError_t gdm3d(const Gdm3dArgs& a, bool f64, hipStream_t st) {

@@ -135,3 +135,32 @@ def test_layered_device_entry(ctx):
     finally:
         O.set_strict(True)
     check(T, R, False)
+
+
+@pytest.mark.parametrize("shape,seed,pad", [((300, 280, 3), 5, True), ((70, 90, 40), 6, False), ((20, 23, 70), 7, False)])
+def test_path3d_windowed(ctx, shape, seed, pad):
+    """Walks longer than the path kernel's LDS window (recentred reloads, back-tracking through
+    the point ring): layered z-padded volumes (integer descent), cubes with trilinear steps and a
+    volume taller in z than the window; the same field through the oracle's walk, <= 1e-9."""
+    rng = np.random.default_rng(seed)
+    c = rng.uniform(1, 3, shape)
+    if pad:  # cubes stay obstacle-free: their walk takes trilinear steps all the way
+        c[rng.random(shape) < 0.05] = np.inf
+        inf = np.full(shape[:2] + (1,), np.inf)
+        c = np.concatenate([inf, c, inf], axis=2)
+    H, W, L = c.shape
+    z = 1 if pad else L // 2
+    goal = np.array([W - 6, H - 5, z])
+    start = np.array([4.0, 5.0, float(z if pad else 2)])
+    c[goal[1], goal[0], goal[2]] = 1.0
+    c[5, 4, int(start[2])] = 1.0
+    O.set_strict(False)
+    try:
+        T = O.fmm3d(c, goal, None)
+    finally:
+        O.set_strict(True)
+    ref, rst = O.gdm3d(T, start, goal.astype(float), 0.5)
+    path, st = ctx.path3d(T, start, goal.astype(float))
+    assert st == rst and path.shape == ref.shape, (st, rst, path.shape, ref.shape)
+    assert np.abs(path - ref).max() <= 1e-9
+    assert len(path) > 40
