@@ -215,9 +215,12 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
     // and nobody else writes it while it is busy, so a pass only refreshes the halo ring,
     // activates the neighbours its last write-back improved, and sweeps again -- no restaging,
     // no queue round trip.  (List mode: one pass; a changed tile re-lists itself.)
+    // quadrant sweeps of this pass (bit w: wave w), in a register: the caller's L.dirs for the
+    // first pass, then set by the in-place branch below
+    unsigned dirs = L.dirs;
     for (int pass = 0;; ++pass) {
         // ---- sweep rounds (quadrant directions concurrently, one per wave; `dirs` selects them)
-        const bool sweep = (L.dirs >> wave) & 1u;
+        const bool sweep = (dirs >> wave) & 1u;
         bool last_changed = false;
         if (a.max_rounds == 1) {  // single round: "changed" is read off the write-back below
             if (sweep) {
@@ -303,12 +306,10 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
             if (!(f & 128u) || pass + 1 >= a.max_passes || a.max_rounds != 1) break;
             if (tid == 0 && a.visits) atomicAdd(a.visits + 1, 1ull);  // in-place passes (stats)
             activate_neighbours(a, tile, f, L.key, 0, 0u);  // lanes 0..4 (T already drained)
+            dirs = 0xFu;  // a self revisit: every direction
             Ts[h] = load_halo();
             __syncthreads();  // every wave has read L.flags and its halo side is in
-            if (tid == 0) {
-                L.flags = 0;
-                L.dirs = 0xFu;  // a self revisit: every direction
-            }
+            if (tid == 0) L.flags = 0;  // next OR-ed after the next sweep barrier
         } else {
             break;
         }

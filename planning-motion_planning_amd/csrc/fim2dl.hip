@@ -178,8 +178,9 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
     __syncthreads();
 
     const int kPasses = COH ? a.max_passes : 1;
+    unsigned dirs = L.dirs;  // this pass's sweeps (register: see fim2d.hip process_tile)
     for (int pass = 0;; ++pass) {
-        if ((L.dirs >> wave) & 1u) {
+        if ((dirs >> wave) & 1u) {
             if (wave == 0)      sweep_layered<NL, +1, +1>(Ts, lane);
             else if (wave == 1) sweep_layered<NL, -1, +1>(Ts, lane);
             else if (wave == 2) sweep_layered<NL, +1, -1>(Ts, lane);
@@ -217,12 +218,10 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
         if (!(f & 128u) || pass + 1 >= kPasses) break;
         if (tid == 0 && a.visits) atomicAdd(a.visits + 1, 1ull);  // in-place passes (stats)
         activate_neighbours(a, tile, f, L.key, 0, 0u);             // lanes 0..4 (T already drained)
+        dirs = 0xFu;  // a self revisit: every direction
         Ts[h] = load_halo();
         __syncthreads();  // every wave has read L.flags and its halo side is in
-        if (tid == 0) {
-            L.flags = 0;
-            L.dirs = 0xFu;  // a self revisit: every direction
-        }
+        if (tid == 0) L.flags = 0;
     }
 }
 
