@@ -993,7 +993,8 @@ int eik_tmap3d_f64(eik_ctx* c, const double* cost, int64_t H, int64_t W, int64_t
 int eik_path3d_dev(eik_ctx* c, const void* d_T, int dtype, int64_t H, int64_t W, int64_t L, const double init[3],
                    const double end[3], double tau, double* d_out, int64_t cap, int64_t* d_n_out, int* d_status,
                    void* stream) {
-    if (!c || !d_T || !init || !end || !d_out || !d_n_out || !d_status || cap < 2 || !(tau > 0))
+    if (!c || !d_T || !init || !end || !d_out || !d_n_out || !d_status || cap < 2 || !(tau > 0) || H < 1 || W < 1 ||
+        L < 1)
         return c ? set_err(c, EIK_ERR_ARG, "bad 3D path arguments") : EIK_ERR_ARG;
     Gdm3dArgs a;
     a.T = d_T;
