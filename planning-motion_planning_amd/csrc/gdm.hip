@@ -431,8 +431,8 @@ template <typename R>
 __global__ __launch_bounds__(64) void gdm3d_kernel(Gdm3dArgs a) {
     __shared__ __attribute__((aligned(16))) char wbuf[kWin3Bytes];
     __shared__ double ring[kRing][3];
-    __shared__ double gsh[3][8], nsh[6];
-    __shared__ int nbad[6];
+    __shared__ double gsh[3][8], nsh[7], psh[6];  // per-step lane exchange (see below)
+    __shared__ int nbad[7];
     const int lane = threadIdx.x;
     const bool lead = lane == 0;
     Win3<R> v;
@@ -509,8 +509,33 @@ __global__ __launch_bounds__(64) void gdm3d_kernel(Gdm3dArgs a) {
                 __syncthreads();
             }
         }
-        // the 24 np.gradient samples (3 axes x 8 trilinear corners), one per lane, then every
-        // lane combines them (broadcast LDS reads)
+        // ONE LDS exchange per step: lanes 0..23 take the 24 np.gradient samples (3 axes x 8
+        // trilinear corners); lanes 24..30 the T of the integer-descent node rint(point) and of its
+        // six neighbours in the reference's order (used when the gradient is NaN and the node
+        // needs no back-tracking); lanes 32..37 the last two path points (the pop test :238-240)
+        const int64_t rx = (int64_t)__builtin_rint(gx), ry = (int64_t)__builtin_rint(gy), rz = (int64_t)__builtin_rint(gz);
+        const bool rin = rx >= 0 && ry >= 0 && rz >= 0 && rx < W && ry < H && rz < L;
+        if (lane >= 24 && lane < 31) {
+            if (rin) {
+                const int q = lane - 25;  // -1: the node; 0..5: y-1, y+1, x-1, x+1, z-1, z+1 (:244-252)
+                int64_t cx = rx, cy = ry, cz = rz;
+                if (q >= 0) {
+                    const int64_t sg = (q & 1) ? 1 : -1;
+                    cy += (q >> 1) == 0 ? sg : 0;
+                    cx += (q >> 1) == 1 ? sg : 0;
+                    cz += (q >> 1) == 2 ? sg : 0;
+                }
+                if (cx < 0) cx += W;  // python negative indices wrap
+                if (cy < 0) cy += H;
+                if (cz < 0) cz += L;
+                const bool bad = cx >= W || cy >= H || cz >= L;
+                nsh[lane - 24] = bad ? __builtin_nan("") : v.at(cy, cx, cz);
+                nbad[lane - 24] = bad;
+            }
+        } else if (lane >= 32 && lane < 38) {
+            const int64_t q = n - 1 - (lane - 32) / 3;
+            psh[lane - 32] = q >= 0 ? point(q, (lane - 32) % 3) : 0.0;
+        }
         if (lane < 24) {
             const int axis = lane >> 3, cj = (lane >> 2) & 1, ci = (lane >> 1) & 1, ck = lane & 1;
             const int64_t y = j + cj, x = i + ci, z = kk + ck;
@@ -528,38 +553,52 @@ __global__ __launch_bounds__(64) void gdm3d_kernel(Gdm3dArgs a) {
         double dy = tri3(gsh[0], gx - i, gy - j, gz - kk);
         double dz = tri3(gsh[2], gx - i, gy - j, gz - kk);
         if (__builtin_isnan(dx) || __builtin_isnan(dy) || __builtin_isnan(dz)) {  // :212-253
-            int64_t nx = (int64_t)__builtin_rint(gx), ny = (int64_t)__builtin_rint(gy), nz = (int64_t)__builtin_rint(gz);
+            int64_t nx = rx, ny = ry, nz = rz;
             bool err = false;
-            for (;;) {
-                if (nx < 0 || ny < 0 || nz < 0 || nx >= W || ny >= H || nz >= L) { err = true; break; }
-                if (!__builtin_isinf(v.at(ny, nx, nz))) break;
-                --n;
-                if (n == 0) { err = true; break; }
-                nx = (int64_t)__builtin_rint(point(n - 1, 0));
-                ny = (int64_t)__builtin_rint(point(n - 1, 1));
-                nz = (int64_t)__builtin_rint(point(n - 1, 2));
+            // fast: the node is in range and reached -- no back-tracking, the gathered values apply
+            const bool fast = rin && !__builtin_isinf(nsh[0]);
+            if (!fast) {
+                for (;;) {
+                    if (nx < 0 || ny < 0 || nz < 0 || nx >= W || ny >= H || nz >= L) { err = true; break; }
+                    if (!__builtin_isinf(v.at(ny, nx, nz))) break;
+                    --n;
+                    if (n == 0) { err = true; break; }
+                    nx = (int64_t)__builtin_rint(point(n - 1, 0));
+                    ny = (int64_t)__builtin_rint(point(n - 1, 1));
+                    nz = (int64_t)__builtin_rint(point(n - 1, 2));
+                }
+                if (err) { status = kGdmError; break; }
             }
-            if (err) { status = kGdmError; break; }
-            while (n > 0 && norm3(point(n - 1, 0) - nx, point(n - 1, 1) - ny, point(n - 1, 2) - nz) < 1) --n;
+            bool deep = !fast;  // pops beyond the two gathered points read the ring
+            if (fast && n > 0 && norm3(psh[0] - nx, psh[1] - ny, psh[2] - nz) < 1) {
+                --n;
+                if (n > 0 && norm3(psh[3] - nx, psh[4] - ny, psh[5] - nz) < 1) {
+                    --n;
+                    deep = true;
+                }
+            }
+            if (deep)
+                while (n > 0 && norm3(point(n - 1, 0) - nx, point(n - 1, 1) - ny, point(n - 1, 2) - nz) < 1) --n;
             if (n >= a.cap) { status = kGdmError; break; }
             if (n < lo) lo = n;
             put(n, (double)nx, (double)ny, (double)nz);
             ++n;
-            // the six neighbours' T in parallel (lanes 0..5), then the reference's ordered scan
-            if (lane < 6) {
-                int64_t cx = nx + off[lane][0], cy = ny + off[lane][1], cz = nz + off[lane][2];
-                if (cx < 0) cx += W;  // python negative indices wrap
-                if (cy < 0) cy += H;
-                if (cz < 0) cz += L;
-                const bool bad = cx >= W || cy >= H || cz >= L;
-                nsh[lane] = bad ? __builtin_nan("") : v.at(cy, cx, cz);
-                nbad[lane] = bad;
+            if (!fast) {  // the six neighbours of a back-tracked node, in parallel (lanes 0..5)
+                if (lane < 6) {
+                    int64_t cx = nx + off[lane][0], cy = ny + off[lane][1], cz = nz + off[lane][2];
+                    if (cx < 0) cx += W;  // python negative indices wrap
+                    if (cy < 0) cy += H;
+                    if (cz < 0) cz += L;
+                    const bool bad = cx >= W || cy >= H || cz >= L;
+                    nsh[lane + 1] = bad ? __builtin_nan("") : v.at(cy, cx, cz);
+                    nbad[lane + 1] = bad;
+                }
+                wave_lds_sync();
             }
-            wave_lds_sync();
-            double curT = v.at(ny, nx, nz);
-            for (int q = 0; q < 6; ++q) {
-                if (nbad[q]) { err = true; break; }
-                const double tc = nsh[q];
+            double curT = fast ? nsh[0] : v.at(ny, nx, nz);
+            for (int q = 0; q < 6; ++q) {  // the reference's ordered scan
+                if (nbad[q + 1]) { err = true; break; }
+                const double tc = nsh[q + 1];
                 if (tc < curT) {
                     curT = tc;
                     dx = ustep[q][0];

@@ -1,0 +1,230 @@
+"""GPU parity at BASELINE.json's full sizes (configs[1..4]), on the bench's own synthetic rasters.
+
+* C2, 4096^2 DEM raster: the fp32 field against the oracle's heap FMM (fp64, the reference's
+  algorithm, ~3 s on one core) -- masks equal, max relative error <= 2e-5; the path
+  kernel on that field against the oracle's walk on the same field, <= 1e-9 cells.
+* C3, 128 x 1024^2 batch: one batched solve, four of its maps against the oracle.
+* C4, 16384^2 DEM raster on one GPU: too large for the oracle inside a test, so size-independent
+  properties of the converged field, evaluated on the device in fp64: T[goal] = 0; every reached
+  cell satisfies the reference's local solve (FastMarching.py:17-29) of its own neighbours to
+  2e-5 relative (the Godunov fixed point the reference FMM also reaches);
+  every reached cell other than the goal has a strictly smaller reached neighbour (a descent to
+  the goal exists) and no unreached finite-cost cell touches a reached one (the reached set is
+  closed, i.e. exactly the goal's component).
+* C5, 4096^2 x 3 layered volume: the same properties with FastMarching3D's n-D local solve and
+  six neighbours, and the 3D path kernel against the oracle's walk on the field, <= 1e-9.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def env():
+    import torch
+
+    import eikonal
+    from eikonal import _lib as L
+    from eikonal import terrain
+
+    dev = torch.device("cuda", 0)
+    ctx = eikonal.Context(0)
+    yield torch, eikonal, L, terrain, dev, ctx
+    ctx.close()
+
+
+def local_solve(torch, T, c):
+    """FastMarching.getEikonal of every cell's own neighbours, fp64 (+inf outside the raster)."""
+    inf = float("inf")
+    P = torch.nn.functional.pad(T, (1, 1, 1, 1), value=inf)
+    a = torch.minimum(P[1:-1, :-2], P[1:-1, 2:])  # Thor: x neighbours (:57-62)
+    b = torch.minimum(P[:-2, 1:-1], P[2:, 1:-1])  # Tver
+    lo, hi = torch.minimum(a, b), torch.maximum(a, b)
+    d = hi - lo
+    two = 0.5 * (a + b + torch.sqrt(torch.clamp(2 * c * c - d * d, min=0)))
+    w = torch.where(c < d, lo + c, two)  # :26-29 (one inf: d = inf, lo + c)
+    return torch.where(torch.isinf(lo), torch.full_like(lo, inf), w)
+
+
+def check_properties(torch, T32, c32, goal, rows=2048):
+    H, W = T32.shape
+    gx, gy = goal
+    assert float(T32[gy, gx]) == 0.0
+    worst = 0.0
+    for y0 in range(0, H, rows):
+        ya, yb = max(y0 - 1, 0), min(y0 + rows + 1, H)
+        T = T32[ya:yb].double()
+        c = c32[ya:yb].double()
+        s, e = y0 - ya, y0 - ya + min(rows, H - y0)
+        fin = torch.isfinite(T)
+        w = local_solve(torch, T, c)[s:e]
+        Tc, finc = T[s:e], fin[s:e]
+        # the goal is the source (T = 0); every other reached cell is its neighbours' local solve
+        src = torch.zeros_like(finc)
+        if ya <= gy < yb and s <= gy - ya < e:
+            src[gy - ya - s, gx] = True
+        chk = finc & ~src
+        assert bool(torch.isfinite(c[s:e][finc]).all()), "a reached cell has infinite cost"
+        rel = ((Tc[chk] - w[chk]).abs() / Tc[chk].clamp(min=1e-30))
+        if rel.numel():
+            worst = max(worst, float(rel.max()))
+        # descent: a reached non-source cell has a strictly smaller reached neighbour
+        inf = float("inf")
+        P = torch.nn.functional.pad(T, (1, 1, 1, 1), value=inf)
+        nmin = torch.minimum(torch.minimum(P[1:-1, :-2], P[1:-1, 2:]), torch.minimum(P[:-2, 1:-1], P[2:, 1:-1]))[s:e]
+        assert bool((nmin[chk] < Tc[chk]).all()), "a reached cell without a descent neighbour"
+        # closure: an unreached finite-cost cell has no reached neighbour
+        open_ = ~finc & torch.isfinite(c[s:e])
+        assert not bool(torch.isfinite(nmin[open_]).any()), "an unreached cell next to a reached one"
+    assert worst <= 2e-5, worst
+    return worst
+
+
+def test_c2_full_size_vs_oracle(env):
+    torch, eikonal, L, terrain, dev, ctx = env
+    N = 4096
+    cost = terrain.cost_block(0, 0, N, N, N, N, seed=42, device=dev).contiguous()
+    T = torch.empty_like(cost)
+    fim = eikonal.Fim2d(ctx, 1, N, N, L.EIK_F32)
+    goal, start = (N // 2, N // 2), (256, 256)
+    stream = torch.cuda.current_stream(dev)
+    fim.solve(cost.data_ptr(), T.data_ptr(), [goal], stream.cuda_stream)
+    torch.cuda.synchronize()
+    fim.close()
+    check_properties(torch, T, cost, goal)
+    c64 = cost.double().cpu().numpy()
+    Tg = T.cpu().numpy()
+    O.set_strict(False)
+    try:
+        R = O.fmm2d(c64, goal)
+    finally:
+        O.set_strict(True)
+    fin = np.isfinite(R)
+    assert np.array_equal(np.isfinite(Tg), fin)
+    rel = np.abs(Tg[fin].astype(np.float64) - R[fin]) / np.maximum(R[fin], 1e-30)
+    assert rel.max() <= 2e-5, rel.max()
+    # the path kernel on the GPU field vs the oracle's walk on the same field
+    path, st = ctx.path2d(Tg, start, goal)
+    ref, rst = O.gdm2d(Tg.astype(np.float64), np.array(start, float), np.array(goal, float))
+    assert st == rst == 0 and path.shape == ref.shape and len(path) > 1000
+    assert np.abs(path - ref).max() <= 1e-9
+
+
+def test_c3_full_batch_vs_oracle(env):
+    torch, eikonal, L, terrain, dev, ctx = env
+    B, N = 128, 1024
+    cost = torch.empty((B, N, N), dtype=torch.float32, device=dev)
+    rng = np.random.default_rng(1000)
+    goals = []
+    for b in range(B):  # the bench's batch (bench.py bench_batch)
+        cost[b] = terrain.cost_block(0, 0, N, N, N, N, seed=1000 + b, device=dev)
+        while True:
+            gx, gy = (int(v) for v in rng.integers(N // 8, N - N // 8, 2))
+            if float(cost[b, gy, gx]) < 50:
+                break
+        goals.append((gx, gy))
+    T = torch.empty_like(cost)
+    fim = eikonal.Fim2d(ctx, B, N, N, L.EIK_F32)
+    fim.solve(cost.data_ptr(), T.data_ptr(), goals, torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize()
+    fim.close()
+    O.set_strict(False)
+    try:
+        for b in (0, 37, 90, 127):
+            R = O.fmm2d(cost[b].double().cpu().numpy(), goals[b])
+            Tg = T[b].cpu().numpy()
+            fin = np.isfinite(R)
+            assert np.array_equal(np.isfinite(Tg), fin), b
+            rel = np.abs(Tg[fin].astype(np.float64) - R[fin]) / np.maximum(R[fin], 1e-30)
+            assert rel.max() <= 2e-5, (b, rel.max())
+    finally:
+        O.set_strict(True)
+
+
+def test_c4_full_size_properties(env):
+    torch, eikonal, L, terrain, dev, ctx = env
+    N = 16384
+    cost = terrain.cost_block(0, 0, N, N, N, N, seed=7, device=dev).contiguous()
+    T = torch.empty_like(cost)
+    fim = eikonal.Fim2d(ctx, 1, N, N, L.EIK_F32)
+    goal = (N // 2, N // 2)
+    fim.solve(cost.data_ptr(), T.data_ptr(), [goal], torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize()
+    fim.close()
+    assert float(torch.isfinite(T).float().mean()) > 0.9
+    check_properties(torch, T, cost, goal)
+
+
+def local_solve3(torch, T, c):
+    """FastMarching3D's n-D local solve (:59-75) of every cell's own six neighbours, fp64: the
+    axis minima sorted, the 3-axis root when C^2 > (s2-s0)^2 + (s2-s1)^2, else the 2-axis root when
+    C^2 > (s1-s0)^2, else s0 + C (an inf maximum is dropped by the same tests)."""
+    inf = float("inf")
+    P = torch.nn.functional.pad(T, (1, 1, 1, 1, 1, 1), value=inf)
+    ty = torch.minimum(P[:-2, 1:-1, 1:-1], P[2:, 1:-1, 1:-1])
+    tx = torch.minimum(P[1:-1, :-2, 1:-1], P[1:-1, 2:, 1:-1])
+    tz = torch.minimum(P[1:-1, 1:-1, :-2], P[1:-1, 1:-1, 2:])
+    s = torch.sort(torch.stack([tx, ty, tz]), dim=0).values
+    s0, s1, s2 = s[0], s[1], s[2]
+    C2 = c * c
+    S2, Q2 = s0 + s1, s0 * s0 + s1 * s1
+    S3, Q3 = S2 + s2, Q2 + s2 * s2
+    t1 = s0 + c
+    t2 = (S2 + torch.sqrt(torch.clamp(2 * C2 + S2 * S2 - 2 * Q2, min=0))) / 2
+    t3 = (S3 + torch.sqrt(torch.clamp(3 * C2 + S3 * S3 - 3 * Q3, min=0))) / 3
+    w = torch.where(C2 > (s2 - s0) ** 2 + (s2 - s1) ** 2, t3, torch.where(C2 > (s1 - s0) ** 2, t2, t1))
+    nmin = torch.minimum(torch.minimum(tx, ty), tz)
+    return torch.where(torch.isinf(s0), torch.full_like(s0, inf), w), nmin
+
+
+def test_c5_full_size_properties(env):
+    """configs[4]: the bench's 4096 x 4096 x 3 layered volume (z padded with +inf layers, 5 in
+    memory) through the layered solver; the FM3D fixed point, descent and closure as for C4; the
+    3D path kernel on that field against the oracle's walk on the same field."""
+    torch, eikonal, L, terrain, dev, ctx = env
+    N = 4096
+    c0 = terrain.cost_block(0, 0, N, N, N, N, seed=42, device=dev).contiguous()
+    inf = torch.full_like(c0, float("inf"))
+    c1 = torch.where(c0 > 100, inf, 1.6 * c0)
+    yy = torch.arange(N, device=dev)[:, None] // 64
+    xx = torch.arange(N, device=dev)[None, :] // 64
+    c2 = torch.where(((yy + 2 * xx) % 5) == 0, inf, 0.8 * c0)
+    cost = torch.stack([inf, c0, c1, c2, inf], dim=-1).contiguous()
+    del c1, c2, inf
+    T = torch.empty_like(cost)
+    goal = (N // 2, N // 2, 1)
+    stream = torch.cuda.current_stream(dev)
+    ctx._chk(L.lib().eik_fim3d_solve(ctx._h, cost.data_ptr(), T.data_ptr(), N, N, 5, L.EIK_F32,
+                                     np.array(goal, np.int64), stream.cuda_stream))
+    torch.cuda.synchronize()
+    assert float(T[goal[1], goal[0], goal[2]]) == 0.0
+    worst, rows = 0.0, 512
+    for y0 in range(0, N, rows):
+        ya, yb = max(y0 - 1, 0), min(y0 + rows + 1, N)
+        s, e = y0 - ya, y0 - ya + min(rows, N - y0)
+        Tb, cb = T[ya:yb].double(), cost[ya:yb].double()
+        w, nmin = local_solve3(torch, Tb, cb)
+        w, nmin, Tc, cc = w[s:e], nmin[s:e], Tb[s:e], cb[s:e]
+        fin = torch.isfinite(Tc)
+        src = torch.zeros_like(fin)
+        if y0 <= goal[1] < y0 + rows:
+            src[goal[1] - y0, goal[0], goal[2]] = True
+        chk = fin & ~src
+        assert bool(torch.isfinite(cc[fin]).all())
+        if bool(chk.any()):
+            worst = max(worst, float(((Tc[chk] - w[chk]).abs() / Tc[chk].clamp(min=1e-30)).max()))
+        assert bool((nmin[chk] < Tc[chk]).all()), "a reached cell without a descent neighbour"
+        assert not bool(torch.isfinite(nmin[~fin & torch.isfinite(cc)]).any()), "reached set not closed"
+    assert worst <= 2e-5, worst
+    assert float(torch.isfinite(T[:, :, 1:4]).float().mean()) > 0.8
+    Th = T.cpu().numpy()
+    del cost
+    start = np.array([256.0, 256.0, 1.0])
+    end = np.array([float(goal[0]), float(goal[1]), 1.0])
+    path, st = ctx.path3d(Th, start, end)
+    ref, rst = O.gdm3d(Th.astype(np.float64), start, end, 0.5)
+    assert st == rst == 0 and path.shape == ref.shape and len(path) > 1000
+    assert np.abs(path - ref).max() <= 1e-9
