@@ -80,6 +80,11 @@ __device__ __forceinline__ double interp2_sel(double a, double b, double g00, do
 __device__ __forceinline__ double norm2(double a, double b) { return __builtin_sqrt(a * a + b * b); }
 
 enum { kGdmDone = 0, kGdmFallback = 1, kGdmError = 2 };
+#ifndef EIK_P3PROBE
+#define EIK_P3PROBE(k) ((void)0)  // 3D walker phase timing hooks (tools/path3_prof.hip)
+#define EIK_P3DECL ((void)0)
+#define EIK_P3FLUSH ((void)0)
+#endif
 #ifndef EIK_P2PROBE
 #define EIK_P2PROBE(k) ((void)0)  // 2D walker phase timing hooks (tools/path2_prof.hip)
 #define EIK_P2DECL ((void)0)
@@ -365,15 +370,96 @@ hipError_t gdm2d(const Gdm2dArgs& a, bool f64, hipStream_t st) {
 // ---------------------------------------------------------------- 3D path (FM3D)
 // np.gradient(T) along `axis` (0 y, 1 x, 2 z) at (j, i, k): central differences / 2 inside,
 // one-sided at the ends (numpy's edge_order=1), no inf awareness (FastMarching3D.py:200).
-// The 3D walk is one wave with every lane running the same scalar step (LDS reads are
+// The 3D walk is one wave (wave 0) with every lane running the same scalar step (LDS reads are
 // broadcasts, so no lane divergence).  T is read from an LDS window [WY][WX][WZ] (z fastest, the
-// volume's own order) that is recentred and reloaded by all 64 lanes when the 4x4x4 cube a step
-// needs (trilinear corners +-1 for np.gradient) leaves it; the integer-descent fallback reads
-// outside the window from global memory.  The last kRing path points are mirrored in LDS, so the
+// volume's own order), double-buffered: waves 1..7 build windows, as the 2D kernel's builders do.
+// When the step's 4x4x4 cube (trilinear corners +-1 for np.gradient) comes within kPre3 cells of
+// an inner window edge, the walker requests the window centred on itself into the idle buffer and
+// keeps walking; it waits only if the cube leaves the current window before that build is done
+// (or the prefetched window does not hold it).  The integer-descent fallback reads outside the
+// window from global memory.  The last kRing path points are mirrored in LDS, so the
 // back-tracking of :231-249 does not wait on its own global stores.  The arithmetic, its order
 // and every branch are FastMarching3D.py's (bit-identical to the oracle's restatement).
-constexpr int kWin3Bytes = 48 * 1024;
+constexpr int kWin3Bytes = 48 * 1024;  // per buffer
 constexpr int kRing = 256;
+constexpr int kP3Threads = 512;        // walker + 7 builder waves
+constexpr int kB3 = kP3Threads / 64 - 1;
+constexpr int kPre3 = 14;              // cells from an inner window edge that trigger a prefetch
+
+struct Path3Lds {
+    __attribute__((aligned(16))) char wbuf[2][kWin3Bytes];
+    double ring[kRing][3];
+    double gsh[3][8], nsh[7], psh[6];  // per-step lane exchange of the walker
+    int nbad[7];
+    long long req_y0, req_x0, req_z0;
+    int req_seq;  // walker -> builders: request number (-1: quit)
+    int req_b;    // target buffer
+    int done;     // builders -> walker: finished builds x kB3
+};
+
+// window dimensions (walker and builders compute the same)
+template <typename R>
+__device__ __forceinline__ void win3_dims(int64_t H, int64_t W, int64_t L, int& WY, int& WX, int& WZ) {
+    constexpr int cells = kWin3Bytes / (int)sizeof(R);
+    WZ = (int)(L < 16 ? L : 16);
+    int s = 1;
+    while ((s + 1) * (s + 1) * WZ <= cells && s < 128) ++s;
+    WY = (int)(H < s ? H : s);
+    WX = (int)(W < s ? W : s);
+}
+
+// Builder wave w (0..kB3-1): cells w * 64 + lane + k * 64 kB3 of the window at (y0, x0, z0) into
+// buffer b -- (yy, xx, zz) advanced by carries, 32 loads in flight per lane before their stores.
+template <typename R>
+__device__ void build3(Path3Lds& s, const R* __restrict__ T, int64_t H, int64_t W, int64_t L, int b, int64_t y0,
+                       int64_t x0, int64_t z0, int w) {
+    int WY, WX, WZ;
+    win3_dims<R>(H, W, L, WY, WX, WZ);
+    R* const wl = reinterpret_cast<R*>(s.wbuf[b]);
+    const int lane = threadIdx.x & 63;
+    const int nc = WY * WX * WZ;
+    constexpr int S = 64 * kB3;
+    const int sz = S % WZ, sx = (S / WZ) % WX, sy = (S / WZ) / WX;
+    const int c00 = w * 64 + lane;
+    int zz = c00 % WZ, xx = (c00 / WZ) % WX, yy = (c00 / WZ) / WX;
+    constexpr int kB = 32;
+    for (int c0 = c00; c0 < nc; c0 += S * kB) {
+        R val[kB];
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            if (c0 + S * u < nc) val[u] = T[((y0 + yy) * W + x0 + xx) * L + z0 + zz];
+            zz += sz;
+            if (zz >= WZ) { zz -= WZ; ++xx; }
+            xx += sx;
+            if (xx >= WX) { xx -= WX; ++yy; }
+            yy += sy;
+        }
+#pragma unroll
+        for (int u = 0; u < kB; ++u)
+            if (c0 + S * u < nc) wl[c0 + S * u] = val[u];
+    }
+}
+
+template <typename R>
+__device__ void path3_builder(Path3Lds& s, const R* __restrict__ T, int64_t H, int64_t W, int64_t L) {
+    const int w = (int)(threadIdx.x >> 6) - 1;
+    int seen = 0;
+    unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        const int q = __hip_atomic_load(&s.req_seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (q < 0) return;
+        if (q == seen) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kPathSpin) return;  // walker gone: give up
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        seen = q;
+        build3<R>(s, T, H, W, L, s.req_b, s.req_y0, s.req_x0, s.req_z0, w);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(&s.done, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        t0 = __builtin_amdgcn_s_memrealtime();
+    }
+}
 
 template <typename R>
 struct Win3 {
@@ -412,7 +498,10 @@ __device__ __forceinline__ double tri3(const double* m, double a, double b, doub
     return a0 + a1 * a + a2 * b + a3 * c + a4 * a * b + a5 * a * c + a6 * b * c + a7 * a * b * c;
 }
 
-__device__ __forceinline__ double norm3(double a, double b, double c) { return __builtin_sqrt(a * a + b * b + c * c); }
+// sqrt(a*a + b*b + c*c) < t  <=>  a*a + b*b + c*c < t*t for t = 1 and 1.5 (t*t exact, sqrt correctly
+// rounded and monotone; the largest double below t*t has a root that rounds below t): the
+// distance tests of :238-240 and :266-267 without the square root on the walker's chain
+__device__ __forceinline__ double sq3(double a, double b, double c) { return a * a + b * b + c * c; }
 
 // The walk is ONE wave: its LDS accesses complete in issue order, so lanes exchange values through
 // LDS with only a compiler fence (and an LDS-count wait) -- a workgroup barrier would also wait
@@ -428,28 +517,65 @@ __device__ __forceinline__ int64_t win_origin(int64_t lo, int64_t hi, int n, int
 }
 
 template <typename R>
-__global__ __launch_bounds__(64) void gdm3d_kernel(Gdm3dArgs a) {
-    __shared__ __attribute__((aligned(16))) char wbuf[kWin3Bytes];
-    __shared__ double ring[kRing][3];
-    __shared__ double gsh[3][8], nsh[7], psh[6];  // per-step lane exchange (see below)
-    __shared__ int nbad[7];
+__global__ __launch_bounds__(kP3Threads) void gdm3d_kernel(Gdm3dArgs a) {
+    __shared__ Path3Lds sl;
+    if (threadIdx.x == 0) {
+        sl.req_seq = 0;
+        sl.done = 0;
+    }
+    __syncthreads();
+    if (threadIdx.x >= 64) {
+        path3_builder<R>(sl, static_cast<const R*>(a.T), a.H, a.W, a.L);
+        return;
+    }
+    auto& ring = sl.ring;
+    auto& gsh = sl.gsh;
+    auto& nsh = sl.nsh;
+    auto& psh = sl.psh;
+    auto& nbad = sl.nbad;
     const int lane = threadIdx.x;
     const bool lead = lane == 0;
     Win3<R> v;
     v.T = static_cast<const R*>(a.T);
     v.H = a.H; v.W = a.W; v.L = a.L;
-    v.w = reinterpret_cast<const R*>(wbuf);
-    R* const wl = reinterpret_cast<R*>(wbuf);
-    {
-        constexpr int cells = kWin3Bytes / (int)sizeof(R);
-        v.WZ = (int)(a.L < 16 ? a.L : 16);
-        int s = 1;
-        while ((s + 1) * (s + 1) * v.WZ <= cells && s < 128) ++s;
-        v.WY = (int)(a.H < s ? a.H : s);
-        v.WX = (int)(a.W < s ? a.W : s);
-    }
-    v.y0 = v.x0 = v.z0 = -((int64_t)1 << 40);  // empty: the first step loads
     const int64_t H = a.H, W = a.W, L = a.L;
+    win3_dims<R>(a.H, a.W, a.L, v.WY, v.WX, v.WZ);
+    v.w = reinterpret_cast<const R*>(sl.wbuf[0]);
+    v.y0 = v.x0 = v.z0 = -((int64_t)1 << 40);  // empty: the first step requests a window
+    // the two buffers' origins (scalars: no private array), the current one mirrored in v
+    int64_t oy[2] = {v.y0, v.y0}, ox[2] = {v.x0, v.x0}, oz[2] = {v.z0, v.z0};
+    int cur = 0, seq = 0;
+    bool pending = false;
+    auto issue = [&](int b, int64_t y0, int64_t x0, int64_t z0) {
+        oy[b] = y0; ox[b] = x0; oz[b] = z0;
+        sl.req_y0 = y0;
+        sl.req_x0 = x0;
+        sl.req_z0 = z0;
+        sl.req_b = b;
+        __hip_atomic_store(&sl.req_seq, ++seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto wait_built = [&]() -> bool {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(&sl.done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < seq * kB3) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kPathSpin) return false;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        return true;
+    };
+    int bj_lo = 1, bj_hi = 0, bi_lo = 1, bi_hi = 0, bk_lo = 1, bk_hi = 0;  // empty: the first step decides
+    // step bounds of the fast path (sufficient conditions for "holds and no prefetch trigger")
+    auto set_bounds = [&]() {
+        const int m = pending ? 0 : kPre3;
+        auto lo = [&](int64_t o) { return o == 0 ? 0 : (int)(o + 1 + m); };
+        auto hi = [&](int64_t o, int n, int64_t len) { return o + n >= len ? (int)(len - 1) : (int)(o + n - 3 - m); };
+        bj_lo = lo(v.y0); bj_hi = hi(v.y0, v.WY, H);
+        bi_lo = lo(v.x0); bi_hi = hi(v.x0, v.WX, W);
+        bk_lo = lo(v.z0); bk_hi = hi(v.z0, v.WZ, L);
+    };
+    auto holds = [&](int b, int64_t ylo, int64_t xlo, int64_t zlo, int64_t yhi, int64_t xhi, int64_t zhi) {
+        return ylo >= oy[b] && xlo >= ox[b] && zlo >= oz[b] && yhi < oy[b] + v.WY && xhi < ox[b] + v.WX &&
+               zhi < oz[b] + v.WZ;
+    };
     double* out = a.out;
     // path point q: the LDS ring while it holds it (the last kRing points), else global memory
     auto pt = [&](int64_t q, int c) -> double { return ring[q % kRing][c]; };
@@ -473,46 +599,48 @@ __global__ __launch_bounds__(64) void gdm3d_kernel(Gdm3dArgs a) {
 #pragma unroll
     for (int q = 0; q < 6; ++q)
         for (int c = 0; c < 3; ++c) ustep[q][c] = (double)(-off[q][c]) / tau;
+    EIK_P3DECL;
     for (long k = 0; k < a.steps; ++k) {
+        EIK_P3PROBE(3);
         const uint32_t i = (uint32_t)__builtin_trunc(gx), j = (uint32_t)__builtin_trunc(gy), kk = (uint32_t)__builtin_trunc(gz);
         if (i + 1 >= (uint64_t)W || j + 1 >= (uint64_t)H || kk + 1 >= (uint64_t)L) { status = kGdmError; break; }
-        {  // the step's 4x4x4 cube (clipped to the volume) must be in the window
+        // fast path: while bj_lo <= j <= bj_hi (and for i, kk) the cube is in the current window and
+        // not within kPre3 of an inner edge (or a build is pending): nothing to do this step
+        if ((int)j < bj_lo || (int)j > bj_hi || (int)i < bi_lo || (int)i > bi_hi || (int)kk < bk_lo || (int)kk > bk_hi) {
             const int64_t ylo = j > 0 ? j - 1 : 0, yhi = j + 2 < H ? j + 2 : H - 1;
             const int64_t xlo = i > 0 ? i - 1 : 0, xhi = i + 2 < W ? i + 2 : W - 1;
             const int64_t zlo = kk > 0 ? kk - 1 : 0, zhi = kk + 2 < L ? kk + 2 : L - 1;
-            if (!v.inside(ylo, xlo, zlo) || !v.inside(yhi, xhi, zhi)) {
-                v.y0 = win_origin(ylo, yhi, v.WY, H);
-                v.x0 = win_origin(xlo, xhi, v.WX, W);
-                v.z0 = win_origin(zlo, zhi, v.WZ, L);
-                __syncthreads();  // every lane's reads of the old window are done
-                // lane c, c + 64, ...: (yy, xx, zz) advanced by carries, no divisions; 32 loads in
-                // flight per lane before their LDS stores
-                const int nc = v.WY * v.WX * v.WZ;
-                const int sz = 64 % v.WZ, sx = (64 / v.WZ) % v.WX, sy = (64 / v.WZ) / v.WX;
-                int zz = lane % v.WZ, xx = (lane / v.WZ) % v.WX, yy = (lane / v.WZ) / v.WX;
-                constexpr int kB = 32;
-                for (int c0 = lane; c0 < nc; c0 += 64 * kB) {
-                    R val[kB];
-#pragma unroll
-                    for (int u = 0; u < kB; ++u) {
-                        if (c0 + 64 * u < nc) val[u] = v.T[((v.y0 + yy) * W + v.x0 + xx) * L + v.z0 + zz];
-                        zz += sz;
-                        if (zz >= v.WZ) { zz -= v.WZ; ++xx; }
-                        xx += sx;
-                        if (xx >= v.WX) { xx -= v.WX; ++yy; }
-                        yy += sy;
-                    }
-#pragma unroll
-                    for (int u = 0; u < kB; ++u)
-                        if (c0 + 64 * u < nc) wl[c0 + 64 * u] = val[u];
+            const int64_t cy0 = win_origin(ylo, yhi, v.WY, H), cx0 = win_origin(xlo, xhi, v.WX, W),
+                          cz0 = win_origin(zlo, zhi, v.WZ, L);
+            if (!holds(cur, ylo, xlo, zlo, yhi, xhi, zhi)) {
+                const int nb = seq == 0 ? 0 : 1 - cur;
+                bool have = false;
+                if (pending) {
+                    pending = false;
+                    if (!wait_built()) { status = kGdmError; break; }
+                    have = holds(nb, ylo, xlo, zlo, yhi, xhi, zhi);
                 }
-                __syncthreads();
+                if (!have) {
+                    issue(nb, cy0, cx0, cz0);
+                    if (!wait_built()) { status = kGdmError; break; }
+                }
+                cur = nb;
+                v.w = reinterpret_cast<const R*>(sl.wbuf[cur]);
+                v.y0 = oy[cur];
+                v.x0 = ox[cur];
+                v.z0 = oz[cur];
             }
+            // near an inner edge of the current window: build the window centred here, meanwhile
+            if (!pending && ((ylo - v.y0 < kPre3 && v.y0 > 0) || (v.y0 + v.WY - 1 - yhi < kPre3 && v.y0 + v.WY < H) ||
+                             (xlo - v.x0 < kPre3 && v.x0 > 0) || (v.x0 + v.WX - 1 - xhi < kPre3 && v.x0 + v.WX < W) ||
+                             (zlo - v.z0 < kPre3 && v.z0 > 0) || (v.z0 + v.WZ - 1 - zhi < kPre3 && v.z0 + v.WZ < L)) &&
+                (cy0 != v.y0 || cx0 != v.x0 || cz0 != v.z0)) {
+                issue(1 - cur, cy0, cx0, cz0);
+                pending = true;
+            }
+            set_bounds();
         }
-        // ONE LDS exchange per step: lanes 0..23 take the 24 np.gradient samples (3 axes x 8
-        // trilinear corners); lanes 24..30 the T of the integer-descent node rint(point) and of its
-        // six neighbours in the reference's order (used when the gradient is NaN and the node
-        // needs no back-tracking); lanes 32..37 the last two path points (the pop test :238-240)
+        EIK_P3PROBE(0);
         const int64_t rx = (int64_t)__builtin_rint(gx), ry = (int64_t)__builtin_rint(gy), rz = (int64_t)__builtin_rint(gz);
         const bool rin = rx >= 0 && ry >= 0 && rz >= 0 && rx < W && ry < H && rz < L;
         if (lane >= 24 && lane < 31) {
@@ -552,6 +680,7 @@ __global__ __launch_bounds__(64) void gdm3d_kernel(Gdm3dArgs a) {
         double dx = tri3(gsh[1], gx - i, gy - j, gz - kk);
         double dy = tri3(gsh[0], gx - i, gy - j, gz - kk);
         double dz = tri3(gsh[2], gx - i, gy - j, gz - kk);
+        EIK_P3PROBE(1);
         if (__builtin_isnan(dx) || __builtin_isnan(dy) || __builtin_isnan(dz)) {  // :212-253
             int64_t nx = rx, ny = ry, nz = rz;
             bool err = false;
@@ -570,15 +699,15 @@ __global__ __launch_bounds__(64) void gdm3d_kernel(Gdm3dArgs a) {
                 if (err) { status = kGdmError; break; }
             }
             bool deep = !fast;  // pops beyond the two gathered points read the ring
-            if (fast && n > 0 && norm3(psh[0] - nx, psh[1] - ny, psh[2] - nz) < 1) {
+            if (fast && n > 0 && sq3(psh[0] - nx, psh[1] - ny, psh[2] - nz) < 1.0) {
                 --n;
-                if (n > 0 && norm3(psh[3] - nx, psh[4] - ny, psh[5] - nz) < 1) {
+                if (n > 0 && sq3(psh[3] - nx, psh[4] - ny, psh[5] - nz) < 1.0) {
                     --n;
                     deep = true;
                 }
             }
             if (deep)
-                while (n > 0 && norm3(point(n - 1, 0) - nx, point(n - 1, 1) - ny, point(n - 1, 2) - nz) < 1) --n;
+                while (n > 0 && sq3(point(n - 1, 0) - nx, point(n - 1, 1) - ny, point(n - 1, 2) - nz) < 1.0) --n;
             if (n >= a.cap) { status = kGdmError; break; }
             if (n < lo) lo = n;
             put(n, (double)nx, (double)ny, (double)nz);
@@ -612,6 +741,7 @@ __global__ __launch_bounds__(64) void gdm3d_kernel(Gdm3dArgs a) {
             gy = (double)ny;
             gz = (double)nz;
         }
+        EIK_P3PROBE(2);
         const double nrm = __builtin_sqrt(dx * dx + dy * dy + dz * dz);  // :255
         double ax, ay, az;
         if (nrm < 0.01) {
@@ -631,8 +761,10 @@ __global__ __launch_bounds__(64) void gdm3d_kernel(Gdm3dArgs a) {
         gy = ay;
         gz = az;
         if (__builtin_isnan(ax) || __builtin_isnan(ay) || __builtin_isnan(az)) { status = kGdmError; break; }
-        if (norm3(ax - a.end[0], ay - a.end[1], az - a.end[2]) < 1.5) break;  // :266-267
+        if (sq3(ax - a.end[0], ay - a.end[1], az - a.end[2]) < 2.25) break;  // :266-267
     }
+    if (pending) wait_built();  // no build may still be writing when the builders are told to quit
+    __hip_atomic_store(&sl.req_seq, -1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (lead) {
         if (status == kGdmDone && n < a.cap) {  // :269
             out[3 * n] = a.end[0];
@@ -643,13 +775,14 @@ __global__ __launch_bounds__(64) void gdm3d_kernel(Gdm3dArgs a) {
         *a.n_out = n;
         *a.status = status;
     }
+    EIK_P3FLUSH;
 }
 
 hipError_t gdm3d(const Gdm3dArgs& a, bool f64, hipStream_t st) {
     if (f64)
-        hipLaunchKernelGGL(gdm3d_kernel<double>, dim3(1), dim3(64), 0, st, a);
+        hipLaunchKernelGGL(gdm3d_kernel<double>, dim3(1), dim3(kP3Threads), 0, st, a);
     else
-        hipLaunchKernelGGL(gdm3d_kernel<float>, dim3(1), dim3(64), 0, st, a);
+        hipLaunchKernelGGL(gdm3d_kernel<float>, dim3(1), dim3(kP3Threads), 0, st, a);
     return hipGetLastError();
 }
 
