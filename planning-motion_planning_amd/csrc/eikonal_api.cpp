@@ -74,6 +74,8 @@ struct eik_ctx {
     DevBuf cost, T, T2, goals, work, misc;
     DevBuf l3, c3, m3, v3;             // 3D solver scratch (lists, counts, marks, visits)
     int max_passes3 = 24;
+    int* h3 = nullptr;                 // 3D solver: pinned count + visits words (made once)
+    hipEvent_t e3[2] = {nullptr, nullptr};
 };
 
 struct eik_fim2d {
@@ -158,6 +160,9 @@ void eik_destroy(eik_ctx* c) {
     if (c->cached) eik_fim2d_destroy(c->cached);
     if (c->cached_l) eik_fim2d_destroy(c->cached_l);
     if (c->cached_fill) eik_fim2d_destroy(c->cached_fill);
+    if (c->h3) (void)hipHostFree(c->h3);
+    for (hipEvent_t e : c->e3)
+        if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -894,16 +899,18 @@ static int fim3d_solve_batch(eik_ctx* c, const void* d_cost, void* d_T, int64_t 
     a.counts = (int*)c->c3.p;
     a.mark = (unsigned*)c->m3.p;
     a.visits = (unsigned long long*)c->v3.p;
-    hipEvent_t e0, e1;
-    HIPCHK(c, hipEventCreate(&e0));
-    HIPCHK(c, hipEventCreate(&e1));
+    // pinned words and events live in the context: a solve of a small volume (the planner's
+    // end-effector volumes) is ~1 ms, so per-call hipHostMalloc / event creation would show
+    if (!c->h3) HIPCHK(c, hipHostMalloc((void**)&c->h3, sizeof(int) * 2 + sizeof(unsigned long long)));
+    for (hipEvent_t& e : c->e3)
+        if (!e) HIPCHK(c, hipEventCreate(&e));
+    hipEvent_t e0 = c->e3[0], e1 = c->e3[1];
     HIPCHK(c, hipEventRecord(e0, st));
     HIPCHK(c, hipMemsetAsync(c->v3.p, 0, sizeof(unsigned long long), st));
     HIPCHK(c, c->goals.ensure(sizeof(int64_t) * 3 * B));
     HIPCHK(c, hipMemcpyAsync(c->goals.p, goals, sizeof(int64_t) * 3 * B, hipMemcpyHostToDevice, st));
     HIPCHK(c, fim3d_init(a, dtype == EIK_F64, (const int64_t*)c->goals.p, (int)B, st));
-    int* h = nullptr;
-    HIPCHK(c, hipHostMalloc((void**)&h, sizeof(int) * 2 + sizeof(unsigned long long)));
+    int* h = c->h3;
     const int grid = c->grid > 0 ? c->grid : 4 * c->cu_count;
     const int64_t max_iters = 64 * ((int64_t)a.ntx + a.nty + a.ntz) + 8 * tiles + 4096;
     int64_t it = 0;
@@ -934,9 +941,6 @@ static int fim3d_solve_batch(eik_ctx* c, const void* d_cost, void* d_T, int64_t 
         c->last.solve_ms = ms;
         c->last.bytes_alg = (double)*hv * (dtype == EIK_F64 ? 8 : 4) * 3.0 * a.tx * a.ty * a.tz;
     }
-    (void)hipHostFree(h);
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
     return rc;
 }
 

@@ -1,0 +1,48 @@
+"""FM3D (general 3D solver, fim3d.hip) on the bench's end-effector volume: wall time, device solve
+time, launches and visits, for several host-sync cadences (EIK_OPT_SYNC_EVERY)."""
+import os, sys, time
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "planning-motion_planning_amd"))
+import eikonal
+from eikonal import _lib as L
+import bench
+
+ctx = eikonal.Context(0)
+_orig = bench.timed_loop
+cap = {}
+
+
+def grab(fn, steps, warmup=1):  # capture the arm volume bench_arm builds, skip its timing loops
+    return _orig(fn, 1, 0)
+
+
+bench.timed_loop = grab
+import planner  # noqa: E402
+orig_arm_path = ctx.arm_path
+
+
+def arm_path(*a, **k):
+    r = orig_arm_path(*a, **k)
+    cap["cost"] = r[2]
+    return r
+
+
+ctx.arm_path = arm_path
+bench.bench_arm(ctx, 1)
+cost = cap["cost"]
+H, W, Lz = cost.shape
+fin = np.argwhere(np.isfinite(cost))
+goal = fin[len(fin) // 2][[1, 0, 2]]
+print("volume", cost.shape, "goal", goal, flush=True)
+for se in (8, 32, 128):
+    ctx.set_option(L.OPT_SYNC_EVERY, se)
+    ctx.tmap3d(cost, goal)
+    t0 = time.perf_counter()
+    for _ in range(10):
+        ctx.tmap3d(cost, goal)
+    el = (time.perf_counter() - t0) / 10 * 1e3
+    s = ctx.stats()
+    print(f"sync_every={se}: wall {el:.3f} ms, device {s['solve_ms']:.3f} ms, launches {s['iterations']}, "
+          f"visits {s['tile_visits']}", flush=True)
