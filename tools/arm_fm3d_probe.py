@@ -36,13 +36,14 @@ H, W, Lz = cost.shape
 fin = np.argwhere(np.isfinite(cost))
 goal = fin[len(fin) // 2][[1, 0, 2]]
 print("volume", cost.shape, "goal", goal, flush=True)
-for se in (8, 32, 128):
+for se, grid in ((32, 0), (32, 64), (32, 256), (32, 512)):
     ctx.set_option(L.OPT_SYNC_EVERY, se)
+    ctx.set_option(L.OPT_GRID, grid)
     ctx.tmap3d(cost, goal)
     t0 = time.perf_counter()
     for _ in range(10):
         ctx.tmap3d(cost, goal)
     el = (time.perf_counter() - t0) / 10 * 1e3
     s = ctx.stats()
-    print(f"sync_every={se}: wall {el:.3f} ms, device {s['solve_ms']:.3f} ms, launches {s['iterations']}, "
+    print(f"sync_every={se} grid={grid or 'default'}: wall {el:.3f} ms, device {s['solve_ms']:.3f} ms, launches {s['iterations']}, "
           f"visits {s['tile_visits']}", flush=True)
