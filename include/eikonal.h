@@ -82,7 +82,7 @@ typedef enum {
                                 EIK_ERR_NOCONVERGE (0: default 1024 x tiles + 2^20)            */
     EIK_OPT_PASSES = 9       /* persistent mode: sweep passes a visit may run in place while its
                                 tile keeps changing before it is re-queued (0, the default:
-                                8 for a single map, 2 for a batch of maps)                     */
+                                24 for a single map, 2 for a batch of maps)                    */
 } eik_option;
 
 typedef enum { EIK_MODE_LIST = 0, EIK_MODE_PERSISTENT = 1 } eik_mode;

@@ -304,7 +304,7 @@ int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
     // in-place passes: a single map's solve is front-latency-bound (long in-place refinement of
     // the front tiles pays), a batch is throughput-bound (hand the workgroup to tiles with fresher
     // halos early): C2 2.07-2.09 ms at 8-16 vs 2.23 at 2; C3 6.86 ms at 2 vs 8.0 at 8
-    f->a.max_passes = c->passes > 0 ? c->passes : f->B > 1 ? 2 : 8;
+    f->a.max_passes = c->passes > 0 ? c->passes : f->B > 1 ? 2 : 24;
     f->a.qbudget = c->max_visits ? c->max_visits : 1024ull * (unsigned long long)(f->B * f->a.tiles_per_map) + (1ull << 20);
     f->iterations = 0;
     f->host_syncs = 0;

@@ -211,7 +211,7 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
     EIK_PROBE(1);
 
     // PERSISTENT mode revisits a tile that changed IN PLACE, up to a.max_passes times
-    // (EIK_OPT_PASSES; by default 8 for one map, 2 for a batch): its interior is already in LDS
+    // (EIK_OPT_PASSES; by default 24 for one map, 2 for a batch): its interior is already in LDS
     // and nobody else writes it while it is busy, so a pass only refreshes the halo ring,
     // activates the neighbours its last write-back improved, and sweeps again -- no restaging,
     // no queue round trip.  (List mode: one pass; a changed tile re-lists itself.)

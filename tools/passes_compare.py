@@ -1,6 +1,6 @@
 """In-place pass cap (EIK_OPT_PASSES) of the persistent driver, and the list driver, on C2 (4096^2
 DEM), C3 (batch 128 x 1024^2) and C4 at one GPU (16384^2): time, visits, in-place passes."""
-import sys, time
+import os, sys, time
 import numpy as np
 import torch
 sys.path.insert(0, 'planning-motion_planning_amd')
@@ -14,8 +14,9 @@ which = sys.argv[1:] or ["C2", "C3", "C4"]
 
 
 def run(name, fim, cost, T, goals, K=5):
-    for mode, passes in ((L.MODE_PERSISTENT, 0), (L.MODE_PERSISTENT, 8), (L.MODE_PERSISTENT, 2),
-                         (L.MODE_PERSISTENT, 16), (L.MODE_PERSISTENT, 0)):
+    import os
+    caps = [int(v) for v in os.environ.get("PASSES", "0,8,2,16,0").split(",")]
+    for mode, passes in [(L.MODE_PERSISTENT, p) for p in caps]:
         ctx.set_option(L.OPT_MODE, mode)
         ctx.set_option(L.OPT_PASSES, passes)
         fim.solve(cost.data_ptr(), T.data_ptr(), goals, s)
@@ -66,4 +67,4 @@ if "C4" in which:
     cost = terrain.cost_block(0, 0, N, N, N, N, seed=7, device=dev).contiguous()
     T = torch.empty_like(cost)
     fim = eikonal.Fim2d(ctx, 1, N, N, L.EIK_F32)
-    run("C4", fim, cost, T, [(N // 2, N // 2)], K=2)
+    run("C4", fim, cost, T, [(N // 2, N // 2)], K=int(os.environ.get("C4K", "2")))
