@@ -812,7 +812,7 @@ static int solve_layered(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, i
     a.edge_dirty = nullptr;
     for (auto& g : a.ghost) g = nullptr;
     a.qtimeout = (unsigned long long)(c->qtimeout_s * 1e8);
-    a.max_passes = c->passes > 0 ? c->passes : 8;
+    a.max_passes = c->passes > 0 ? c->passes : 24;  // C5 A/B: 8 -> 24 passes 15.9 -> 13.1 ms
     a.qbudget = c->max_visits ? c->max_visits : 1024ull * (unsigned long long)a.tiles_per_map + (1ull << 20);
     if (c->resident_l[nl] == 0) c->resident_l[nl] = fim2dl_persist_resident(nl, c->cu_count);
     const int grid = std::min(c->grid > 0 ? c->grid : 4 * c->cu_count, c->resident_l[nl]);
