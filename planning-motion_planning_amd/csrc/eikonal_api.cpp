@@ -303,7 +303,9 @@ int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
     f->a.qtimeout = (unsigned long long)(c->qtimeout_s * 1e8);  // s_memrealtime: 100 MHz
     // in-place passes: a single map's solve is front-latency-bound (long in-place refinement of
     // the front tiles pays), a batch is throughput-bound (hand the workgroup to tiles with fresher
-    // halos early): C2 2.07-2.09 ms at 8-16 vs 2.23 at 2; C3 6.86 ms at 2 vs 8.0 at 8
+    // halos early): C2 2.07-2.09 ms at 8-16 vs 2.23 at 2; C3 6.86 ms at 2 vs 8.0 at 8.  Single map
+    // 24 (profiles/r01g_passes_8_16_24.log): C2 2.03-2.04 ms vs 2.05-2.08 at 16 (within noise),
+    // C4 at one GPU 16.4-16.6 vs 16.3-16.4 at 16 (within noise); 8 is clearly slower on both.
     f->a.max_passes = c->passes > 0 ? c->passes : f->B > 1 ? 2 : 24;
     f->a.qbudget = c->max_visits ? c->max_visits : 1024ull * (unsigned long long)(f->B * f->a.tiles_per_map) + (1ull << 20);
     f->iterations = 0;
@@ -812,7 +814,8 @@ static int solve_layered(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, i
     a.edge_dirty = nullptr;
     for (auto& g : a.ghost) g = nullptr;
     a.qtimeout = (unsigned long long)(c->qtimeout_s * 1e8);
-    a.max_passes = c->passes > 0 ? c->passes : 24;  // C5 A/B: 8 -> 24 passes 15.9 -> 13.1 ms
+    // C5 A/B (profiles/r02a_c5_passes.log): 8 / 16 / 24 passes 15.5-16.3 / 13.9 / 12.9 ms
+    a.max_passes = c->passes > 0 ? c->passes : 24;
     a.qbudget = c->max_visits ? c->max_visits : 1024ull * (unsigned long long)a.tiles_per_map + (1ull << 20);
     if (c->resident_l[nl] == 0) c->resident_l[nl] = fim2dl_persist_resident(nl, c->cu_count);
     const int grid = std::min(c->grid > 0 ? c->grid : 4 * c->cu_count, c->resident_l[nl]);

@@ -216,7 +216,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
         __syncthreads();
         const unsigned f = L.flags;  // uniform
         if (!(f & 128u) || pass + 1 >= kPasses) break;
-        if (tid == 0 && a.visits) atomicAdd(a.visits + 1, 1ull);  // in-place passes (stats)
+        if (tid == 0) charge_inplace_pass(a);  // in-place passes: stats and the visit budget
         activate_neighbours(a, tile, f, L.key, 0, 0u);             // lanes 0..4 (T already drained)
         dirs = 0xFu;  // a self revisit: every direction
         Ts[h] = load_halo();
@@ -247,7 +247,7 @@ __global__ __launch_bounds__(kThreads) void fim2dl_persist_kernel(Fim2dArgs a) {
                 if (threadIdx.x == 0) {
                     qfinish(a, tile);
                     if (++nvis == 64u) {  // visit cap (negative costs never converge)
-                        if (atomicAdd(a.visits, 64ull) + 64ull >= a.qbudget) atomicOr(a.qerror, 2u);
+                        charge_visits(a, 64ull);
                         nvis = 0;
                     }
                 }

@@ -276,6 +276,21 @@ __device__ __forceinline__ int qgrab(const Fim2dArgs& a, unsigned& trig) {
     }
 }
 
+// Visit budget (EIK_OPT_MAX_VISITS; negative costs on device buffers never converge): full
+// visits (counter 0, flushed 64 at a time) and in-place passes (counter 1) are charged alike --
+// an in-place pass sweeps the tile like a visit does.  One lane calls these.
+__device__ __forceinline__ void charge_visits(const Fim2dArgs& a, unsigned long long n) {
+    const unsigned long long v = atomicAdd(a.visits, n) + n;
+    if (v + __hip_atomic_load(a.visits + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.qbudget)
+        atomicOr(a.qerror, 2u);
+}
+__device__ __forceinline__ void charge_inplace_pass(const Fim2dArgs& a) {
+    const unsigned long long p = atomicAdd(a.visits + 1, 1ull) + 1ull;
+    if ((p & 63ull) == 0ull &&
+        p + __hip_atomic_load(a.visits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.qbudget)
+        atomicOr(a.qerror, 2u);
+}
+
 // Retire a visited tile (after its activations completed): re-queue it if it was activated
 // while busy (it stays counted), else it stops counting as active.
 __device__ __forceinline__ void qfinish(const Fim2dArgs& a, int tile) {

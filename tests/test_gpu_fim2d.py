@@ -170,10 +170,11 @@ def test_stats_count_visits(ctx):
     assert s["tile_visits"] >= 64 and s["iterations"] >= 1 and s["solve_ms"] > 0
 
 
-@pytest.mark.parametrize("passes", [1, 2, 16])
+@pytest.mark.parametrize("passes", [1, 2, 8, 16])
 def test_pass_cap_option(passes):
     """EIK_OPT_PASSES (in-place passes per persistent visit) changes the schedule, not the field:
-    a single map and a batch against the oracle at caps other than the defaults (8 / 2)."""
+    a single map and a batch against the oracle at caps other than the defaults (24 for a single
+    map, 2 for a batch; 2 is also run here on the single map and 1 / 16 on the batch)."""
     import eikonal
     from eikonal import _lib as L
 
@@ -194,5 +195,52 @@ def test_pass_cap_option(passes):
         T = c.tmap2d_batch(costs, goals)
         for b in range(4):
             check_field(T[b], oracle_field(costs[b], goals[b]), goals[b], False)
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("neg", [False, True])
+def test_visit_budget_device_buffers(neg):
+    """EIK_OPT_MAX_VISITS on the device-buffer entry (eik_fim2d_solve: no host-side cost check).
+    In-place passes are charged to the budget like full visits, so a single-map solve (24 passes
+    per visit by default) whose workgroups never reach 64 full visits each still stops with
+    EIK_ERR_NOCONVERGE.  neg: a negative-cost block (reference semantics undefined) must end in
+    NOCONVERGE or a finished solve -- never a hang (the test's own timeout)."""
+    import torch
+    import eikonal
+    from eikonal import _lib as L
+
+    rng = np.random.default_rng(3)
+    cost = rng.uniform(1, 10, (1024, 1024)).astype(np.float32)
+    cost[rng.random(cost.shape) < 0.15] = np.inf
+    if neg:
+        cost[400:600, 400:600] = -2.0
+    goal = np.array([[512, 300]], np.int64)
+    cost[300, 512] = 1.0
+    c = eikonal.Context(0)
+    try:
+        c.set_option(L.OPT_MAX_VISITS, 128)
+        dev = torch.device("cuda", 0)
+        cd = torch.from_numpy(cost).to(dev)
+        Td = torch.empty_like(cd)
+        f = L.Fim2d(c, 1, 1024, 1024, L.EIK_F32)
+        try:
+            if neg:
+                try:
+                    f.solve(cd.data_ptr(), Td.data_ptr(), goal, torch.cuda.current_stream(dev).cuda_stream)
+                except eikonal.EikError as e:
+                    assert e.code == L.EIK_ERR_NOCONVERGE, e
+            else:
+                with pytest.raises(eikonal.EikError) as ei:
+                    f.solve(cd.data_ptr(), Td.data_ptr(), goal, torch.cuda.current_stream(dev).cuda_stream)
+                assert ei.value.code == L.EIK_ERR_NOCONVERGE
+            # the context stays usable: default budget, same map, solves
+            c.set_option(L.OPT_MAX_VISITS, 0)
+            if not neg:
+                f.solve(cd.data_ptr(), Td.data_ptr(), goal, torch.cuda.current_stream(dev).cuda_stream)
+                torch.cuda.synchronize()
+                check_field(Td.cpu().numpy(), oracle_field(cost, goal[0]), goal[0], False)
+        finally:
+            f.close()
     finally:
         c.close()

@@ -137,6 +137,51 @@ def test_layered_device_entry(ctx):
     check(T, R, False)
 
 
+@pytest.mark.parametrize("passes", [1, 8])
+def test_layered_pass_cap_option(passes):
+    """EIK_OPT_PASSES also sets the layered solver's in-place pass cap (default 24): the schedule
+    changes, the field does not."""
+    import eikonal
+    from eikonal import _lib as L
+
+    c3, goal = _layered_case((200, 230, 3), 31, pad=True, switch=True)
+    c = eikonal.Context(0)
+    try:
+        c.set_option(L.OPT_PASSES, passes)
+        O.set_strict(False)
+        try:
+            R = O.fmm3d(c3, goal, None)
+        finally:
+            O.set_strict(True)
+        check(c.tmap3d(c3, goal, dtype=np.float32), R, False)
+        if passes == 1:
+            assert c.stats()["inplace_passes"] == 0
+    finally:
+        c.close()
+
+
+def test_layered_visit_budget():
+    """A tiny EIK_OPT_MAX_VISITS stops the layered solver (device-buffer entry, no host-side cost
+    check) with EIK_ERR_NOCONVERGE: its in-place passes are charged to the budget too."""
+    import torch
+    import eikonal
+    from eikonal import _lib as L
+
+    c3, goal = _layered_case((700, 700, 3), 32, pad=True, switch=True)
+    c = eikonal.Context(0)
+    try:
+        c.set_option(L.OPT_MAX_VISITS, 128)
+        dev = torch.device("cuda", 0)
+        cd = torch.from_numpy(c3.astype(np.float32)).to(dev)
+        Td = torch.empty_like(cd)
+        H, W, Lz = c3.shape
+        rc = L.lib().eik_fim3d_solve(c._h, cd.data_ptr(), Td.data_ptr(), H, W, Lz, L.EIK_F32,
+                                     np.ascontiguousarray(goal, np.int64), torch.cuda.current_stream(dev).cuda_stream)
+        assert rc == L.EIK_ERR_NOCONVERGE, rc
+    finally:
+        c.close()
+
+
 @pytest.mark.parametrize("shape,seed,pad", [((300, 280, 3), 5, True), ((70, 90, 40), 6, False), ((20, 23, 70), 7, False)])
 def test_path3d_windowed(ctx, shape, seed, pad):
     """Walks longer than the path kernel's LDS window (recentred reloads, back-tracking through
