@@ -80,9 +80,14 @@ typedef enum {
                                 the solve fails with EIK_ERR_HIP instead of hanging (default 30) */
     EIK_OPT_MAX_VISITS = 8,  /* persistent mode: tile visits after which a solve fails with
                                 EIK_ERR_NOCONVERGE (0: default 1024 x tiles + 2^20)            */
-    EIK_OPT_PASSES = 9       /* persistent mode: sweep passes a visit may run in place while its
+    EIK_OPT_PASSES = 9,      /* persistent mode: sweep passes a visit may run in place while its
                                 tile keeps changing before it is re-queued (0, the default:
                                 24 for a single map, 2 for a batch of maps)                    */
+    EIK_OPT_FRESH_FIRST = 10,/* persistent mode: 1 queues a tile's first activation ahead of
+                                re-visits while the queue has a backlog (default 0: one FIFO)  */
+    EIK_OPT_SCHED = 11       /* persistent mode, bit mask: 1 = a busy tile serves activations that
+                                reach it in place (no re-queued visit); 2 = after a visit's first
+                                pass, neighbour activations wait for the visit's end           */
 } eik_option;
 
 typedef enum { EIK_MODE_LIST = 0, EIK_MODE_PERSISTENT = 1 } eik_mode;

@@ -32,7 +32,9 @@ struct Fim2dArgs {
     unsigned* qerror;      // nonzero: a spin timed out           -- qctl + 192
     unsigned* qslot;       // [qmask + 1] FIFO slots: tile + 1, 0 = empty
     unsigned qmask;        // power of two >= tiles, minus one
-    unsigned* qstate;      // per tile: kPending | kBusy
+    unsigned* qstate;      // per tile: kPending | kBusy | trigger bits | kVisited
+    int fresh_first;       // nonzero: a tile's first activation jumps a backlog (qslot_put_front)
+    int sched;             // persistent visits: bit 0 consume activations in place, bit 1 defer in-place activations
     unsigned long long qtimeout;  // spin limit, s_memrealtime ticks (100 MHz)
     unsigned long long qbudget;   // tile-visit cap (negative costs never converge)
     int max_passes;        // in-place sweep passes per persistent visit (EIK_OPT_PASSES)

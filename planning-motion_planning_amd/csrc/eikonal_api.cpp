@@ -62,6 +62,8 @@ struct eik_ctx {
     double qtimeout_s = 30.0;    // EIK_OPT_QTIMEOUT: persistent-mode spin limit
     unsigned long long max_visits = 0;  // EIK_OPT_MAX_VISITS (0: per-solver default)
     int passes = 0;              // EIK_OPT_PASSES: in-place passes per persistent visit (0: adaptive)
+    bool fresh_first = false;    // EIK_OPT_FRESH_FIRST: fresh tiles jump a backlogged FIFO
+    int sched = 0;               // EIK_OPT_SCHED: in-place scheduling of persistent visits
     int timing = 0;
     int grid = 0;
     eik_stats last{};
@@ -185,6 +187,8 @@ int eik_set_option(eik_ctx* c, int opt, double v) {
         case EIK_OPT_QTIMEOUT: c->qtimeout_s = v > 0 ? v : 30.0; break;
         case EIK_OPT_MAX_VISITS: c->max_visits = v > 0 ? (unsigned long long)v : 0ull; break;
         case EIK_OPT_PASSES: c->passes = std::max(0, std::min(64, (int)v)); break;
+        case EIK_OPT_FRESH_FIRST: c->fresh_first = v != 0; break;
+        case EIK_OPT_SCHED: c->sched = std::max(0, std::min(3, (int)v)); break;
         default: return set_err(c, EIK_ERR_ARG, "unknown option %d", opt);
     }
     return EIK_OK;
@@ -353,7 +357,10 @@ int eik_fim2d_iterate(eik_fim2d* f, int64_t max_iters, int64_t* active) {
             HIPCHK(c, hipEventRecord(f->ev_pool[f->ev_used++], f->stream));
         }
         if (f->persist_grid == 0) f->persist_grid = fim2d_persist_resident(f->f64, c->cu_count);
-        HIPCHK(c, fim2d_persist(f->a, f->f64, std::min(grid, f->persist_grid), f->stream));
+        const int g = std::min(grid, f->persist_grid);
+        f->a.fresh_first = c->fresh_first;
+        f->a.sched = c->sched;
+        HIPCHK(c, fim2d_persist(f->a, f->f64, g, f->stream));
         if (c->timing) HIPCHK(c, hipEventRecord(f->ev_pool[f->ev_used++], f->stream));
         ++f->iterations;
         HIPCHK(c, hipMemcpyAsync(f->h_q, f->qctl.p, kQueueCtlBytes, hipMemcpyDeviceToHost, f->stream));
@@ -539,6 +546,8 @@ int eik_fim2d_launch(eik_fim2d* f, int live) {
     }
     // live: the last workgroup is the halo agent; all must be co-resident (grid <= resident)
     const int g = std::max(live ? 2 : 1, std::min(grid, f->persist_grid));
+    a.fresh_first = c->fresh_first;
+    a.sched = c->sched;
     HIPCHK(c, fim2d_persist(a, f->f64, g, f->stream));
     if (c->timing) HIPCHK(c, hipEventRecord(f->ev_pool[f->ev_used++], f->stream));
     f->live_on = live != 0;
@@ -819,6 +828,7 @@ static int solve_layered(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, i
     a.qbudget = c->max_visits ? c->max_visits : 1024ull * (unsigned long long)a.tiles_per_map + (1ull << 20);
     if (c->resident_l[nl] == 0) c->resident_l[nl] = fim2dl_persist_resident(nl, c->cu_count);
     const int grid = std::min(c->grid > 0 ? c->grid : 4 * c->cu_count, c->resident_l[nl]);
+    a.fresh_first = c->fresh_first;
     HIPCHK(c, hipEventRecord(f->ev_start, st));
     HIPCHK(c, hipMemsetAsync(f->visits.p, 0, 2 * sizeof(unsigned long long), st));
     HIPCHK(c, fim2dl_init(a, goal[0], goal[1], goal[2], st));

@@ -37,36 +37,43 @@
 namespace eik {
 
 // ------------------------------------------------------------------------- quadrant sweep
-// Cs sits right after the Ts ring in TileLds: Cs - Ts is a compile-time constant, so every LDS
-// access of a sweep step is one per-lane address plus an immediate offset.
-constexpr int kCsOff = (kLds + 1) * kLds;  // elements
+// A tile cell in LDS: arrival time and cost side by side, so one ds_read_b64 (fp32) fetches both.
+template <typename R>
+struct alignas(2 * sizeof(R)) Cell {
+    R t, c;
+};
 
 // One quadrant sweep of the staged tile.  DX/DY = +-1: direction of propagation.
 // Lane l owns column x; at step s it updates row r = s - l (skewed Gauss-Seidel), so its
 // upstream x neighbour is lane l-1's previous result (DPP) and its upstream y neighbour its own.
+// Each quadrant sweep reads only its UPSTREAM neighbours: the four concurrent sweeps together
+// evaluate the local solve on every combination of one x and one y neighbour, and since the
+// Godunov update is monotone in both, the smallest of those four is the update on the two minima
+// -- the same fixed point as reading both neighbours per axis in every sweep (tools/sched_sim.c:
+// identical field, +1 % passes on the 4096^2 DEM), for 2 LDS reads per step instead of 5 (the
+// sweep is LDS-bound at three workgroups per CU: 14 -> 8 LDS cycles per wave-step).
 // Branch- and select-free: r is clamped to [-1, 64] (one add + one med3 on the byte offset);
-// rows -1 and 64 are the halo rows, whose cost is +inf in Cs, so a lane outside the tile
-// computes +inf or NaN and its ds_min / min / `<` are no-ops.  TRACK: also report whether any
-// cell decreased by more than the tolerance (only needed for multi-round visits; single-round
-// visits read it off the write-back).
+// rows -1 and 64 are the halo rows, whose cost is +inf, so a lane outside the tile computes +inf
+// or NaN and its ds_min / min / `<` are no-ops.  TRACK: also report whether any cell decreased by
+// more than the tolerance (only needed for multi-round visits; single-round visits read it off
+// the write-back).
 // Software pipeline depth of a sweep: the LDS reads of step s + kAhead are issued at step s,
 // so the ~100-cycle LDS round trip overlaps kAhead steps of the Godunov chain instead of being
-// exposed once per step.  Reading ahead is safe: a lane's own column is written only by itself,
-// the downstream-x column (lane l+1) reaches row r one step after lane l, and the upstream-x
-// value of lanes 1..63 comes from the DPP register path (the LDS upstream-x read serves lane 0,
-// whose upstream column is the halo, which no sweep writes).  Another wave's concurrent ds_min
-// may make a pre-read value stale (larger): that only delays convergence -- a visit whose
-// sweeps changed nothing had no concurrent writes, so its reads were exact.
+// exposed once per step.  Reading ahead is safe: a lane's own column is written only by itself
+// within this sweep, and the upstream-x value of lanes 1..63 comes from the DPP register path (the
+// LDS upstream-x read serves lane 0, whose upstream column is the halo, which no sweep writes).
+// Another wave's concurrent ds_min may make a pre-read value stale (larger): that only delays
+// convergence -- a visit whose sweeps changed nothing had no concurrent writes, so its reads
+// were exact.
 constexpr int kAhead = 4;
 
 template <typename R, int DX, int DY, bool TRACK>
-__device__ __forceinline__ bool sweep_quadrant(R* __restrict__ Ts, int lane, R keep) {
-    constexpr int S = (int)sizeof(R);
+__device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lane, R keep) {
+    constexpr int S = (int)sizeof(Cell<R>);
     constexpr int kRow = kLds * S;
     constexpr int D = kAhead;
     static_assert((2 * kTile) % D == 0, "pipeline depth must divide the step count");
     char* const base = reinterpret_cast<char*>(Ts);
-    auto ld = [&](int off) { return *reinterpret_cast<const R*>(base + off); };
     const int col = (DX > 0 ? lane : kTile - 1 - lane) + 1;
     const int lo_b = col * S, hi_b = (kLds - 1) * kRow + col * S;  // LDS rows 0 and 65
     // step s: tile row r = s - lane -> LDS row (DY > 0 ? r + 1 : 64 - r), clamped to [0, 65]
@@ -78,18 +85,17 @@ __device__ __forceinline__ bool sweep_quadrant(R* __restrict__ Ts, int lane, R k
     };
     bool changed = false;
     // the upstream halo row value is the lane's "previous row" result before it starts
-    R cur = ld((DY > 0 ? 0 : kLds - 1) * kRow + col * S);
+    R cur = reinterpret_cast<const Cell<R>*>(base + (DY > 0 ? 0 : kLds - 1) * kRow + col * S)->t;
     int q_o[D];
-    R q_old[D], q_dnx[D], q_dny[D], q_upx[D], q_c[D];
+    R q_old[D], q_upx[D], q_c[D];
     auto fetch = [&](int u) {
         const int o = clampb(raw);
         raw += DY * kRow;
         q_o[u] = o;
-        q_old[u] = ld(o);
-        q_dnx[u] = ld(o + DX * S);
-        q_dny[u] = ld(o + DY * kRow);
-        q_upx[u] = ld(o - DX * S);
-        q_c[u] = ld(o + kCsOff * S);
+        const Cell<R> v = *reinterpret_cast<const Cell<R>*>(base + o);
+        q_old[u] = v.t;
+        q_c[u] = v.c;
+        q_upx[u] = reinterpret_cast<const Cell<R>*>(base + o - DX * S)->t;
     };
 #pragma unroll
     for (int u = 0; u < D; ++u) fetch(u);
@@ -98,11 +104,11 @@ __device__ __forceinline__ bool sweep_quadrant(R* __restrict__ Ts, int lane, R k
         for (int u = 0; u < D; ++u) {
             // x side: lane 0 takes the halo column; lanes 1.. take lane l-1's fresh value (DPP)
             // -- the prefetched LDS value of that cell is a valid, possibly stale, upper bound, so
-            // one v_min3 serves both cases; the chain to w is godunov2_chain's (see there)
-            const R xs = umin(q_upx[u], q_dnx[u]);
+            // one v_min_u32_dpp serves both (lane 0, whose shift source is out of range, keeps
+            // the LDS value); the chain to w is godunov2_chain's (see there)
             const R c2x2 = R(2) * (q_c[u] * q_c[u]);
-            const R w = godunov2_chain(umin(wave_shr1_umin_id(cur), xs), umin(cur, q_dny[u]), q_c[u], c2x2);
-            lds_min(reinterpret_cast<R*>(base + q_o[u]), w);
+            const R w = godunov2_chain(umin(wave_shr1_umin_id(cur), q_upx[u]), cur, q_c[u], c2x2);
+            lds_min(&reinterpret_cast<Cell<R>*>(base + q_o[u])->t, w);
             if constexpr (TRACK) changed |= w < q_old[u] * keep;
             cur = umin(w, q_old[u]);  // NaN (both-inf case) sorts above every value: keeps old
             fetch(u);  // refill the slot: step s + u + D (past the last step: clamped halo rows)
@@ -117,18 +123,17 @@ __device__ __forceinline__ bool sweep_quadrant(R* __restrict__ Ts, int lane, R k
 // LDS of one tile visit
 template <typename R>
 struct TileLds {
-    // Tbuf: tile + halo ring (66 x 66 at offset kLds), plus one guard row above and below (the
-    // clamped r = -1 / 64 steps read one row beyond the halo: in-bounds, +inf, and masked by the
-    // +inf halo cost anyway)
-    R Tbuf[(kLds + 2) * kLds];
-    R Cs[kLds * kLds];  // same layout as Ts; halo ring = +inf
+    // tile + halo ring (66 x 66 at offset kLds), plus one guard row above and below (the clamped
+    // r = -1 / 64 steps read one row beyond the halo: in-bounds, +inf, and masked by the +inf halo
+    // cost anyway); halo ring cost = +inf
+    Cell<R> Tc[(kLds + 2) * kLds];
     unsigned round, flags;
+    unsigned flags_acc; // persistent mode: neighbour activations deferred to the visit's end
+    unsigned pend;      // persistent mode: the tile's state word as the last pass consumed it
     unsigned key[5];    // min new value entering: self, N, S, W, E (f32 bits; ordered mode)
     int defer, tile, last;
     unsigned dirs;      // quadrant sweeps of this visit (bit w: wave w's direction)
 };
-static_assert(offsetof(TileLds<float>, Cs) == sizeof(float) * (kLds + 2) * kLds, "Cs must follow Tbuf");
-static_assert(offsetof(TileLds<double>, Cs) == sizeof(double) * (kLds + 2) * kLds, "Cs must follow Tbuf");
 
 // ---------------------------------------------------------------------------- tile body
 // Stage, sweep and write back one tile; leaves the activation decisions in L.flags (bits 0..3:
@@ -141,8 +146,7 @@ static_assert(offsetof(TileLds<double>, Cs) == sizeof(double) * (kLds + 2) * kLd
 template <typename R, bool COH>
 __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileLds<R>& L, R keep) {
     constexpr R INF = Real<R>::inf();
-    R* const Ts = L.Tbuf + kLds;
-    R* const Cs = L.Cs;
+    Cell<R>* const Ts = L.Tc + kLds;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int map = tile / a.tiles_per_map;
     const int rem = tile - map * a.tiles_per_map;
@@ -156,6 +160,8 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
     if (tid == 0) {
         L.round = 0;
         L.flags = 0;
+        L.flags_acc = 0;
+        L.pend = 0;
     }
     if (tid < 5) L.key[tid] = 0x7f800000u;
     // ---- stage the tile: 16 cells per thread (4 rows x 4 consecutive columns)
@@ -166,7 +172,7 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
         const int ry = (tid >> 4) + 16 * k;
         const int64_t gy = y0 + ry;
         R tv[4];
-        R* cr = &Cs[(ry + 1) * kLds + cx + 1];
+        R cr[4];
         if (full) {
             T.ld4(gy * a.W + x0 + cx, tv);
             if constexpr (sizeof(R) == 4) {
@@ -189,7 +195,7 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             told[4 * k + e] = tv[e];
-            Ts[(ry + 1) * kLds + cx + e + 1] = tv[e];
+            Ts[(ry + 1) * kLds + cx + e + 1] = Cell<R>{tv[e], cr[e]};
         }
     }
     // halo ring: wave 0 north row, 1 south row, 2 west column, 3 east column
@@ -204,9 +210,8 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
         else if (wave == 2) return load_T<R, COH>(a, T, y0 + lane, x0 - 1);
         else                return load_T<R, COH>(a, T, y0 + lane, x0 + kTile);
     };
-    Ts[h] = load_halo();
-    Cs[h] = INF;
-    if (lane < 4) Cs[(lane >> 1) * (kLds - 1) * kLds + (lane & 1) * (kLds - 1)] = INF;  // corners
+    Ts[h] = Cell<R>{load_halo(), INF};
+    if (lane < 4) Ts[(lane >> 1) * (kLds - 1) * kLds + (lane & 1) * (kLds - 1)].c = INF;  // corners
     __syncthreads();
     EIK_PROBE(1);
 
@@ -247,6 +252,12 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
         }
 
         EIK_PROBE(2);
+        // PERSISTENT mode, a.sched bit 0: consume the activations that reached this busy tile
+        // during the pass (neighbours' edges drained before their atomicOr, and this clear comes
+        // before the halo reload) -- an in-place pass then serves them instead of a re-queued
+        // visit.  Issued now, awaited with the write-back's drain.
+        unsigned pend_old = 0;
+        if (COH && (a.sched & 1) && tid == 0) pend_old = atomicAnd(&a.qstate[tile], kBusy | kVisited);
         // ---- write back changed cells, collect side flags (and entering values, ordered mode)
         unsigned fl = 0;
         R kmin_self = INF, kmin[4] = {INF, INF, INF, INF};
@@ -258,7 +269,7 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
             bool any = false;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                nv[e] = Ts[(ry + 1) * kLds + cx + e + 1];
+                nv[e] = Ts[(ry + 1) * kLds + cx + e + 1].t;
                 any |= nv[e] < told[4 * k + e];
                 if (nv[e] < told[4 * k + e] * keep) {
                     fl |= 128u;  // changed in this visit
@@ -266,10 +277,10 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
                     // A neighbour can only improve if this edge value undercuts the neighbour's
                     // adjacent cell (the halo value, stale => larger => conservative).
                     const int lx = cx + e + 1, ly = ry + 1;
-                    if (ry == 0 && nv[e] < Ts[lx]) { fl |= 1u; kmin[0] = umin(kmin[0], nv[e]); }
-                    if (ry == kTile - 1 && nv[e] < Ts[(kLds - 1) * kLds + lx]) { fl |= 2u; kmin[1] = umin(kmin[1], nv[e]); }
-                    if (cx + e == 0 && nv[e] < Ts[ly * kLds]) { fl |= 4u; kmin[2] = umin(kmin[2], nv[e]); }
-                    if (cx + e == kTile - 1 && nv[e] < Ts[ly * kLds + kLds - 1]) { fl |= 8u; kmin[3] = umin(kmin[3], nv[e]); }
+                    if (ry == 0 && nv[e] < Ts[lx].t) { fl |= 1u; kmin[0] = umin(kmin[0], nv[e]); }
+                    if (ry == kTile - 1 && nv[e] < Ts[(kLds - 1) * kLds + lx].t) { fl |= 2u; kmin[1] = umin(kmin[1], nv[e]); }
+                    if (cx + e == 0 && nv[e] < Ts[ly * kLds].t) { fl |= 4u; kmin[2] = umin(kmin[2], nv[e]); }
+                    if (cx + e == kTile - 1 && nv[e] < Ts[ly * kLds + kLds - 1].t) { fl |= 8u; kmin[3] = umin(kmin[3], nv[e]); }
                     const int64_t gx = x0 + cx + e;  // subdomain edges inside a partial tile (DD)
                     if (gy == a.H - 1 && ry != kTile - 1) fl |= 32u;
                     if (gx == a.W - 1 && cx + e != kTile - 1) fl |= 64u;
@@ -299,17 +310,28 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
                 if (kmin[q] < INF) atomicMin(&L.key[q + 1], __float_as_uint((float)kmin[q]));
         }
         if (tid == 0) L.last = a.max_rounds == 1 ? -1 : (int)last_changed;  // -1: see flags bit 7
+        if (COH && (a.sched & 1) && tid == 0) L.pend = pend_old;
         if constexpr (COH) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
         __syncthreads();
+        EIK_PROBE(7);
         if (COH) {
             const unsigned f = L.flags;  // uniform
-            if (!(f & 128u) || pass + 1 >= a.max_passes || a.max_rounds != 1) break;
+            const unsigned pend = L.pend & (kPending | kFromN | kFromS | kFromW | kFromE);
+            const bool self = (f & 128u) != 0u;
+            if ((!self && !pend) || pass + 1 >= a.max_passes || a.max_rounds != 1) break;
             if (tid == 0) charge_inplace_pass(a);  // in-place passes: stats and the visit budget
-            activate_neighbours(a, tile, f, L.key, 0, 0u);  // lanes 0..4 (T already drained)
-            dirs = 0xFu;  // a self revisit: every direction
-            Ts[h] = load_halo();
+            // a.sched bit 1: after the first pass, neighbour activations wait for the visit's end
+            // (one activation with the converged edges instead of one per pass)
+            const bool defer = (a.sched & 2) && pass > 0;
+            activate_neighbours(a, tile, defer ? 0u : f, L.key, 0, 0u);  // lanes 0..4 (T already drained)
+            if (defer && tid == 0) L.flags_acc |= f & 0x6fu;
+            dirs = self ? 0xFu : sweep_dirs(pend);  // a self revisit: every direction
+            Ts[h].t = load_halo();
             __syncthreads();  // every wave has read L.flags and its halo side is in
-            if (tid == 0) L.flags = 0;  // next OR-ed after the next sweep barrier
+            if (tid == 0) {
+                L.flags = 0;  // next OR-ed after the next sweep barrier
+                L.pend = 0;   // consumed by this pass
+            }
         } else {
             break;
         }
@@ -317,17 +339,22 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
     EIK_PROBE(3);
 }
 
-// Activations after a tile visit: the neighbours, and the tile itself if it changed.
+// Activations after a tile visit: the neighbours (with any deferred in-place ones), and the
+// tile itself if it changed -- or if it consumed activations (L.pend) it then did not serve.
 template <typename R>
 __device__ __forceinline__ void activate_after(const Fim2dArgs& a, int tile, const TileLds<R>& L, int list,
                                                unsigned stamp) {
     const unsigned f = L.flags;
-    activate_neighbours(a, tile, f, L.key, list, stamp);
-    if (threadIdx.x == 0 && (L.last < 0 ? (f & 128u) != 0u : L.last != 0)) {
-        if (a.mode == kModePersistent)
-            atomicOr(&a.qstate[tile], kPending | kSelf);  // busy: re-queued by its own finish
-        else
+    activate_neighbours(a, tile, f | L.flags_acc, L.key, list, stamp);
+    if (threadIdx.x == 0) {
+        const bool self = L.last < 0 ? (f & 128u) != 0u : L.last != 0;
+        if (a.mode == kModePersistent) {
+            const unsigned p = L.pend & (kFromN | kFromS | kFromW | kFromE);
+            if (self || (L.pend & kPending))
+                atomicOr(&a.qstate[tile], kPending | (self ? kSelf : p));  // busy: re-queued by its own finish
+        } else if (self) {
             enqueue(a, tile, list, stamp, __uint_as_float(L.key[0]));
+        }
     }
 }
 
@@ -335,8 +362,8 @@ template <typename R>
 __device__ __forceinline__ void init_guard_rows(TileLds<R>& L) {
     const int tid = threadIdx.x;
     if (tid < kLds) {
-        L.Tbuf[tid] = Real<R>::inf();
-        L.Tbuf[(kLds + 1) * kLds + tid] = Real<R>::inf();
+        L.Tc[tid] = Cell<R>{Real<R>::inf(), Real<R>::inf()};
+        L.Tc[(kLds + 1) * kLds + tid] = Cell<R>{Real<R>::inf(), Real<R>::inf()};
     }
 }
 
@@ -479,6 +506,7 @@ __global__ __launch_bounds__(kThreads) void fim2d_persist_kernel(Fim2dArgs a) {
         return;
     }
     init_guard_rows(L);
+    EIK_KSTART();
     const R keep = (R)a.keep;
     int tile = -1;
     unsigned nvis = 0;  // wave 0 lane 0: visits not yet added to the global counter
@@ -505,7 +533,7 @@ __global__ __launch_bounds__(kThreads) void fim2d_persist_kernel(Fim2dArgs a) {
             const int t = qgrab(a, trig);
             L.tile = t;
             L.dirs = sweep_dirs(trig);
-            if (t >= 0) EIK_VISIT(trig, L.dirs);
+            if (t >= 0) EIK_VISIT(t, trig, L.dirs);
         }
         __syncthreads();
         EIK_PROBE(6);

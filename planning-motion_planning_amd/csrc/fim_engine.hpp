@@ -13,6 +13,9 @@ namespace eik {
 // tile itself (last visit changed it: every direction)
 constexpr unsigned kPending = 1u, kBusy = 2u;
 constexpr unsigned kFromN = 4u, kFromS = 8u, kFromW = 16u, kFromE = 32u, kSelf = 64u;
+// set by the first grab of a tile and never cleared within a solve: a tile without it is FRESH --
+// its T is still +inf everywhere, and its first activation is the front arriving
+constexpr unsigned kVisited = 128u;
 
 // Quadrant sweeps that can carry the triggering information: wave 0 (+x,+y) and 1 (-x,+y) move
 // it away from the north edge, 2 and 3 from the south; 0 and 2 from the west, 1 and 3 from the
@@ -28,9 +31,18 @@ __device__ __forceinline__ unsigned sweep_dirs(unsigned trig) {
     if (trig & kFromE) d |= 0xAu;
     return d ? d : 0xFu;
 }
+// profiling hooks (tools/qprof.hip phase timers, tools/trace.hip event logs); no-ops here
 #ifndef EIK_PROBE
-#define EIK_PROBE(k) ((void)0)  // phase timing hooks (scratch profiling harness)
-#define EIK_VISIT(trig, dirs) ((void)0)
+#define EIK_PROBE(k) ((void)0)
+#endif
+#ifndef EIK_VISIT
+#define EIK_VISIT(tile, trig, dirs) ((void)0)
+#endif
+#ifndef EIK_ACT
+#define EIK_ACT(tile, old) ((void)0)
+#endif
+#ifndef EIK_KSTART
+#define EIK_KSTART() ((void)0)
 #endif
 
 // ------------------------------------------------------------------- memory access policy
@@ -195,16 +207,44 @@ __device__ __forceinline__ void enqueue(const Fim2dArgs& a, int tile, int list, 
     }
 }
 
-// PERSISTENT mode: append to the FIFO unless the tile is already pending (nothing to do) or
-// busy (its processor re-queues it when it finishes).
+// PERSISTENT mode: a FIFO of tiles, consumers take tickets (qgrab), producers append at the tail.
+// A FRESH tile's first activation is the front advancing into it, and the front's advance is the
+// solve's critical path (tools/trace.hip: on the 4096^2 DEM the chain of first visits from the
+// goal to the far corner waited 766 us of a 2.1 ms solve behind re-visits of tiles the front had
+// already passed).  So while the FIFO has a backlog (tail ahead of head: no workgroup waiting) a
+// fresh tile takes the slot of the NEXT ticket to be issued -- a CAS on that slot's old entry,
+// which is re-appended at the tail -- instead of queueing behind the backlog.  (A separate
+// priority FIFO polled by every grabber was tried: hundreds of workgroups CAS-ing its head
+// serialised for hundreds of microseconds.)
 __device__ __forceinline__ void qslot_put(const Fim2dArgs& a, int tile) {
     const unsigned long long pos = atomicAdd(a.qtail, 1ull);
     __hip_atomic_store(&a.qslot[pos & a.qmask], (unsigned)tile + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ void qslot_put_front(const Fim2dArgs& a, int tile) {
+    const unsigned long long h = __hip_atomic_load(a.qhead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long t = __hip_atomic_load(a.qtail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t > h + 1ull) {  // a backlog: slot h (the next ticket's) is filled, or about to be
+        unsigned* slot = &a.qslot[h & a.qmask];
+        const unsigned v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the ticket holder takes its slot with an exchange, so a CAS that wins lands before it
+        if (v != 0u && atomicCAS(slot, v, (unsigned)tile + 1u) == v) {
+            qslot_put(a, (int)(v - 1u));  // the displaced tile goes to the back (still pending)
+            return;
+        }
+    }
+    qslot_put(a, tile);
+}
+// Queue the tile unless it is already pending (nothing to do) or busy (its processor re-queues it
+// when it finishes).
 __device__ __forceinline__ void qpush(const Fim2dArgs& a, int tile, unsigned trig) {
-    if (atomicOr(&a.qstate[tile], kPending | trig) == 0u) {
+    const unsigned old = atomicOr(&a.qstate[tile], kPending | trig);
+    EIK_ACT(tile, old);
+    if ((old & (kPending | kBusy)) == 0u) {
         atomicAdd(a.qactive, 1);  // before the slot store: a waiter never sees "empty and idle"
-        qslot_put(a, tile);
+        if (!(old & kVisited) && a.fresh_first)
+            qslot_put_front(a, tile);
+        else
+            qslot_put(a, tile);
     }
 }
 
@@ -244,21 +284,20 @@ __device__ __forceinline__ void activate_neighbours(const Fim2dArgs& a, int tile
 
 // ------------------------------------------------------------------- PERSISTENT driver
 // Take a ticket and wait for its slot: the next queued tile, or -1 when the solve has ended
-// (no tile pending or busy) or failed.  ONE lane polls (relaxed agent-scope loads = sc1).
+// (no tile pending or busy) or failed.  ONE lane polls (relaxed agent-scope loads = sc1) and takes
+// the entry with an exchange (a producer may CAS a fresh tile into a filled slot, qslot_put_front).
 __device__ __forceinline__ int qgrab(const Fim2dArgs& a, unsigned& trig) {
     if (__hip_atomic_load(a.qerror, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return -1;
     const unsigned long long pos = atomicAdd(a.qhead, 1ull);
     unsigned* slot = &a.qslot[pos & a.qmask];
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     for (unsigned spin = 0;; ++spin) {
-        const unsigned v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (v != 0u) {
+        if (__hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
             // free the slot BEFORE the tile can be re-queued (slot reuse)
-            __hip_atomic_store(slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int tile = (int)(v - 1u);
+            const int tile = (int)(atomicExch(slot, 0u) - 1u);
             // pending -> busy before T is read: any activation from here on makes the finish
             // re-queue the tile, so no update is lost
-            trig = atomicExch(&a.qstate[tile], kBusy);  // consumed after the staging loads
+            trig = atomicExch(&a.qstate[tile], kBusy | kVisited);  // consumed after the staging loads
             return tile;
         }
         if ((spin & 7u) == 7u) {

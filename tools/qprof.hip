@@ -11,7 +11,7 @@
 __device__ unsigned long long* g_prof;
 #define EIK_PROBE(k) do { if (threadIdx.x == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memrealtime(); \
     unsigned long long* p_ = g_prof + blockIdx.x * 32; if (p_[15]) { p_[k] += t_ - p_[15]; p_[8 + k]++; } p_[15] = t_; } } while (0)
-#define EIK_VISIT(trig, dirs) do { unsigned long long* p_ = g_prof + blockIdx.x * 32; p_[16] += __builtin_popcount(dirs); p_[17] += ((trig) & 64u) ? 1 : 0; } while (0)
+#define EIK_VISIT(tile, trig, dirs) do { unsigned long long* p_ = g_prof + blockIdx.x * 32; p_[16] += __builtin_popcount(dirs); p_[17] += ((trig) & 64u) ? 1 : 0; } while (0)
 #include "../planning-motion_planning_amd/csrc/fim2d.hip"
 using namespace eik;
 #define CK(x) do { hipError_t e = (x); if (e) { printf("%s -> %s\n", #x, hipGetErrorString(e)); exit(2);} } while (0)
@@ -37,6 +37,8 @@ int main(int argc, char** argv) {
     a.qmask = qn - 1; CK(hipMalloc(&a.qslot, 4ull * qn)); CK(hipMalloc(&a.qstate, 4ull * tiles));
     a.qtimeout = 1000000000ull; a.qbudget = 1ull << 40; a.max_passes = 8;
     a.ls = 1; a.z0 = 0;
+    a.fresh_first = getenv("EIK_FRESH_FIRST") && atoi(getenv("EIK_FRESH_FIRST")) == 1;
+    a.sched = getenv("EIK_SCHED") ? atoi(getenv("EIK_SCHED")) : 0;
     int64_t* goals; CK(hipMalloc(&goals, 16)); int64_t hg[2] = {N / 2, N / 2}; CK(hipMemcpy(goals, hg, 16, hipMemcpyHostToDevice));
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     float ms = 0;

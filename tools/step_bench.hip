@@ -12,11 +12,11 @@ __global__ __launch_bounds__(256) void kern(const float* cost, float* out, unsig
     for (int i = tid; i < (kLds + 2) * kLds; i += 256) {
         const int row = i / kLds - 1, colx = i % kLds;
         const bool inner = row >= 1 && row <= kTile && colx >= 1 && colx <= kTile;
-        L.Tbuf[i] = (i % 97 == 0 && inner) ? 0.f : __builtin_inff();
-        if (row >= 0 && row < kLds) L.Cs[row * kLds + colx] = inner ? cost[(row - 1) * kTile + colx - 1] : __builtin_inff();
+        L.Tc[i].t = (i % 97 == 0 && inner) ? 0.f : __builtin_inff();
+        L.Tc[i].c = inner ? cost[(row - 1) * kTile + colx - 1] : __builtin_inff();
     }
     __syncthreads();
-    float* Ts = L.Tbuf + kLds;
+    Cell<float>* Ts = L.Tc + kLds;
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     for (int r = 0; r < reps; ++r) {
         if (wave == 0) sweep_quadrant<float, +1, +1, false>(Ts, lane, 1.f);
@@ -27,7 +27,7 @@ __global__ __launch_bounds__(256) void kern(const float* cost, float* out, unsig
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     if (tid == 0) cyc[blockIdx.x] = t1 - t0;
-    out[blockIdx.x * 256 + tid] = Ts[tid * 3 + kLds];
+    out[blockIdx.x * 256 + tid] = Ts[tid * 3 + kLds].t;
 }
 
 int main() {
