@@ -164,53 +164,73 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
         L.pend = 0;
     }
     if (tid < 5) L.key[tid] = 0x7f800000u;
-    // ---- stage the tile: 16 cells per thread (4 rows x 4 consecutive columns)
-    R told[16];
-    const int cx = (tid & 15) * 4;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int ry = (tid >> 4) + 16 * k;
-        const int64_t gy = y0 + ry;
-        R tv[4];
-        R cr[4];
-        if (full) {
-            T.ld4(gy * a.W + x0 + cx, tv);
-            if constexpr (sizeof(R) == 4) {
-                const float4 c4 = *reinterpret_cast<const float4*>(&cost[gy * a.W + x0 + cx]);
-                cr[0] = c4.x; cr[1] = c4.y; cr[2] = c4.z; cr[3] = c4.w;
-            } else {
-                const double2 c0 = *reinterpret_cast<const double2*>(&cost[gy * a.W + x0 + cx]);
-                const double2 c1 = *reinterpret_cast<const double2*>(&cost[gy * a.W + x0 + cx + 2]);
-                cr[0] = c0.x; cr[1] = c0.y; cr[2] = c1.x; cr[3] = c1.y;
-            }
-        } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int64_t gx = x0 + cx + e;
-                const bool in = gy < a.H && gx < a.W;
-                tv[e] = load_T<R, COH>(a, T, gy, gx);  // ghost cells land in padding
-                cr[e] = in ? cost[gy * a.W + gx] : INF;
-            }
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            told[4 * k + e] = tv[e];
-            Ts[(ry + 1) * kLds + cx + e + 1] = Cell<R>{tv[e], cr[e]};
-        }
-    }
     // halo ring: wave 0 north row, 1 south row, 2 west column, 3 east column
     int h;
     if (wave == 0)      h = 0 * kLds + lane + 1;
     else if (wave == 1) h = (kLds - 1) * kLds + lane + 1;
     else if (wave == 2) h = (lane + 1) * kLds + 0;
     else                h = (lane + 1) * kLds + kLds - 1;
+    // this lane's halo cell; in range of the raster: one unconditional load (no branch, so it
+    // issues together with the staging loads), else a ghost strip or +inf
+    const int64_t hy = wave == 0 ? y0 - 1 : wave == 1 ? y0 + kTile : y0 + lane;
+    const int64_t hx = wave == 0 || wave == 1 ? x0 + lane : wave == 2 ? x0 - 1 : x0 + kTile;
+    const bool h_in = hy >= 0 && hy < a.H && hx >= 0 && hx < a.W;
+    const int64_t h_idx = h_in ? hy * a.W + hx : 0;
     auto load_halo = [&]() {
-        if (wave == 0)      return load_T<R, COH>(a, T, y0 - 1, x0 + lane);
-        else if (wave == 1) return load_T<R, COH>(a, T, y0 + kTile, x0 + lane);
-        else if (wave == 2) return load_T<R, COH>(a, T, y0 + lane, x0 - 1);
-        else                return load_T<R, COH>(a, T, y0 + lane, x0 + kTile);
+        R v = T.ld(h_idx);
+        if (!h_in) v = load_T<R, COH>(a, T, hy, hx);
+        return v;
     };
-    Ts[h] = Cell<R>{load_halo(), INF};
+    // ---- stage the tile: 16 cells per thread (4 rows x 4 consecutive columns).  Every global
+    // load of the visit (T, cost, halo) is issued before the first LDS store, and each path does
+    // its own stores (no loaded value flows through a join, whose register copies would wait for
+    // the loads): the compiler does not move the sc1 buffer loads across LDS stores, and the
+    // interleaved form cost one memory round trip per row group (5 serial trips per staging).
+    R told[16];
+    const int cx = (tid & 15) * 4;
+    auto store_tile = [&](const R (&cr)[16], R hv) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int ry = (tid >> 4) + 16 * k;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) Ts[(ry + 1) * kLds + cx + e + 1] = Cell<R>{told[4 * k + e], cr[4 * k + e]};
+        }
+        Ts[h] = Cell<R>{hv, INF};
+    };
+    if (full) {
+        R cr[16];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t gy = y0 + (tid >> 4) + 16 * k;
+            R tv[4];
+            T.ld4(gy * a.W + x0 + cx, tv);
+            if constexpr (sizeof(R) == 4) {
+                const float4 c4 = *reinterpret_cast<const float4*>(&cost[gy * a.W + x0 + cx]);
+                cr[4 * k] = c4.x; cr[4 * k + 1] = c4.y; cr[4 * k + 2] = c4.z; cr[4 * k + 3] = c4.w;
+            } else {
+                const double2 c0 = *reinterpret_cast<const double2*>(&cost[gy * a.W + x0 + cx]);
+                const double2 c1 = *reinterpret_cast<const double2*>(&cost[gy * a.W + x0 + cx + 2]);
+                cr[4 * k] = c0.x; cr[4 * k + 1] = c0.y; cr[4 * k + 2] = c1.x; cr[4 * k + 3] = c1.y;
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) told[4 * k + e] = tv[e];
+        }
+        store_tile(cr, load_halo());
+    } else {
+        R cr[16];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t gy = y0 + (tid >> 4) + 16 * k;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int64_t gx = x0 + cx + e;
+                const bool in = gy < a.H && gx < a.W;
+                told[4 * k + e] = load_T<R, COH>(a, T, gy, gx);  // ghost cells land in padding
+                cr[4 * k + e] = in ? cost[gy * a.W + gx] : INF;
+            }
+        }
+        store_tile(cr, load_halo());
+    }
     if (lane < 4) Ts[(lane >> 1) * (kLds - 1) * kLds + (lane & 1) * (kLds - 1)].c = INF;  // corners
     __syncthreads();
     EIK_PROBE(1);

@@ -136,23 +136,6 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
 
     if (tid == 0) L.flags = 0;
     if (tid < 5) L.key[tid] = 0x7f800000u;
-    float told[16][NL];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const int ry = wave + 4 * j;
-        const int64_t gy = y0 + ry, gx = x0 + lane;
-        const bool in = gy < a.H && gx < a.W;
-        const int64_t gi = (gy * a.W + gx) * ls + a.z0;
-        float t4[4] = {INF, INF, INF, INF}, c4[4] = {INF, INF, INF, INF};
-#pragma unroll
-        for (int z = 0; z < NL; ++z) {
-            t4[z] = in ? T.ld(gi + z) : INF;
-            c4[z] = in ? cost[gi + z] : INF;
-            told[j][z] = t4[z];
-        }
-        Ts[(ry + 1) * kLds + lane + 1] = make_float4(t4[0], t4[1], t4[2], t4[3]);
-        Cs[(ry + 1) * kLds + lane + 1] = make_float4(c4[0], c4[1], c4[2], c4[3]);
-    }
     // halo ring: wave 0 north row, 1 south row, 2 west column, 3 east column (out of range: +inf)
     int h;
     int64_t hy, hx;
@@ -161,14 +144,62 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
     else if (wave == 2) { h = (lane + 1) * kLds + 0;        hy = y0 + lane;   hx = x0 - 1; }
     else                { h = (lane + 1) * kLds + kLds - 1; hy = y0 + lane;   hx = x0 + kTile; }
     const bool hin = hy >= 0 && hy < a.H && hx >= 0 && hx < a.W;
-    const int64_t hgi = (hy * a.W + hx) * ls + a.z0;
-    auto load_halo = [&]() {
+    const int64_t hgi = hin ? (hy * a.W + hx) * ls + a.z0 : 0;
+    auto load_halo = [&]() {  // unconditional loads (an in-range index), then the +inf select
         float v[4] = {INF, INF, INF, INF};
 #pragma unroll
-        for (int z = 0; z < NL; ++z) v[z] = hin ? T.ld(hgi + z) : INF;
+        for (int z = 0; z < NL; ++z) v[z] = T.ld(hgi + z);
+#pragma unroll
+        for (int z = 0; z < NL; ++z) v[z] = hin ? v[z] : INF;
         return make_float4(v[0], v[1], v[2], v[3]);
     };
-    Ts[h] = load_halo();
+    // ---- stage: every global load of the visit (T, cost, halo) is issued before the first LDS
+    // store and each path stores its own values (as fim2d.hip's process_tile; interleaved, the
+    // staging took one memory round trip per row, 16 in all)
+    float told[16][NL];
+    auto store_tile = [&](const float (&cc)[16][NL], float4 hv) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int ry = wave + 4 * j;
+            float t4[4] = {INF, INF, INF, INF}, c4[4] = {INF, INF, INF, INF};
+#pragma unroll
+            for (int z = 0; z < NL; ++z) {
+                t4[z] = told[j][z];
+                c4[z] = cc[j][z];
+            }
+            Ts[(ry + 1) * kLds + lane + 1] = make_float4(t4[0], t4[1], t4[2], t4[3]);
+            Cs[(ry + 1) * kLds + lane + 1] = make_float4(c4[0], c4[1], c4[2], c4[3]);
+        }
+        Ts[h] = hv;
+    };
+    if (y0 + kTile <= a.H && x0 + kTile <= a.W) {  // full tile: no per-cell range test
+        float cc[16][NL];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int64_t gi = ((y0 + wave + 4 * j) * a.W + x0 + lane) * ls + a.z0;
+#pragma unroll
+            for (int z = 0; z < NL; ++z) {
+                told[j][z] = T.ld(gi + z);
+                cc[j][z] = cost[gi + z];
+            }
+        }
+        store_tile(cc, load_halo());
+    } else {
+        float cc[16][NL];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int64_t gy = y0 + wave + 4 * j, gx = x0 + lane;
+            const bool in = gy < a.H && gx < a.W;
+            const int64_t gi = in ? (gy * a.W + gx) * ls + a.z0 : 0;
+#pragma unroll
+            for (int z = 0; z < NL; ++z) {
+                const float t = T.ld(gi + z), c = cost[gi + z];
+                told[j][z] = in ? t : INF;
+                cc[j][z] = in ? c : INF;
+            }
+        }
+        store_tile(cc, load_halo());
+    }
     Cs[h] = INF4;
     if (lane < 4) {
         const int corner = (lane >> 1) * (kLds - 1) * kLds + (lane & 1) * (kLds - 1);
