@@ -87,7 +87,8 @@ typedef enum {
                                 re-visits while the queue has a backlog (default 0: one FIFO)  */
     EIK_OPT_SCHED = 11       /* persistent mode, bit mask: 1 = a busy tile serves activations that
                                 reach it in place (no re-queued visit); 2 = after a visit's first
-                                pass, neighbour activations wait for the visit's end           */
+                                pass, neighbour activations wait for the visit's end (default 1:
+                                profiles/r02d_grab_sched_ab.log)                                 */
 } eik_option;
 
 typedef enum { EIK_MODE_LIST = 0, EIK_MODE_PERSISTENT = 1 } eik_mode;

@@ -63,7 +63,7 @@ struct eik_ctx {
     unsigned long long max_visits = 0;  // EIK_OPT_MAX_VISITS (0: per-solver default)
     int passes = 0;              // EIK_OPT_PASSES: in-place passes per persistent visit (0: adaptive)
     bool fresh_first = false;    // EIK_OPT_FRESH_FIRST: fresh tiles jump a backlogged FIFO
-    int sched = 0;               // EIK_OPT_SCHED: in-place scheduling of persistent visits
+    int sched = 1;               // EIK_OPT_SCHED: in-place scheduling of persistent visits
     int timing = 0;
     int grid = 0;
     eik_stats last{};

@@ -339,14 +339,17 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
             const unsigned pend = L.pend & (kPending | kFromN | kFromS | kFromW | kFromE);
             const bool self = (f & 128u) != 0u;
             if ((!self && !pend) || pass + 1 >= a.max_passes || a.max_rounds != 1) break;
-            if (tid == 0) charge_inplace_pass(a);  // in-place passes: stats and the visit budget
+            // the halo reload is issued first and the budget charge goes to wave 1, so wave 0's
+            // activation atomics are the only round trips the next pass waits for
+            const R hv = load_halo();
+            if (tid == 64) charge_inplace_pass(a);  // in-place passes: stats and the visit budget
             // a.sched bit 1: after the first pass, neighbour activations wait for the visit's end
             // (one activation with the converged edges instead of one per pass)
             const bool defer = (a.sched & 2) && pass > 0;
             activate_neighbours(a, tile, defer ? 0u : f, L.key, 0, 0u);  // lanes 0..4 (T already drained)
             if (defer && tid == 0) L.flags_acc |= f & 0x6fu;
             dirs = self ? 0xFu : sweep_dirs(pend);  // a self revisit: every direction
-            Ts[h].t = load_halo();
+            Ts[h].t = hv;
             __syncthreads();  // every wave has read L.flags and its halo side is in
             if (tid == 0) {
                 L.flags = 0;  // next OR-ed after the next sweep barrier

@@ -247,10 +247,13 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
         __syncthreads();
         const unsigned f = L.flags;  // uniform
         if (!(f & 128u) || pass + 1 >= kPasses) break;
-        if (tid == 0) charge_inplace_pass(a);  // in-place passes: stats and the visit budget
-        activate_neighbours(a, tile, f, L.key, 0, 0u);             // lanes 0..4 (T already drained)
+        // the halo reload is issued first and the budget charge goes to wave 1, so wave 0's
+        // activation atomics are the only round trips the next pass waits for
+        const float4 hv = load_halo();
+        if (tid == 64) charge_inplace_pass(a);  // in-place passes: stats and the visit budget
+        activate_neighbours(a, tile, f, L.key, 0, 0u);  // lanes 0..4 (T already drained)
         dirs = 0xFu;  // a self revisit: every direction
-        Ts[h] = load_halo();
+        Ts[h] = hv;
         __syncthreads();  // every wave has read L.flags and its halo side is in
         if (tid == 0) L.flags = 0;
     }

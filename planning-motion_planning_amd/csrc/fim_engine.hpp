@@ -292,9 +292,21 @@ __device__ __forceinline__ int qgrab(const Fim2dArgs& a, unsigned& trig) {
     unsigned* slot = &a.qslot[pos & a.qmask];
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     for (unsigned spin = 0;; ++spin) {
-        if (__hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
-            // free the slot BEFORE the tile can be re-queued (slot reuse)
-            const int tile = (int)(atomicExch(slot, 0u) - 1u);
+        const unsigned v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v != 0u) {
+            // free the slot BEFORE the tile can be re-queued (slot reuse).  Only fresh-first
+            // producers write a filled slot (their CAS): then the entry is taken with an exchange.
+            // Otherwise this ticket owns the slot alone (at most `grid` tickets are outstanding,
+            // far fewer than the slots, so no other holder polls it and the tail is a lap away):
+            // the value polled is the entry, and a relaxed store clears it -- one device-scope
+            // round trip less per grab.
+            int tile;
+            if (a.fresh_first) {
+                tile = (int)(atomicExch(slot, 0u) - 1u);
+            } else {
+                tile = (int)(v - 1u);
+                __hip_atomic_store(slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             // pending -> busy before T is read: any activation from here on makes the finish
             // re-queue the tile, so no update is lost
             trig = atomicExch(&a.qstate[tile], kBusy | kVisited);  // consumed after the staging loads

@@ -199,6 +199,36 @@ def test_pass_cap_option(passes):
         c.close()
 
 
+@pytest.mark.parametrize("opts", [(("SCHED", 0),), (("SCHED", 2),), (("SCHED", 3),), (("FRESH_FIRST", 1),),
+                                  (("SCHED", 0), ("FRESH_FIRST", 1))])
+def test_schedule_options(opts):
+    """The queue-scheduling options (EIK_OPT_SCHED other than the default 1, EIK_OPT_FRESH_FIRST)
+    change the order of tile visits, never the fixed point: single map and batch vs the oracle."""
+    import eikonal
+    from eikonal import _lib as L
+
+    c = eikonal.Context(0)
+    try:
+        for name, v in opts:
+            c.set_option(getattr(L, "OPT_" + name), v)
+        rng = np.random.default_rng(12)
+        cost = rng.uniform(1, 10, (640, 770))
+        cost[rng.random(cost.shape) < 0.15] = np.inf
+        cost = cost.astype(np.float32).astype(np.float64)
+        goal = [500, 120]
+        cost[goal[1], goal[0]] = 1.0
+        check_field(c.tmap2d(cost, goal, dtype=np.float32), oracle_field(cost, goal), goal, False)
+        costs = rng.uniform(1, 8, (3, 130, 260)).astype(np.float32)
+        goals = np.array([[3, 4], [250, 120], [128, 64]], np.int64)
+        for b in range(3):
+            costs[b, goals[b, 1], goals[b, 0]] = 1.0
+        T = c.tmap2d_batch(costs, goals)
+        for b in range(3):
+            check_field(T[b], oracle_field(costs[b], goals[b]), goals[b], False)
+    finally:
+        c.close()
+
+
 @pytest.mark.parametrize("neg", [False, True])
 def test_visit_budget_device_buffers(neg):
     """EIK_OPT_MAX_VISITS on the device-buffer entry (eik_fim2d_solve: no host-side cost check).
