@@ -85,10 +85,13 @@ typedef enum {
                                 24 for a single map, 2 for a batch of maps)                    */
     EIK_OPT_FRESH_FIRST = 10,/* persistent mode: 1 queues a tile's first activation ahead of
                                 re-visits while the queue has a backlog (default 0: one FIFO)  */
-    EIK_OPT_SCHED = 11       /* persistent mode, bit mask: 1 = a busy tile serves activations that
+    EIK_OPT_SCHED = 11,      /* persistent mode, bit mask: 1 = a busy tile serves activations that
                                 reach it in place (no re-queued visit); 2 = after a visit's first
                                 pass, neighbour activations wait for the visit's end (default 1:
                                 profiles/r02d_grab_sched_ab.log)                                 */
+    EIK_OPT_PATH_LOOP = 12   /* 2D path kernel: 1 (default) = one exit branch per step (the step is
+                                computed before its special cases are tested); 0 = the loop in
+                                the reference's statement order.  Same path bits either way.    */
 } eik_option;
 
 typedef enum { EIK_MODE_LIST = 0, EIK_MODE_PERSISTENT = 1 } eik_mode;

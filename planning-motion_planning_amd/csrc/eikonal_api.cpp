@@ -64,6 +64,7 @@ struct eik_ctx {
     int passes = 0;              // EIK_OPT_PASSES: in-place passes per persistent visit (0: adaptive)
     bool fresh_first = false;    // EIK_OPT_FRESH_FIRST: fresh tiles jump a backlogged FIFO
     int sched = 1;               // EIK_OPT_SCHED: in-place scheduling of persistent visits
+    int path_loop = 1;           // EIK_OPT_PATH_LOOP: 2D walker loop form
     int timing = 0;
     int grid = 0;
     eik_stats last{};
@@ -189,6 +190,7 @@ int eik_set_option(eik_ctx* c, int opt, double v) {
         case EIK_OPT_PASSES: c->passes = std::max(0, std::min(64, (int)v)); break;
         case EIK_OPT_FRESH_FIRST: c->fresh_first = v != 0; break;
         case EIK_OPT_SCHED: c->sched = std::max(0, std::min(3, (int)v)); break;
+        case EIK_OPT_PATH_LOOP: c->path_loop = v != 0; break;
         default: return set_err(c, EIK_ERR_ARG, "unknown option %d", opt);
     }
     return EIK_OK;
@@ -769,6 +771,7 @@ int eik_path2d_dev(eik_ctx* c, const void* d_T, int dtype, int64_t H, int64_t W,
     a.cap = cap;
     a.n_out = d_n_out;
     a.status = d_status;
+    a.fused = c->path_loop;
     HIPCHK(c, gdm2d(a, dtype == EIK_F64, (hipStream_t)stream));
     return EIK_OK;
 }

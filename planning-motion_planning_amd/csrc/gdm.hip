@@ -188,7 +188,7 @@ __device__ void path_builder(PathLds& s, const R* __restrict__ T, int64_t H, int
     }
 }
 
-template <typename R>
+template <typename R, bool FUSED>
 __global__ __launch_bounds__(kPathThreads) void gdm2d_kernel(Gdm2dArgs a) {
     __shared__ PathLds s;
     const R* __restrict__ T = static_cast<const R*>(a.T);
@@ -258,92 +258,173 @@ __global__ __launch_bounds__(kPathThreads) void gdm2d_kernel(Gdm2dArgs a) {
         hi_x = hi_x < (int)W - 2 ? hi_x : (int)W - 2;  // inside the bounds implies i + 1 < W, j + 1 < H
         hi_y = hi_y < (int)H - 2 ? hi_y : (int)H - 2;
     };
+    // Window bookkeeping of a step whose cell (i, j) left the fast bounds: errors (NaN point, out
+    // of range) set status and return false; else the corners are in window `cur` afterwards.
+    auto slow_step = [&](uint32_t i, uint32_t j) -> bool {
+        if (__builtin_isnan(px) || __builtin_isnan(py)) { status = kGdmError; return false; }
+        if (i + 1 >= (uint64_t)W || j + 1 >= (uint64_t)H) { status = kGdmError; return false; }
+        if (!inside(cur, i, j)) {  // the 2 x 2 interpolation corners left the window
+            const int nb = seq == 0 ? 0 : 1 - cur;
+            bool have = false;
+            if (pending) {
+                pending = false;
+                if (!wait_built()) { status = kGdmError; return false; }
+                have = inside(nb, i, j);
+            }
+            if (!have) {
+                issue(nb, i, j);
+                if (!wait_built()) { status = kGdmError; return false; }
+            }
+            cur = nb;
+        }
+        const int64_t cx0 = cur ? wx1 : wx0, cy0 = cur ? wy1 : wy0;
+        if (!pending && ((i - cx0 < kPrefetch && cx0 > 0) || (cx0 + kPW - 2 - i < kPrefetch && cx0 < xmax) ||
+                         (j - cy0 < kPrefetch && cy0 > 0) || (cy0 + kPW - 2 - j < kPrefetch && cy0 < ymax))) {
+            issue(1 - cur, i, j);
+            pending = true;
+        }
+        set_bounds();
+        return true;
+    };
+    // NaN fallback (:178-218) as the reference behaves under numpy 2: the neighbour probe
+    // `np.uint32(nearN + [0,-1])` raises OverflowError, caught at :217.  Lane 0 edits the path.
+    auto nan_fallback = [&]() {
+        if (lead) {
+            int64_t nx = (int64_t)__builtin_rint(px), ny = (int64_t)__builtin_rint(py);
+            bool empty = false, oob = false;
+            for (;;) {
+                const int64_t qx = nx < 0 ? nx + W : nx, qy = ny < 0 ? ny + H : ny;
+                if (qx < 0 || qy < 0 || qx >= W || qy >= H) { oob = true; break; }
+                if (!__builtin_isinf(tv(T, W, qy, qx))) break;
+                --n;
+                if (n == 0) { empty = true; break; }
+                nx = (int64_t)__builtin_rint(out[2 * (n - 1)]);
+                ny = (int64_t)__builtin_rint(out[2 * (n - 1) + 1]);
+            }
+            if (!empty && !oob) {
+                while (n > 0 && norm2(out[2 * (n - 1)] - (double)nx, out[2 * (n - 1) + 1] - (double)ny) < 1) --n;
+                if (n < a.cap) {
+                    out[2 * n] = (double)nx;
+                    out[2 * n + 1] = (double)ny;
+                    ++n;
+                }
+            }
+        }
+        status = kGdmFallback;
+    };
+    // One step's arithmetic from the four corners (g00, g01, g10, g11) of cell (i, j):
+    // :175-176 interpolation, :220-229 normalisation, :230 step.
+    struct StepOut {
+        double dx, dy, sx, sy;
+    };
+    auto step_math = [&](const double2& g00, const double2& g01, const double2& g10, const double2& g11, double fa,
+                         double fb) -> StepOut {
+        StepOut o;
+        o.dx = interp2_sel(fa, fb, g00.x, g01.x, g10.x, g11.x);  // :175
+        o.dy = interp2_sel(fa, fb, g00.y, g01.y, g10.y, g11.y);  // :176
+        // |(dx, dy)| is the same value in the test (:220) and both normalisations (:221-227)
+        const double nrm = __builtin_sqrt(o.dx * o.dx + o.dy * o.dy);
+        const double dxn = o.dx / nrm;  // both branches
+        // :220-224 (|g| < 0.01: unit step) or :225-229 (dy normalised with the normalised dx)
+        const double dyn = nrm < 0.01 ? o.dy / nrm : o.dy / __builtin_sqrt(dxn * dxn + o.dy * o.dy);
+        o.sx = px - tau * dxn;
+        o.sy = py - tau * dyn;
+        return o;
+    };
     // the point budget folded into the step count: point n = k + 1 is stored at step k (:173)
     const long kmax = a.steps < a.cap - 1 ? a.steps : a.cap - 1;
     long k = 0;
-    for (; k < kmax; ++k) {
-        EIK_P2PROBE(0);
-        const uint32_t i = (uint32_t)__builtin_trunc(px), j = (uint32_t)__builtin_trunc(py);
-        // one test on the chain: NaN point, out of range, or window bookkeeping due
-        if (__builtin_isnan(px + py) || (int)i < lo_x || (int)i > hi_x || (int)j < lo_y || (int)j > hi_y) {
-            if (__builtin_isnan(px) || __builtin_isnan(py)) { status = kGdmError; break; }
-            if (i + 1 >= (uint64_t)W || j + 1 >= (uint64_t)H) { status = kGdmError; break; }
-            if (!inside(cur, i, j)) {  // the 2 x 2 interpolation corners left the window
-                const int nb = seq == 0 ? 0 : 1 - cur;
-                bool have = false;
-                if (pending) {
-                    pending = false;
-                    if (!wait_built()) { status = kGdmError; break; }
-                    have = inside(nb, i, j);
-                }
-                if (!have) {
-                    issue(nb, i, j);
-                    if (!wait_built()) { status = kGdmError; break; }
-                }
-                cur = nb;
+    if constexpr (FUSED) {
+        // One exit per step: the step is computed before its special cases are known (window
+        // bookkeeping due, NaN gradient, stop radius, point budget), and a single uniform branch
+        // leaves the tight loop when any of them holds; the handler below then takes the same
+        // decisions as the reference-structured loop (the `else` branch) for that step.  The
+        // many uniform branches of that loop, each behind a VALU compare, cost more per step than
+        // the arithmetic they skip.  The LDS address of a step whose cell is outside the fast
+        // bounds is clamped into the window buffers (its values are discarded).
+        constexpr unsigned kWinBytes = sizeof(s.g[0]);
+        for (; k < kmax;) {
+            uint32_t i, j;
+            bool in;
+            StepOut o;
+            double fa, fb;
+            for (;;) {
+                EIK_P2PROBE(0);
+                i = (uint32_t)__builtin_trunc(px);
+                j = (uint32_t)__builtin_trunc(py);
+                in = !__builtin_isnan(px + py) && (int)i >= lo_x && (int)i <= hi_x && (int)j >= lo_y && (int)j <= hi_y;
+                unsigned off = (unsigned)(((int)j - cy0i) * kPW + ((int)i - cx0i)) * (unsigned)sizeof(double2);
+                off = off <= kWinBytes - (kPW + 2) * sizeof(double2) ? off : 0u;  // unsigned: negatives too
+                const double2* g = reinterpret_cast<const double2*>(reinterpret_cast<const char*>(s.g[cur]) + off);
+                EIK_P2PROBE(1);
+                fa = px - i;
+                fb = py - j;
+                o = step_math(g[0], g[1], g[kPW], g[kPW + 1], fa, fb);
+                EIK_P2PROBE(2);
+                const double ex = o.sx - a.ex, ey = o.sy - a.ey;
+                const bool stop = ex * ex + ey * ey < 2.25;  // :231-232, as in the loop below
+                EIK_P2PROBE(3);
+                // one branch: the conditions combined bitwise (a || chain becomes one branch each)
+                const bool leave = (int)!in | (int)__builtin_isnan(o.dx + o.dy) | (int)stop | (int)(k + 1 >= kmax);
+                if (leave) break;
+                *reinterpret_cast<double2*>(out + 2 * n) = make_double2(o.sx, o.sy);
+                ++n;
+                px = o.sx;
+                py = o.sy;
+                ++k;
             }
-            const int64_t cx0 = cur ? wx1 : wx0, cy0 = cur ? wy1 : wy0;
-            if (!pending && ((i - cx0 < kPrefetch && cx0 > 0) || (cx0 + kPW - 2 - i < kPrefetch && cx0 < xmax) ||
-                             (j - cy0 < kPrefetch && cy0 > 0) || (cy0 + kPW - 2 - j < kPrefetch && cy0 < ymax))) {
-                issue(1 - cur, i, j);
-                pending = true;
+            if (!in) {  // window bookkeeping (or an error), then this step again
+                if (!slow_step(i, j)) break;
+                const int li = (int)i - cx0i, lj = (int)j - cy0i;
+                o = step_math(s.g[cur][lj][li], s.g[cur][lj][li + 1], s.g[cur][lj + 1][li], s.g[cur][lj + 1][li + 1],
+                              fa, fb);
             }
-            set_bounds();
-        }
-        EIK_P2PROBE(1);
-        const int li = (int)i - cx0i, lj = (int)j - cy0i;
-        const double2 g00 = s.g[cur][lj][li], g01 = s.g[cur][lj][li + 1];
-        const double2 g10 = s.g[cur][lj + 1][li], g11 = s.g[cur][lj + 1][li + 1];
-        const double fa = px - i, fb = py - j;
-        double dx = interp2_sel(fa, fb, g00.x, g01.x, g10.x, g11.x);  // :175
-        double dy = interp2_sel(fa, fb, g00.y, g01.y, g10.y, g11.y);  // :176
-        EIK_P2PROBE(2);
-        // |(dx, dy)| is the same value in the test (:220) and both normalisations (:221-227)
-        const double nrm = __builtin_sqrt(dx * dx + dy * dy);
-        const double dxn = dx / nrm;  // both branches
-        // :220-224 (|g| < 0.01: unit step) or :225-229 (dy normalised with the already-normalised dx)
-        const double dyn = nrm < 0.01 ? dy / nrm : dy / __builtin_sqrt(dxn * dxn + dy * dy);
-        const double sx = px - tau * dxn, sy = py - tau * dyn;
-        // :231-232  sqrt(e) < 1.5  <=>  e < 2.25 for a correctly rounded sqrt (2.25 = 1.5^2 exactly)
-        const double ex = sx - a.ex, ey = sy - a.ey;
-        const bool stop = ex * ex + ey * ey < 2.25;
-        EIK_P2PROBE(3);
-        // one test after the step: a NaN gradient (the fallback: nothing of this step is kept)
-        // or the stop radius; NaN in dx + dy also catches inf - inf, re-tested precisely
-        if (__builtin_isnan(dx + dy) || stop) {
-            if (__builtin_isnan(dx) || __builtin_isnan(dy)) {
-                // NaN fallback (:178-218) as the reference behaves under numpy 2: the neighbour
-                // probe `np.uint32(nearN + [0,-1])` raises OverflowError, caught at :217.
-                if (lead) {
-                    int64_t nx = (int64_t)__builtin_rint(px), ny = (int64_t)__builtin_rint(py);
-                    bool empty = false, oob = false;
-                    for (;;) {
-                        const int64_t qx = nx < 0 ? nx + W : nx, qy = ny < 0 ? ny + H : ny;
-                        if (qx < 0 || qy < 0 || qx >= W || qy >= H) { oob = true; break; }
-                        if (!__builtin_isinf(tv(T, W, qy, qx))) break;
-                        --n;
-                        if (n == 0) { empty = true; break; }
-                        nx = (int64_t)__builtin_rint(out[2 * (n - 1)]);
-                        ny = (int64_t)__builtin_rint(out[2 * (n - 1) + 1]);
-                    }
-                    if (!empty && !oob) {
-                        while (n > 0 && norm2(out[2 * (n - 1)] - (double)nx, out[2 * (n - 1) + 1] - (double)ny) < 1) --n;
-                        if (n < a.cap) {
-                            out[2 * n] = (double)nx;
-                            out[2 * n + 1] = (double)ny;
-                            ++n;
-                        }
-                    }
-                }
-                status = kGdmFallback;
+            // the reference-structured loop's end of step
+            const double ex = o.sx - a.ex, ey = o.sy - a.ey;
+            const bool stop = ex * ex + ey * ey < 2.25;
+            if (__builtin_isnan(o.dx) || __builtin_isnan(o.dy)) {
+                nan_fallback();
                 break;
             }
+            *reinterpret_cast<double2*>(out + 2 * n) = make_double2(o.sx, o.sy);
+            ++n;
+            px = o.sx;
+            py = o.sy;
+            if (stop) break;  // k counts completed non-final steps, as the for loop's ++k
+            if (++k >= kmax) break;
         }
-        *reinterpret_cast<double2*>(out + 2 * n) = make_double2(sx, sy);  // every lane: same address and value
-        ++n;
-        px = sx;
-        py = sy;
-        if (stop) break;
+    } else {
+        for (; k < kmax; ++k) {
+            EIK_P2PROBE(0);
+            const uint32_t i = (uint32_t)__builtin_trunc(px), j = (uint32_t)__builtin_trunc(py);
+            // one test on the chain: NaN point, out of range, or window bookkeeping due
+            if (__builtin_isnan(px + py) || (int)i < lo_x || (int)i > hi_x || (int)j < lo_y || (int)j > hi_y) {
+                if (!slow_step(i, j)) break;
+            }
+            EIK_P2PROBE(1);
+            const int li = (int)i - cx0i, lj = (int)j - cy0i;
+            const double fa = px - i, fb = py - j;
+            const StepOut o = step_math(s.g[cur][lj][li], s.g[cur][lj][li + 1], s.g[cur][lj + 1][li],
+                                        s.g[cur][lj + 1][li + 1], fa, fb);
+            EIK_P2PROBE(2);
+            // :231-232  sqrt(e) < 1.5  <=>  e < 2.25 for a correctly rounded sqrt (2.25 = 1.5^2 exactly)
+            const double ex = o.sx - a.ex, ey = o.sy - a.ey;
+            const bool stop = ex * ex + ey * ey < 2.25;
+            EIK_P2PROBE(3);
+            // one test after the step: a NaN gradient (the fallback: nothing of this step is kept)
+            // or the stop radius; NaN in dx + dy also catches inf - inf, re-tested precisely
+            if (__builtin_isnan(o.dx + o.dy) || stop) {
+                if (__builtin_isnan(o.dx) || __builtin_isnan(o.dy)) {
+                    nan_fallback();
+                    break;
+                }
+            }
+            *reinterpret_cast<double2*>(out + 2 * n) = make_double2(o.sx, o.sy);  // every lane: same address and value
+            ++n;
+            px = o.sx;
+            py = o.sy;
+            if (stop) break;
+        }
     }
     if (k == kmax && kmax < a.steps && status == kGdmDone) status = kGdmError;  // out of point budget
     __hip_atomic_store(&s.req_seq, -1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);  // builders exit
@@ -360,10 +441,13 @@ __global__ __launch_bounds__(kPathThreads) void gdm2d_kernel(Gdm2dArgs a) {
 }
 
 hipError_t gdm2d(const Gdm2dArgs& a, bool f64, hipStream_t st) {
-    if (f64)
-        hipLaunchKernelGGL(gdm2d_kernel<double>, dim3(1), dim3(kPathThreads), 0, st, a);
-    else
-        hipLaunchKernelGGL(gdm2d_kernel<float>, dim3(1), dim3(kPathThreads), 0, st, a);
+    if (f64) {
+        if (a.fused) hipLaunchKernelGGL((gdm2d_kernel<double, true>), dim3(1), dim3(kPathThreads), 0, st, a);
+        else        hipLaunchKernelGGL((gdm2d_kernel<double, false>), dim3(1), dim3(kPathThreads), 0, st, a);
+    } else {
+        if (a.fused) hipLaunchKernelGGL((gdm2d_kernel<float, true>), dim3(1), dim3(kPathThreads), 0, st, a);
+        else        hipLaunchKernelGGL((gdm2d_kernel<float, false>), dim3(1), dim3(kPathThreads), 0, st, a);
+    }
     return hipGetLastError();
 }
 

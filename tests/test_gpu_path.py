@@ -125,3 +125,53 @@ def test_path_device_fp32_field(ctx):
     path = out[:k].cpu().numpy()
     assert k == len(ref) and int(st.item()) == rst
     assert np.abs(path - ref).max() < 1e-3  # fp32 field vs fp64 field (BASELINE.md path tolerance)
+
+
+def _walker_fields():
+    """Fields for the walker-loop check: the golden fields (ties, obstacles, NaN
+    fallbacks), a large smooth field (many windows), a V-shaped valley (interpolated gradients
+    cancel: |g| < 0.01 unit steps, tiny operands) and fields with obstacles."""
+    import oracle as O2
+
+    out = []
+    rng = np.random.default_rng(21)
+    for H, W, p_inf in ((1500, 1700, 0.0), (600, 500, 0.08), (300, 900, 0.2)):
+        cost = rng.uniform(1, 6, (H, W))
+        cost[rng.random((H, W)) < p_inf] = np.inf
+        cost[0, :] = cost[-1, :] = cost[:, 0] = cost[:, -1] = np.inf
+        goal = (W - 40, H - 30)
+        cost[goal[1], goal[0]] = 1.0
+        O2.set_strict(False)
+        out.append((O2.fmm2d(cost, goal), (25.3, 31.7), goal))
+    yy, xx = np.mgrid[0:400, 0:400].astype(np.float64)
+    valley = np.abs(xx - 200.0) * 3 + (399 - yy)  # descent runs into the x = 200 crease
+    out.append((valley, (37.5, 12.25), (200.0, 395.0)))
+    return out
+
+
+@pytest.mark.parametrize("tau", [0.5, 1.7])
+def test_walker_loop_forms_bit_identical(golden, tau):
+    """EIK_OPT_PATH_LOOP: the single-exit step loop (default) and the loop in the reference's
+    statement order return the SAME bits (array_equal, same status) -- on the golden fields and on fields that
+    exercise window switches, NaN fallbacks, |g| < 0.01 unit steps and, at tau = 1.7, points that
+    move more than one cell per step (the walker's slow path)."""
+    import eikonal
+    from eikonal import _lib as L
+
+    cases = []
+    d = golden("fmm2d_fields")
+    for i in range(12):
+        p = f"c{i}_"
+        cases.append((d[p + "T"], _f(d[p + "start"]), _f(d[p + "goal"])))
+    cases += _walker_fields()
+    c0, c1 = eikonal.Context(0), eikonal.Context(0)
+    try:
+        c0.set_option(L.OPT_PATH_LOOP, 0)
+        c1.set_option(L.OPT_PATH_LOOP, 1)
+        for T, s, g in cases:
+            a, sa = c0.path2d(T, _f(s), _f(g), tau)
+            b, sb = c1.path2d(T, _f(s), _f(g), tau)
+            assert sa == sb and a.shape == b.shape and np.array_equal(a, b)
+    finally:
+        c0.close()
+        c1.close()

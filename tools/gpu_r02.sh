@@ -22,7 +22,7 @@ for v in "${VARS[@]}"; do
   if [ -z "$NO_TRACE" ]; then
     ff=$(echo "$opt" | grep -o "FRESH_FIRST=[01]" | cut -d= -f2 || true)
     sc=$(echo "$opt" | grep -o "SCHED=[0-9]" | cut -d= -f2 || true)
-    EIK_FRESH_FIRST=${ff:-0} EIK_SCHED=${sc:-0} bash tools/gpu_trace.sh > /dev/null || { echo trace failed; cat $O/trace.txt; exit 1; }
+    EIK_FRESH_FIRST=${ff:-0} EIK_SCHED=${sc:-1} bash tools/gpu_trace.sh > /dev/null || { echo trace failed; cat $O/trace.txt; exit 1; }
     cp $O/trace.txt "$O/${TAG}_trace_${v//[^A-Za-z0-9_]/_}.txt"; echo "trace [$v]"; grep -E "kernel|critical|busy" $O/trace.txt
   fi
 done

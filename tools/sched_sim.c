@@ -6,7 +6,8 @@
  * adjacent cells an improved edge undercuts are activated.  A held tile stays (in place) while it
  * changes or was activated meanwhile, up to `passes`; then it is released (re-queued if still
  * changing).  Policies: 0 FIFO (the GPU's queue), 1 smallest entering value first (the key of an
- * activation is the smallest improved edge value).
+ * activation is the smallest improved edge value), 2 buckets of width delta (then FIFO), 3 the first
+ * activation of a never-visited tile (the front) ahead of the FIFO.
  *   gcc -O3 -march=native -o /tmp/sched_sim tools/sched_sim.c -lm
  *   /tmp/sched_sim cost.f32 N policy passes K
  */
@@ -45,6 +46,8 @@ static HE hpop(void) {
     return r;
 }
 static int* fifo; static size_t fh, ft, fcap;
+static int* ffifo; static size_t ffh, fft;  /* policy 3: first activations of never-visited tiles */
+static unsigned char* visited;
 
 static void activate(int t, float k) {
     if (k < key_of[t]) key_of[t] = k;
@@ -57,10 +60,13 @@ static void activate(int t, float k) {
     if (held[t]) return;  /* served in place by its worker */
     if (policy == 1) hpush(key_of[t], t);
     else if (policy == 2) hpush(floor(key_of[t] / delta) * 1e9 + (double)(seq++), t);  /* bucket, then FIFO */
+    else if (policy == 3 && !visited[t]) ffifo[(fft++) % fcap] = t;
     else fifo[(ft++) % fcap] = t;
 }
 static int take(void) {
-    if (policy) {
+    if (policy == 3)
+        while (ffh != fft) { int t = ffifo[(ffh++) % fcap]; if (pend[t] && !held[t]) return t; }
+    if (policy && policy != 3) {
         while (hn) {
             HE e = hpop();
             if (pend[e.t] && !held[e.t] &&
@@ -86,6 +92,7 @@ int main(int argc, char** argv) {
     FILE* f = fopen(cf, "rb"); if (!f || fread(cost, 4, (size_t)N * N, f) != (size_t)N * N) { printf("bad cost\n"); return 1; } fclose(f);
     for (size_t i = 0; i < (size_t)N * N; ++i) T[i] = INFINITY;
     heap = malloc(sizeof(HE) * 256L * nt); fcap = 16L * nt; fifo = malloc(sizeof(int) * fcap);
+    ffifo = malloc(sizeof(int) * fcap); visited = calloc(nt, 1);
     for (int i = 0; i < nt; ++i) key_of[i] = INFINITY;
     T[(size_t)(N / 2) * N + N / 2] = 0.f;
     activate((N / 2 / TS) * NT + N / 2 / TS, 0.f);
@@ -101,7 +108,7 @@ int main(int argc, char** argv) {
             if (W[k].t < 0) {
                 int t = take();
                 if (t < 0) continue;
-                held[t] = 1; pend[t] = 0; key_of[t] = INFINITY; ++visits;
+                held[t] = 1; pend[t] = 0; key_of[t] = INFINITY; ++visits; visited[t] = 1;
                 W[k].t = t; W[k].p = 0;
                 int ty = t / NT, tx = t % NT, y0 = ty * TS, x0 = tx * TS;
                 for (int y = -1; y <= TS; ++y)

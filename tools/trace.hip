@@ -55,7 +55,7 @@ int main(int argc, char** argv) {
     a.qtimeout = 1000000000ull; a.qbudget = 1ull << 40; a.max_passes = passes;
     a.ls = 1; a.z0 = 0;
     a.fresh_first = getenv("EIK_FRESH_FIRST") && atoi(getenv("EIK_FRESH_FIRST")) == 1;
-    a.sched = getenv("EIK_SCHED") ? atoi(getenv("EIK_SCHED")) : 0;
+    a.sched = getenv("EIK_SCHED") ? atoi(getenv("EIK_SCHED")) : 1;  // library default
     int64_t* goals; CK(hipMalloc(&goals, 16)); int64_t hg[2] = {N / 2, N / 2}; CK(hipMemcpy(goals, hg, 16, hipMemcpyHostToDevice));
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     float ms = 0;
