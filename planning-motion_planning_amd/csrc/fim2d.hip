@@ -164,16 +164,22 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
         L.pend = 0;
     }
     if (tid < 5) L.key[tid] = 0x7f800000u;
-    // halo ring: wave 0 north row, 1 south row, 2 west column, 3 east column
+    // halo ring: wave 0 north row, 1 south row, 2 west column, 3 east column.  In a tile cut by
+    // the raster's south / east end the south row / east column is the one just past the raster
+    // (row H / column W) inside the tile: a subdomain's ghost strip lives there, and the in-place
+    // passes' halo reload must refresh it like any halo (the cells beyond it are +inf cost, so
+    // the ring's own row / column is never an upstream value of a finite-cost cell).
+    const int64_t sy = y0 + kTile < a.H ? y0 + kTile : a.H;
+    const int64_t sx = x0 + kTile < a.W ? x0 + kTile : a.W;
     int h;
     if (wave == 0)      h = 0 * kLds + lane + 1;
-    else if (wave == 1) h = (kLds - 1) * kLds + lane + 1;
+    else if (wave == 1) h = (int)(sy - y0 + 1) * kLds + lane + 1;
     else if (wave == 2) h = (lane + 1) * kLds + 0;
-    else                h = (lane + 1) * kLds + kLds - 1;
+    else                h = (lane + 1) * kLds + (int)(sx - x0 + 1);
     // this lane's halo cell; in range of the raster: one unconditional load (no branch, so it
     // issues together with the staging loads), else a ghost strip or +inf
-    const int64_t hy = wave == 0 ? y0 - 1 : wave == 1 ? y0 + kTile : y0 + lane;
-    const int64_t hx = wave == 0 || wave == 1 ? x0 + lane : wave == 2 ? x0 - 1 : x0 + kTile;
+    const int64_t hy = wave == 0 ? y0 - 1 : wave == 1 ? sy : y0 + lane;
+    const int64_t hx = wave == 0 || wave == 1 ? x0 + lane : wave == 2 ? x0 - 1 : sx;
     const bool h_in = hy >= 0 && hy < a.H && hx >= 0 && hx < a.W;
     const int64_t h_idx = h_in ? hy * a.W + hx : 0;
     auto load_halo = [&]() {
@@ -291,7 +297,8 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
             for (int e = 0; e < 4; ++e) {
                 nv[e] = Ts[(ry + 1) * kLds + cx + e + 1].t;
                 any |= nv[e] < told[4 * k + e];
-                if (nv[e] < told[4 * k + e] * keep) {
+                // (a ghost cell inside a cut tile is lowered by the halo reload, never by a sweep)
+                if (nv[e] < told[4 * k + e] * keep && (full || (gy < a.H && x0 + cx + e < a.W))) {
                     fl |= 128u;  // changed in this visit
                     kmin_self = umin(kmin_self, nv[e]);
                     // A neighbour can only improve if this edge value undercuts the neighbour's
