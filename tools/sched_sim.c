@@ -7,7 +7,9 @@
  * changes or was activated meanwhile, up to `passes`; then it is released (re-queued if still
  * changing).  Policies: 0 FIFO (the GPU's queue), 1 smallest entering value first (the key of an
  * activation is the smallest improved edge value), 2 buckets of width delta (then FIFO), 3 the first
- * activation of a never-visited tile (the front) ahead of the FIFO.
+ * activation of a never-visited tile (the front) ahead of the FIFO, 4 as 2 but a queued tile keeps the
+ * bucket of the activation that queued it (no re-push on a lower key; a released tile that still
+ * changes is re-queued with the smallest value it changed to -- the GPU's bucket queue).
  *   gcc -O3 -march=native -o /tmp/sched_sim tools/sched_sim.c -lm
  *   /tmp/sched_sim cost.f32 N policy passes K
  */
@@ -59,7 +61,7 @@ static void activate(int t, float k) {
     pend[t] = 1;
     if (held[t]) return;  /* served in place by its worker */
     if (policy == 1) hpush(key_of[t], t);
-    else if (policy == 2) hpush(floor(key_of[t] / delta) * 1e9 + (double)(seq++), t);  /* bucket, then FIFO */
+    else if (policy == 2 || policy == 4) hpush(floor(key_of[t] / delta) * 1e9 + (double)(seq++), t);  /* bucket, then FIFO */
     else if (policy == 3 && !visited[t]) ffifo[(fft++) % fcap] = t;
     else fifo[(ft++) % fcap] = t;
 }
@@ -70,7 +72,7 @@ static int take(void) {
         while (hn) {
             HE e = hpop();
             if (pend[e.t] && !held[e.t] &&
-                (policy == 2 ? floor(e.k / 1e9) == floor(key_of[e.t] / delta) : e.k == key_of[e.t])) return e.t;
+                (policy == 4 || (policy == 2 ? floor(e.k / 1e9) == floor(key_of[e.t] / delta) : e.k == key_of[e.t]))) return e.t;
         }
         return -1;
     }
@@ -78,7 +80,7 @@ static int take(void) {
     return -1;
 }
 
-typedef struct { int t, p; float L[TS + 2][TS + 2], C[TS + 2][TS + 2]; } Work;
+typedef struct { int t, p; float kmin; float L[TS + 2][TS + 2], C[TS + 2][TS + 2]; } Work;
 
 int main(int argc, char** argv) {
     const char* cf = argv[1]; N = atoi(argv[2]); policy = atoi(argv[3]);
@@ -170,7 +172,7 @@ int main(int argc, char** argv) {
             if (ke[1] < INFINITY && ty + 1 < NT) activate(t + NT, ke[1]);
             if (ke[2] < INFINITY && tx > 0) activate(t - 1, ke[2]);
             if (ke[3] < INFINITY && tx + 1 < NT) activate(t + 1, ke[3]);
-            (void)kmin;
+            W[k].kmin = kmin;
         }
         for (int k = 0; k < K; ++k) {
             if (W[k].t < 0) continue;
@@ -178,7 +180,7 @@ int main(int argc, char** argv) {
             int go_on = changed[k] || pend[t];
             if (go_on && W[k].p < maxp) continue;  /* in place next round */
             held[t] = 0; W[k].t = -1;
-            if (go_on) { pend[t] = 0; activate(t, 0.f); }  /* re-queue (key: keep order fair) */
+            if (go_on) { pend[t] = 0; activate(t, policy == 4 && !getenv("REQ0") ? W[k].kmin : 0.f); }  /* re-queue (key: keep order fair) */
         }
     }
     double s = 0; long fin = 0;
