@@ -89,9 +89,11 @@ typedef enum {
                                 reach it in place (no re-queued visit); 2 = after a visit's first
                                 pass, neighbour activations wait for the visit's end (default 1:
                                 profiles/r02d_grab_sched_ab.log)                                 */
-    EIK_OPT_PATH_LOOP = 12   /* 2D path kernel: 1 (default) = one exit branch per step (the step is
-                                computed before its special cases are tested); 0 = the loop in
-                                the reference's statement order.  Same path bits either way.    */
+    EIK_OPT_PATH_LOOP = 12   /* 2D path kernel: 2 (default) = one exit branch per step (the step is
+                                computed before its special cases are tested) with the f64 sqrt /
+                                division free of range handling inside their safe domain; 1 = the
+                                same loop with the compiler's sqrt / division; 0 = the loop in
+                                the reference's statement order.  Same path bits in all three.  */
 } eik_option;
 
 typedef enum { EIK_MODE_LIST = 0, EIK_MODE_PERSISTENT = 1 } eik_mode;

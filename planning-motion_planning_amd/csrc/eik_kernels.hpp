@@ -110,7 +110,8 @@ struct Gdm2dArgs {
     int64_t cap;
     int64_t* n_out;        // device
     int* status;           // device
-    int fused;             // 1: single-exit step loop (EIK_OPT_PATH_LOOP), 0: reference-structured loop
+    int fused;             // EIK_OPT_PATH_LOOP: 2 single-exit loop + range-free sqrt/div, 1 single-exit loop,
+                           // 0 reference-structured loop (same path bits)
 };
 hipError_t gdm2d(const Gdm2dArgs& a, bool f64, hipStream_t st);
 

@@ -64,7 +64,7 @@ struct eik_ctx {
     int passes = 0;              // EIK_OPT_PASSES: in-place passes per persistent visit (0: adaptive)
     bool fresh_first = false;    // EIK_OPT_FRESH_FIRST: fresh tiles jump a backlogged FIFO
     int sched = 1;               // EIK_OPT_SCHED: in-place scheduling of persistent visits
-    int path_loop = 1;           // EIK_OPT_PATH_LOOP: 2D walker loop form
+    int path_loop = 2;           // EIK_OPT_PATH_LOOP: 2D walker loop form (profiles/r02i_path_walker.log)
     int timing = 0;
     int grid = 0;
     eik_stats last{};
@@ -190,7 +190,7 @@ int eik_set_option(eik_ctx* c, int opt, double v) {
         case EIK_OPT_PASSES: c->passes = std::max(0, std::min(64, (int)v)); break;
         case EIK_OPT_FRESH_FIRST: c->fresh_first = v != 0; break;
         case EIK_OPT_SCHED: c->sched = std::max(0, std::min(3, (int)v)); break;
-        case EIK_OPT_PATH_LOOP: c->path_loop = v != 0; break;
+        case EIK_OPT_PATH_LOOP: c->path_loop = std::max(0, std::min(2, (int)v)); break;
         default: return set_err(c, EIK_ERR_ARG, "unknown option %d", opt);
     }
     return EIK_OK;

@@ -79,6 +79,55 @@ __device__ __forceinline__ double interp2_sel(double a, double b, double g00, do
 
 __device__ __forceinline__ double norm2(double a, double b) { return __builtin_sqrt(a * a + b * b); }
 
+// Correctly rounded f64 square root and division exactly as the compiler lowers them for gfx950,
+// minus the range handling: the same operations in the same order, so the same bits wherever
+// that handling is the identity.  sqrt: the input scaling (x < 2^-767) and its undo are
+// identities for x >= 2^-767 (and the compiler's final select, which keeps +-0 and +inf, is one
+// for finite x > 0, so it is left out: the walker never takes x = 0 or +inf here).  n / d: v_div_scale_f64 leaves
+// both operands as they are and v_div_fmas_f64 is a plain fma when d is normal in
+// [2^-900, 2^100], n is 0 or normal with |n| >= 2^-900 and |n| <= |d|; v_div_fixup_f64 then only
+// forces the sign of the quotient to sign(n) ^ sign(d), which it already has -- except a zero
+// quotient of n = -0, which comes out +0 here (only ever squared or subtracted later: same path
+// bits).  The walker takes these on its fast path and leaves it for the exact forms outside
+// that domain (walk_odd).
+__device__ __forceinline__ double sqrt_core(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = y * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    double d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, x);
+    return __builtin_fma(d, h, g);
+}
+__device__ __forceinline__ double div_core(double n, double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    double e = __builtin_fma(-d, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-d, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    const double q = n * r;
+    e = __builtin_fma(-d, q, n);
+    return __builtin_fma(e, r, q);
+}
+// interpolatePoint's general case (:336) for every (a, b): where a == 0 or b == 0 it equals the
+// special cases of :327-334 bit for bit (the skipped terms are exact zeros added to a nonzero
+// sum; only the sign of a zero result can differ) as long as the four corners are finite; a NaN
+// corner makes |g|^2 NaN, and walk_odd sends the step to the exact form.
+__device__ __forceinline__ double interp2_general(double a, double b, double g00, double g01, double g10, double g11) {
+    const double a10 = g01 - g00, a01 = g10 - g00, a11 = g11 + g00 - g01 - g10;
+    return g00 + a10 * a + a01 * b + a11 * a * b;
+}
+// The step's operands leave the domain of sqrt_core / div_core: |g|^2 below 2^-767 or not
+// finite, or an interpolated component that is nonzero but below 2^-900 in magnitude.  (With
+// |g|^2 >= 2^-767 every divisor is >= 2^-383; in the |g| >= 0.01 branch dx_n^2 + dy^2 >= 5e-5.)
+__device__ __forceinline__ bool walk_odd(double dx, double dy, double s1) {
+    const double lo = 0x1p-767, big = 0x1p1000, tiny = 0x1p-900;
+    return !(s1 >= lo && s1 <= big) | ((dx != 0.0) & (__builtin_fabs(dx) < tiny)) |
+           ((dy != 0.0) & (__builtin_fabs(dy) < tiny));
+}
+
 enum { kGdmDone = 0, kGdmFallback = 1, kGdmError = 2 };
 #ifndef EIK_P3PROBE
 #define EIK_P3PROBE(k) ((void)0)  // 3D walker phase timing hooks (tools/path3_prof.hip)
@@ -188,7 +237,7 @@ __device__ void path_builder(PathLds& s, const R* __restrict__ T, int64_t H, int
     }
 }
 
-template <typename R, bool FUSED>
+template <typename R, int LOOP>
 __global__ __launch_bounds__(kPathThreads) void gdm2d_kernel(Gdm2dArgs a) {
     __shared__ PathLds s;
     const R* __restrict__ T = static_cast<const R*>(a.T);
@@ -331,10 +380,30 @@ __global__ __launch_bounds__(kPathThreads) void gdm2d_kernel(Gdm2dArgs a) {
         o.sy = py - tau * dyn;
         return o;
     };
+    // step_math with interp2_general, sqrt_core and div_core (same bits where walk_odd is false,
+    // set in `odd`)
+    auto step_math_core = [&](const double2& g00, const double2& g01, const double2& g10, const double2& g11, double fa,
+                              double fb, bool& odd) -> StepOut {
+        StepOut o;
+        o.dx = interp2_general(fa, fb, g00.x, g01.x, g10.x, g11.x);
+        o.dy = interp2_general(fa, fb, g00.y, g01.y, g10.y, g11.y);
+        const double s1 = o.dx * o.dx + o.dy * o.dy;
+        const double nrm = sqrt_core(s1);
+        const double dxn = div_core(o.dx, nrm);
+        // both divisors computed, selected bitwise (a ?: here becomes a branch on the chain)
+        const double r2 = sqrt_core(dxn * dxn + o.dy * o.dy);
+        const long long small = -(long long)(nrm < 0.01);
+        const double den = __longlong_as_double((__double_as_longlong(nrm) & small) | (__double_as_longlong(r2) & ~small));
+        const double dyn = div_core(o.dy, den);
+        o.sx = px - tau * dxn;
+        o.sy = py - tau * dyn;
+        odd = walk_odd(o.dx, o.dy, s1);
+        return o;
+    };
     // the point budget folded into the step count: point n = k + 1 is stored at step k (:173)
     const long kmax = a.steps < a.cap - 1 ? a.steps : a.cap - 1;
     long k = 0;
-    if constexpr (FUSED) {
+    if constexpr (LOOP >= 1) {
         // One exit per step: the step is computed before its special cases are known (window
         // bookkeeping due, NaN gradient, stop radius, point budget), and a single uniform branch
         // leaves the tight loop when any of them holds; the handler below then takes the same
@@ -345,7 +414,7 @@ __global__ __launch_bounds__(kPathThreads) void gdm2d_kernel(Gdm2dArgs a) {
         constexpr unsigned kWinBytes = sizeof(s.g[0]);
         for (; k < kmax;) {
             uint32_t i, j;
-            bool in;
+            bool in, odd = false;
             StepOut o;
             double fa, fb;
             for (;;) {
@@ -359,13 +428,17 @@ __global__ __launch_bounds__(kPathThreads) void gdm2d_kernel(Gdm2dArgs a) {
                 EIK_P2PROBE(1);
                 fa = px - i;
                 fb = py - j;
-                o = step_math(g[0], g[1], g[kPW], g[kPW + 1], fa, fb);
+                if constexpr (LOOP == 2)
+                    o = step_math_core(g[0], g[1], g[kPW], g[kPW + 1], fa, fb, odd);
+                else
+                    o = step_math(g[0], g[1], g[kPW], g[kPW + 1], fa, fb);
                 EIK_P2PROBE(2);
                 const double ex = o.sx - a.ex, ey = o.sy - a.ey;
                 const bool stop = ex * ex + ey * ey < 2.25;  // :231-232, as in the loop below
                 EIK_P2PROBE(3);
                 // one branch: the conditions combined bitwise (a || chain becomes one branch each)
-                const bool leave = (int)!in | (int)__builtin_isnan(o.dx + o.dy) | (int)stop | (int)(k + 1 >= kmax);
+                const bool leave = (int)!in | (int)odd | (int)__builtin_isnan(o.dx + o.dy) | (int)stop |
+                                   (int)(k + 1 >= kmax);
                 if (leave) break;
                 *reinterpret_cast<double2*>(out + 2 * n) = make_double2(o.sx, o.sy);
                 ++n;
@@ -373,8 +446,8 @@ __global__ __launch_bounds__(kPathThreads) void gdm2d_kernel(Gdm2dArgs a) {
                 py = o.sy;
                 ++k;
             }
-            if (!in) {  // window bookkeeping (or an error), then this step again
-                if (!slow_step(i, j)) break;
+            if (!in || odd) {  // window bookkeeping (or an error), then this step again -- exactly
+                if (!in && !slow_step(i, j)) break;
                 const int li = (int)i - cx0i, lj = (int)j - cy0i;
                 o = step_math(s.g[cur][lj][li], s.g[cur][lj][li + 1], s.g[cur][lj + 1][li], s.g[cur][lj + 1][li + 1],
                               fa, fb);
@@ -441,12 +514,15 @@ __global__ __launch_bounds__(kPathThreads) void gdm2d_kernel(Gdm2dArgs a) {
 }
 
 hipError_t gdm2d(const Gdm2dArgs& a, bool f64, hipStream_t st) {
+    const dim3 g(1), b(kPathThreads);
     if (f64) {
-        if (a.fused) hipLaunchKernelGGL((gdm2d_kernel<double, true>), dim3(1), dim3(kPathThreads), 0, st, a);
-        else        hipLaunchKernelGGL((gdm2d_kernel<double, false>), dim3(1), dim3(kPathThreads), 0, st, a);
+        if (a.fused == 2)      hipLaunchKernelGGL((gdm2d_kernel<double, 2>), g, b, 0, st, a);
+        else if (a.fused == 1) hipLaunchKernelGGL((gdm2d_kernel<double, 1>), g, b, 0, st, a);
+        else                   hipLaunchKernelGGL((gdm2d_kernel<double, 0>), g, b, 0, st, a);
     } else {
-        if (a.fused) hipLaunchKernelGGL((gdm2d_kernel<float, true>), dim3(1), dim3(kPathThreads), 0, st, a);
-        else        hipLaunchKernelGGL((gdm2d_kernel<float, false>), dim3(1), dim3(kPathThreads), 0, st, a);
+        if (a.fused == 2)      hipLaunchKernelGGL((gdm2d_kernel<float, 2>), g, b, 0, st, a);
+        else if (a.fused == 1) hipLaunchKernelGGL((gdm2d_kernel<float, 1>), g, b, 0, st, a);
+        else                   hipLaunchKernelGGL((gdm2d_kernel<float, 0>), g, b, 0, st, a);
     }
     return hipGetLastError();
 }

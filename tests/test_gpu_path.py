@@ -149,12 +149,14 @@ def _walker_fields():
     return out
 
 
+@pytest.mark.parametrize("form", [1, 2])
 @pytest.mark.parametrize("tau", [0.5, 1.7])
-def test_walker_loop_forms_bit_identical(golden, tau):
-    """EIK_OPT_PATH_LOOP: the single-exit step loop (default) and the loop in the reference's
-    statement order return the SAME bits (array_equal, same status) -- on the golden fields and on fields that
-    exercise window switches, NaN fallbacks, |g| < 0.01 unit steps and, at tau = 1.7, points that
-    move more than one cell per step (the walker's slow path)."""
+def test_walker_loop_forms_bit_identical(golden, tau, form):
+    """EIK_OPT_PATH_LOOP: the single-exit step loop (1) and that loop with the range-free f64
+    sqrt / division (2, gdm.hip sqrt_core / div_core) return the SAME bits as the loop in the
+    reference's statement order (0) (array_equal, same status) -- on the golden fields and on
+    fields that exercise window switches, NaN fallbacks, |g| < 0.01 unit steps and, at tau = 1.7,
+    points that move more than one cell per step (the walker's slow path)."""
     import eikonal
     from eikonal import _lib as L
 
@@ -167,7 +169,7 @@ def test_walker_loop_forms_bit_identical(golden, tau):
     c0, c1 = eikonal.Context(0), eikonal.Context(0)
     try:
         c0.set_option(L.OPT_PATH_LOOP, 0)
-        c1.set_option(L.OPT_PATH_LOOP, 1)
+        c1.set_option(L.OPT_PATH_LOOP, form)
         for T, s, g in cases:
             a, sa = c0.path2d(T, _f(s), _f(g), tau)
             b, sb = c1.path2d(T, _f(s), _f(g), tau)

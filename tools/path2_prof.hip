@@ -35,7 +35,7 @@ int main(int argc, char** argv) {
     (void)hipMemcpy(T, hT.data(), hT.size() * 4, hipMemcpyHostToDevice);
     Gdm2dArgs a{};
     a.T = T; a.H = H; a.W = W; a.ix = sx; a.iy = sy; a.ex = gx; a.ey = gy; a.tau = 0.5; a.steps = 30000;
-    a.out = out; a.cap = 30004; a.n_out = (int64_t*)n; a.status = st; a.fused = getenv("FUSED") ? atoi(getenv("FUSED")) : 1;
+    a.out = out; a.cap = 30004; a.n_out = (int64_t*)n; a.status = st; a.fused = getenv("FUSED") ? atoi(getenv("FUSED")) : 2;
     unsigned long long z[16] = {0};
     for (int rep = 0; rep < 2; ++rep) {
         (void)hipMemcpyToSymbol(HIP_SYMBOL(g_p2), z, sizeof z);
