@@ -549,7 +549,7 @@ constexpr int kPre3 = 14;              // cells from an inner window edge that t
 struct Path3Lds {
     __attribute__((aligned(16))) char wbuf[2][kWin3Bytes];
     double ring[kRing][3];
-    double gsh[3][8], nsh[7], psh[6];  // per-step lane exchange of the walker
+    double gsh[3][8], nsh[7];  // per-step lane exchange of the walker
     int nbad[7];
     long long req_y0, req_x0, req_z0;
     int req_seq;  // walker -> builders: request number (-1: quit)
@@ -667,6 +667,12 @@ __device__ __forceinline__ double sq3(double a, double b, double c) { return a *
 // LDS with only a compiler fence (and an LDS-count wait) -- a workgroup barrier would also wait
 // for the path's global stores.
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
 
 // window origin along one axis: the needed span [lo, hi] (clipped to the volume) centred in a
 // window of n cells that stays inside [0, len)
@@ -691,7 +697,6 @@ __global__ __launch_bounds__(kP3Threads) void gdm3d_kernel(Gdm3dArgs a) {
     auto& ring = sl.ring;
     auto& gsh = sl.gsh;
     auto& nsh = sl.nsh;
-    auto& psh = sl.psh;
     auto& nbad = sl.nbad;
     const int lane = threadIdx.x;
     const bool lead = lane == 0;
@@ -738,14 +743,14 @@ __global__ __launch_bounds__(kP3Threads) void gdm3d_kernel(Gdm3dArgs a) {
     };
     double* out = a.out;
     // path point q: the LDS ring while it holds it (the last kRing points), else global memory
-    auto pt = [&](int64_t q, int c) -> double { return ring[q % kRing][c]; };
+    auto pt = [&](int64_t q, int c) -> double { return ring[(int)q & (kRing - 1)][c]; };  // q >= 0
     auto put = [&](int64_t q, double x, double y, double z) {
         out[3 * q] = x;  // every lane: same address and value (each lane reads back its own
         out[3 * q + 1] = y;  // stores when back-tracking below the ring)
         out[3 * q + 2] = z;
-        ring[q % kRing][0] = x;
-        ring[q % kRing][1] = y;
-        ring[q % kRing][2] = z;
+        ring[(int)q & (kRing - 1)][0] = x;
+        ring[(int)q & (kRing - 1)][1] = y;
+        ring[(int)q & (kRing - 1)][2] = z;
     };
     int64_t n = 0, lo = 0;  // ring holds points [lo, n); below lo: global
     auto point = [&](int64_t q, int c) -> double { return q >= lo ? pt(q, c) : out[3 * q + c]; };
@@ -759,6 +764,17 @@ __global__ __launch_bounds__(kP3Threads) void gdm3d_kernel(Gdm3dArgs a) {
 #pragma unroll
     for (int q = 0; q < 6; ++q)
         for (int c = 0; c < 3; ++c) ustep[q][c] = (double)(-off[q][c]) / tau;
+    // what the step's tail (:255-264) subtracts from the node after the descent move q: its
+    // |(dx, dy, dz)| is the one nonzero |ustep| (sqrt(u*u) == |u| for a correctly rounded root), so
+    // the branch and the products are known per move
+    double mstep[6][3];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+        const double u = ustep[q][q >> 1 == 0 ? 1 : q >> 1 == 1 ? 0 : 2];
+        const double nrm = __builtin_fabs(u);
+        for (int c = 0; c < 3; ++c) mstep[q][c] = nrm < 0.01 ? tau * (ustep[q][c] / nrm) : tau * ustep[q][c];
+    }
+    double p2x = 0.0, p2y = 0.0, p2z = 0.0;  // path point n - 2 (point n - 1 is (gx, gy, gz))
     EIK_P3DECL;
     for (long k = 0; k < a.steps; ++k) {
         EIK_P3PROBE(3);
@@ -803,6 +819,11 @@ __global__ __launch_bounds__(kP3Threads) void gdm3d_kernel(Gdm3dArgs a) {
         EIK_P3PROBE(0);
         const int64_t rx = (int64_t)__builtin_rint(gx), ry = (int64_t)__builtin_rint(gy), rz = (int64_t)__builtin_rint(gz);
         const bool rin = rx >= 0 && ry >= 0 && rz >= 0 && rx < W && ry < H && rz < L;
+        // per-lane gather, kept in registers: lanes 0..23 the two T samples of one np.gradient value
+        // (axis, corner), lanes 24..30 the node and its six neighbours (:244-252).  (The last two
+        // path points, which the pops of :238-240 test, are (gx, gy, gz) and (p2x, p2y, p2z).)
+        double t_hi = 0.0, t_lo = 0.0, gscale = 0.5, nv = 0.0;
+        bool bad = false;
         if (lane >= 24 && lane < 31) {
             if (rin) {
                 const int q = lane - 25;  // -1: the node; 0..5: y-1, y+1, x-1, x+1, z-1, z+1 (:244-252)
@@ -816,13 +837,9 @@ __global__ __launch_bounds__(kP3Threads) void gdm3d_kernel(Gdm3dArgs a) {
                 if (cx < 0) cx += W;  // python negative indices wrap
                 if (cy < 0) cy += H;
                 if (cz < 0) cz += L;
-                const bool bad = cx >= W || cy >= H || cz >= L;
-                nsh[lane - 24] = bad ? __builtin_nan("") : v.at(cy, cx, cz);
-                nbad[lane - 24] = bad;
+                bad = cx >= W || cy >= H || cz >= L;
+                nv = bad ? __builtin_nan("") : v.at(cy, cx, cz);
             }
-        } else if (lane >= 32 && lane < 38) {
-            const int64_t q = n - 1 - (lane - 32) / 3;
-            psh[lane - 32] = q >= 0 ? point(q, (lane - 32) % 3) : 0.0;
         }
         if (lane < 24) {
             const int axis = lane >> 3, cj = (lane >> 2) & 1, ci = (lane >> 1) & 1, ck = lane & 1;
@@ -831,15 +848,71 @@ __global__ __launch_bounds__(kP3Threads) void gdm3d_kernel(Gdm3dArgs a) {
             const int64_t p = axis == 0 ? y : axis == 1 ? x : z;
             const bool first = p == 0, last = !first && p == len - 1;
             const int64_t dlo = first ? 0 : 1, dhi = last ? 0 : 1;
-            const double t_hi = v.atw(y + (axis == 0) * dhi, x + (axis == 1) * dhi, z + (axis == 2) * dhi);
-            const double t_lo = v.atw(y - (axis == 0) * dlo, x - (axis == 1) * dlo, z - (axis == 2) * dlo);
-            // (/ 1.0 at the ends, / 2.0 inside: both exact, as multiplications)
-            gsh[axis][lane & 7] = (t_hi - t_lo) * (first || last ? 1.0 : 0.5);
+            t_hi = v.atw(y + (axis == 0) * dhi, x + (axis == 1) * dhi, z + (axis == 2) * dhi);
+            t_lo = v.atw(y - (axis == 0) * dlo, x - (axis == 1) * dlo, z - (axis == 2) * dlo);
+            gscale = first || last ? 1.0 : 0.5;  // (/ 1.0 at the ends, / 2.0 inside: both exact)
+        }
+        // Integer-node step (the C5 regime: on a z-padded few-layer volume every step is the
+        // integer descent).  At a point whose three coordinates are integers every fraction of
+        // the trilinear interpolation is 0, so each of dx, dy, dz is a0 + a1*0 + ... + a7*0*0*0:
+        // NaN exactly when one of its coefficients is not finite (a*0 = NaN), i.e. when one of
+        // its eight np.gradient samples is (every corner enters some a1..a7), i.e. when one of
+        // their T samples is; otherwise a0.  So the fallback is taken iff a lane's T sample is not
+        // finite -- a ballot, no interpolation and no lane exchange through LDS.  When it is
+        // taken with the node reached and in range, no neighbour out of range and some
+        // neighbour lower, the step is the descent below, in the reference's order with the
+        // same operations as the general path (which handles every other case).
+        double dx = 0.0, dy = 0.0, dz = 0.0;
+        bool intstep = false;
+        int best = -1;
+        double tnode = 0.0;
+        if (gx == (double)i && gy == (double)j && gz == (double)kk && rin) {
+            const unsigned long long nonfin =
+                __ballot(lane < 24 && !(__builtin_isfinite(t_hi) && __builtin_isfinite(t_lo)));
+            const unsigned long long badm = __ballot(lane >= 24 && lane < 31 && bad);
+            tnode = readlane_f64(nv, 24);
+            if (nonfin != 0ull && badm == 0ull && !__builtin_isinf(tnode)) {
+                double curT = tnode;
+#pragma unroll
+                for (int q = 0; q < 6; ++q) {  // the reference's ordered scan
+                    const double tc = readlane_f64(nv, 25 + q);
+                    if (tc < curT) {
+                        curT = tc;
+                        best = q;
+                    }
+                }
+                intstep = best >= 0;
+            }
+        }
+        if (intstep) {
+            const int64_t nx = rx, ny = ry, nz = rz;
+            bool deep = false;  // as the NaN branch below with fast = true
+            if (n > 0 && sq3(gx - nx, gy - ny, gz - nz) < 1.0) {
+                --n;
+                if (n > 0 && sq3(p2x - nx, p2y - ny, p2z - nz) < 1.0) {
+                    --n;
+                    deep = true;
+                }
+            }
+            if (deep)
+                while (n > 0 && sq3(point(n - 1, 0) - nx, point(n - 1, 1) - ny, point(n - 1, 2) - nz) < 1.0) --n;
+            if (n >= a.cap) { status = kGdmError; break; }
+            if (n < lo) lo = n;
+            put(n, (double)nx, (double)ny, (double)nz);
+            ++n;
+            gx = (double)nx;
+            gy = (double)ny;
+            gz = (double)nz;
+        } else {
+        if (lane < 24) gsh[lane >> 3][lane & 7] = (t_hi - t_lo) * gscale;
+        if (lane >= 24 && lane < 31 && rin) {
+            nsh[lane - 24] = nv;
+            nbad[lane - 24] = bad;
         }
         wave_lds_sync();
-        double dx = tri3(gsh[1], gx - i, gy - j, gz - kk);
-        double dy = tri3(gsh[0], gx - i, gy - j, gz - kk);
-        double dz = tri3(gsh[2], gx - i, gy - j, gz - kk);
+        dx = tri3(gsh[1], gx - i, gy - j, gz - kk);
+        dy = tri3(gsh[0], gx - i, gy - j, gz - kk);
+        dz = tri3(gsh[2], gx - i, gy - j, gz - kk);
         EIK_P3PROBE(1);
         if (__builtin_isnan(dx) || __builtin_isnan(dy) || __builtin_isnan(dz)) {  // :212-253
             int64_t nx = rx, ny = ry, nz = rz;
@@ -859,9 +932,9 @@ __global__ __launch_bounds__(kP3Threads) void gdm3d_kernel(Gdm3dArgs a) {
                 if (err) { status = kGdmError; break; }
             }
             bool deep = !fast;  // pops beyond the two gathered points read the ring
-            if (fast && n > 0 && sq3(psh[0] - nx, psh[1] - ny, psh[2] - nz) < 1.0) {
+            if (fast && n > 0 && sq3(gx - nx, gy - ny, gz - nz) < 1.0) {
                 --n;
-                if (n > 0 && sq3(psh[3] - nx, psh[4] - ny, psh[5] - nz) < 1.0) {
+                if (n > 0 && sq3(p2x - nx, p2y - ny, p2z - nz) < 1.0) {
                     --n;
                     deep = true;
                 }
@@ -901,22 +974,40 @@ __global__ __launch_bounds__(kP3Threads) void gdm3d_kernel(Gdm3dArgs a) {
             gy = (double)ny;
             gz = (double)nz;
         }
+        }
         EIK_P3PROBE(2);
-        const double nrm = __builtin_sqrt(dx * dx + dy * dy + dz * dz);  // :255
         double ax, ay, az;
-        if (nrm < 0.01) {
-            ax = gx - tau * (dx / nrm);
-            ay = gy - tau * (dy / nrm);
-            az = gz - tau * (dz / nrm);
-        } else {  // unnormalised step (:262-264)
-            ax = gx - tau * dx;
-            ay = gy - tau * dy;
-            az = gz - tau * dz;
+        if (intstep) {  // the tail below for the move `best`, from the table
+            double m0 = 0.0, m1 = 0.0, m2 = 0.0;
+#pragma unroll
+            for (int q = 0; q < 6; ++q)
+                if (q == best) {
+                    m0 = mstep[q][0];
+                    m1 = mstep[q][1];
+                    m2 = mstep[q][2];
+                }
+            ax = gx - m0;
+            ay = gy - m1;
+            az = gz - m2;
+        } else {
+            const double nrm = __builtin_sqrt(dx * dx + dy * dy + dz * dz);  // :255
+            if (nrm < 0.01) {
+                ax = gx - tau * (dx / nrm);
+                ay = gy - tau * (dy / nrm);
+                az = gz - tau * (dz / nrm);
+            } else {  // unnormalised step (:262-264)
+                ax = gx - tau * dx;
+                ay = gy - tau * dy;
+                az = gz - tau * dz;
+            }
         }
         if (n >= a.cap) { status = kGdmError; break; }
         put(n, ax, ay, az);
         ++n;
         if (n - lo > kRing) lo = n - kRing;
+        p2x = gx;  // (gx, gy, gz) is point n - 2 now
+        p2y = gy;
+        p2z = gz;
         gx = ax;
         gy = ay;
         gz = az;
