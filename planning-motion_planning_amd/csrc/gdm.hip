@@ -705,6 +705,23 @@ __global__ __launch_bounds__(kP3Threads) void gdm3d_kernel(Gdm3dArgs a) {
     v.H = a.H; v.W = a.W; v.L = a.L;
     const int64_t H = a.H, W = a.W, L = a.L;
     win3_dims<R>(a.H, a.W, a.L, v.WY, v.WX, v.WZ);
+    // lane constants of the interior gather (see the step): lanes 0..23 sample np.gradient along
+    // axis g_ax at corner (cj, ci, ck) of the cube -- window offset g_off from the cube's origin,
+    // g_str the axis stride, g_c the corner's coordinate along its axis; lanes 24..30 read the
+    // rint node (-1) and its six neighbours (0..5: y-1, y+1, x-1, x+1, z-1, z+1) at g_off from it
+    const int sy = v.WX * v.WZ, sx = v.WZ;
+    int g_ax = 0, g_c = 0, g_off = 0, g_str = 0;
+    if (lane < 24) {
+        g_ax = lane >> 3;
+        const int cj = (lane >> 2) & 1, ci = (lane >> 1) & 1, ck = lane & 1;
+        g_c = g_ax == 0 ? cj : g_ax == 1 ? ci : ck;
+        g_off = cj * sy + ci * sx + ck;
+        g_str = g_ax == 0 ? sy : g_ax == 1 ? sx : 1;
+    } else if (lane < 31) {
+        const int q = lane - 25;
+        const int st = q < 0 ? 0 : (q >> 1) == 0 ? sy : (q >> 1) == 1 ? sx : 1;
+        g_off = q < 0 ? 0 : (q & 1) ? st : -st;
+    }
     v.w = reinterpret_cast<const R*>(sl.wbuf[0]);
     v.y0 = v.x0 = v.z0 = -((int64_t)1 << 40);  // empty: the first step requests a window
     // the two buffers' origins (scalars: no private array), the current one mirrored in v
@@ -824,6 +841,23 @@ __global__ __launch_bounds__(kP3Threads) void gdm3d_kernel(Gdm3dArgs a) {
         // path points, which the pops of :238-240 test, are (gx, gy, gz) and (p2x, p2y, p2z).)
         double t_hi = 0.0, t_lo = 0.0, gscale = 0.5, nv = 0.0;
         bool bad = false;
+        if (ry >= 1 && ry + 1 < H && rx >= 1 && rx + 1 < W && rz >= 1 && rz + 1 < L) {
+            // interior rint node: its six neighbours are in range (no wrap, none bad) and, like the
+            // cube, inside the window -- every lane reads window cells at a lane-constant offset,
+            // the same code on every lane (lanes 24..30 with stride 0 read their cell twice)
+            const bool grad = lane < 24;
+            const int base = grad ? (((int)(j - v.y0) * v.WX + (int)(i - v.x0)) * v.WZ + (int)(kk - v.z0))
+                                  : (((int)(ry - v.y0) * v.WX + (int)(rx - v.x0)) * v.WZ + (int)(rz - v.z0));
+            const int64_t pc = (g_ax == 0 ? (int64_t)j : g_ax == 1 ? (int64_t)i : (int64_t)kk) + g_c;
+            const int64_t len = g_ax == 0 ? H : g_ax == 1 ? W : L;
+            const bool first = pc == 0, last = !first && pc == len - 1;
+            const int idx = lane < 31 ? base + g_off : base;
+            const R* w = v.w;
+            t_hi = (double)w[idx + (last ? 0 : g_str)];
+            t_lo = (double)w[idx - (first ? 0 : g_str)];
+            gscale = first || last ? 1.0 : 0.5;  // (/ 1.0 at the ends, / 2.0 inside: both exact)
+            nv = t_hi;
+        } else {
         if (lane >= 24 && lane < 31) {
             if (rin) {
                 const int q = lane - 25;  // -1: the node; 0..5: y-1, y+1, x-1, x+1, z-1, z+1 (:244-252)
@@ -851,6 +885,7 @@ __global__ __launch_bounds__(kP3Threads) void gdm3d_kernel(Gdm3dArgs a) {
             t_hi = v.atw(y + (axis == 0) * dhi, x + (axis == 1) * dhi, z + (axis == 2) * dhi);
             t_lo = v.atw(y - (axis == 0) * dlo, x - (axis == 1) * dlo, z - (axis == 2) * dlo);
             gscale = first || last ? 1.0 : 0.5;  // (/ 1.0 at the ends, / 2.0 inside: both exact)
+        }
         }
         // Integer-node step (the C5 regime: on a z-padded few-layer volume every step is the
         // integer descent).  At a point whose three coordinates are integers every fraction of
