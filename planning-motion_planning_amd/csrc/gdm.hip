@@ -667,6 +667,20 @@ __device__ __forceinline__ double sq3(double a, double b, double c) { return a *
 // LDS with only a compiler fence (and an LDS-count wait) -- a workgroup barrier would also wait
 // for the path's global stores.
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// (uint32_t)trunc(x) and rint(x) as int: one conversion each (the hardware truncates and clamps
+// to the type's range, NaN -> 0).  The walker's coordinates are finite (a NaN point ends the walk)
+// and below 2^31: out-of-range values clamp to 0 / INT_MIN / INT_MAX, which fail the same range
+// tests as the 64-bit conversions did.
+__device__ __forceinline__ uint32_t cvt_u32(double x) {
+    uint32_t r;
+    asm("v_cvt_u32_f64 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+__device__ __forceinline__ int rint_i32(double x) {
+    int r;
+    asm("v_cvt_i32_f64 %0, %1" : "=v"(r) : "v"(__builtin_rint(x)));
+    return r;
+}
 __device__ __forceinline__ double readlane_f64(double v, int l) {
     const unsigned long long b = (unsigned long long)__double_as_longlong(v);
     const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
@@ -795,7 +809,7 @@ __global__ __launch_bounds__(kP3Threads) void gdm3d_kernel(Gdm3dArgs a) {
     EIK_P3DECL;
     for (long k = 0; k < a.steps; ++k) {
         EIK_P3PROBE(3);
-        const uint32_t i = (uint32_t)__builtin_trunc(gx), j = (uint32_t)__builtin_trunc(gy), kk = (uint32_t)__builtin_trunc(gz);
+        const uint32_t i = cvt_u32(gx), j = cvt_u32(gy), kk = cvt_u32(gz);
         if (i + 1 >= (uint64_t)W || j + 1 >= (uint64_t)H || kk + 1 >= (uint64_t)L) { status = kGdmError; break; }
         // fast path: while bj_lo <= j <= bj_hi (and for i, kk) the cube is in the current window and
         // not within kPre3 of an inner edge (or a build is pending): nothing to do this step
@@ -834,7 +848,7 @@ __global__ __launch_bounds__(kP3Threads) void gdm3d_kernel(Gdm3dArgs a) {
             set_bounds();
         }
         EIK_P3PROBE(0);
-        const int64_t rx = (int64_t)__builtin_rint(gx), ry = (int64_t)__builtin_rint(gy), rz = (int64_t)__builtin_rint(gz);
+        const int64_t rx = rint_i32(gx), ry = rint_i32(gy), rz = rint_i32(gz);
         const bool rin = rx >= 0 && ry >= 0 && rz >= 0 && rx < W && ry < H && rz < L;
         // per-lane gather, kept in registers: lanes 0..23 the two T samples of one np.gradient value
         // (axis, corner), lanes 24..30 the node and its six neighbours (:244-252).  (The last two
