@@ -211,6 +211,12 @@ int eik_ipc_free(eik_ctx* ctx, void* d_ptr);
 int eik_ipc_open(eik_ctx* ctx, const unsigned char handle[64], void** d_ptr);
 int eik_ipc_close(eik_ctx* ctx, void* d_ptr);
 
+/* Self-test (no reference counterpart): the 2D path kernel's fast-path f64 square root,
+ * division and interpolation against the exact forms they replace, on n pseudo-random inputs
+ * each from their domain (gdm.hip walker_math_selftest_kernel); counts[0..2] = mismatches of
+ * each (0 expected), counts[3] = samples evaluated (n). */
+int eik_selftest_walker_math(eik_ctx* ctx, int64_t n, uint64_t seed, int64_t counts[4]);
+
 /* getPathGDM on a device-resident field; out/n_out/status are device pointers. */
 int eik_path2d_dev(eik_ctx* ctx, const void* d_T, int dtype, int64_t H, int64_t W, const double init[2],
                    const double end[2], double tau, double* d_out, int64_t cap, int64_t* d_n_out, int* d_status,

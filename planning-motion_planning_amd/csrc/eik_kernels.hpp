@@ -114,6 +114,8 @@ struct Gdm2dArgs {
                            // 0 reference-structured loop (same path bits)
 };
 hipError_t gdm2d(const Gdm2dArgs& a, bool f64, hipStream_t st);
+// fast-path arithmetic of the 2D walker vs the exact forms (gdm.hip): mismatch counts [3] + samples, device
+hipError_t walker_math_selftest(long long n, unsigned long long seed, unsigned long long* d_counts, hipStream_t st);
 
 // FastMarching3D.getPathGDM (:198-271): np.gradient field, trilinear (a7 as in :290), integer
 // 6-neighbour fallback, unnormalised step.

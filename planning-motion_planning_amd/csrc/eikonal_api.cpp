@@ -752,6 +752,20 @@ int eik_tmap2d_bidir_f64(eik_ctx* c, const double* cost, int64_t H, int64_t W, i
     return EIK_OK;
 }
 
+int eik_selftest_walker_math(eik_ctx* c, int64_t n, uint64_t seed, int64_t mismatches[4]) {
+    if (!c || !mismatches || n < 1) return EIK_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, c->misc.ensure(64));
+    unsigned long long* d = (unsigned long long*)c->misc.p;
+    HIPCHK(c, hipMemsetAsync(d, 0, 4 * sizeof(unsigned long long), c->stream));
+    HIPCHK(c, walker_math_selftest((long long)n, (unsigned long long)seed, d, c->stream));
+    unsigned long long h[4];
+    HIPCHK(c, hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int k = 0; k < 4; ++k) mismatches[k] = (int64_t)h[k];
+    return EIK_OK;
+}
+
 int eik_path2d_dev(eik_ctx* c, const void* d_T, int dtype, int64_t H, int64_t W, const double init[2],
                    const double end[2], double tau, double* d_out, int64_t cap, int64_t* d_n_out, int* d_status,
                    void* stream) {

@@ -513,6 +513,51 @@ __global__ __launch_bounds__(kPathThreads) void gdm2d_kernel(Gdm2dArgs a) {
     }
 }
 
+// Self-test of the 2D walker's fast-path arithmetic against the exact forms it stands in for,
+// on n pseudo-random inputs per function drawn from the walker's fast-path domain (walk_odd
+// false): sqrt_core(x) vs sqrt(x) for x in [2^-767, 2^1000]; div_core(n, d) vs n / d for d in
+// [2^-900, 2^100], |n| <= d, n = 0 or |n| >= 2^-900 (a zero quotient may differ in sign only);
+// interp2_general vs interp2_sel for corners in [-1, 1] and fractions in [0, 1) that are exactly
+// 0 a quarter of the time.  counts[0..2]: mismatches of each; counts[3]: samples evaluated.
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {  // splitmix64
+    z += 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ double dbl_exp(unsigned long long r, int e_lo, int e_hi) {  // 2^e * (1 + m)
+    const int e = e_lo + (int)((r >> 52) % (unsigned long long)(e_hi - e_lo + 1));
+    return __longlong_as_double((long long)(((unsigned long long)(e + 1023) << 52) | (r & 0xfffffffffffffull)));
+}
+__device__ __forceinline__ double unit_f(unsigned long long r) { return (double)(r >> 11) * 0x1p-53; }  // [0, 1)
+__global__ void walker_math_selftest_kernel(long long n, unsigned long long seed, unsigned long long* counts) {
+    unsigned long long bad[3] = {0, 0, 0}, done = 0;
+    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (long long)gridDim.x * blockDim.x) {
+        ++done;
+        const unsigned long long r0 = mix64(seed ^ (4 * t)), r1 = mix64(seed ^ (4 * t + 1)), r2 = mix64(seed ^ (4 * t + 2)),
+                                 r3 = mix64(seed ^ (4 * t + 3));
+        const double x = t == 0 ? 0x1p-767 : dbl_exp(r0, -767, 999);
+        if (__double_as_longlong(sqrt_core(x)) != __double_as_longlong(__builtin_sqrt(x))) ++bad[0];
+        const double d = dbl_exp(r1, -900, 99);
+        double q = d * (2.0 * unit_f(r2) - 1.0);
+        if (__builtin_fabs(q) < 0x1p-900 || (r2 & 15) == 0) q = (r2 & 16) ? -0.0 : 0.0;
+        const double e1 = div_core(q, d), e0 = q / d;
+        if (e0 == 0.0 ? e1 != 0.0 : __double_as_longlong(e1) != __double_as_longlong(e0)) ++bad[1];
+        const double fa = (r3 & 3) == 0 ? 0.0 : unit_f(mix64(r3)), fb = (r3 & 12) == 0 ? 0.0 : unit_f(mix64(r3 + 1));
+        double g[4];
+        for (int c = 0; c < 4; ++c) g[c] = 2.0 * unit_f(mix64(r3 + 2 + c)) - 1.0;
+        const double i1 = interp2_general(fa, fb, g[0], g[1], g[2], g[3]), i0 = interp2_sel(fa, fb, g[0], g[1], g[2], g[3]);
+        if (i0 == 0.0 ? i1 != 0.0 : __double_as_longlong(i1) != __double_as_longlong(i0)) ++bad[2];
+    }
+    for (int k = 0; k < 3; ++k)
+        if (bad[k]) atomicAdd(&counts[k], bad[k]);
+    if (done) atomicAdd(&counts[3], done);
+}
+hipError_t walker_math_selftest(long long n, unsigned long long seed, unsigned long long* d_counts, hipStream_t st) {
+    hipLaunchKernelGGL(walker_math_selftest_kernel, dim3(1024), dim3(256), 0, st, n, seed, d_counts);
+    return hipGetLastError();
+}
+
 hipError_t gdm2d(const Gdm2dArgs& a, bool f64, hipStream_t st) {
     const dim3 g(1), b(kPathThreads);
     if (f64) {

@@ -106,6 +106,7 @@ def lib():
         L.eik_tmap2d_batch_f32.argtypes = [vp, _f32p, i64, i64, i64, _i64p, _f32p]
         L.eik_path2d_f64.argtypes = [vp, _f64p, i64, i64, _f64p, _f64p, C.c_double, _f64p, i64, P(i64), P(C.c_int)]
         L.eik_gradient2d_f64.argtypes = [vp, _f64p, i64, i64, _f64p, _f64p]
+        L.eik_selftest_walker_math.argtypes = [vp, i64, C.c_uint64, _i64p]
         L.eik_fim2d_create.argtypes = [vp, i64, i64, i64, C.c_int, P(vp)]
         L.eik_fim2d_destroy.argtypes = [vp]
         L.eik_fim2d_destroy.restype = None
@@ -161,7 +162,7 @@ EXPORTED = [
     "eik_tmap2d_f32", "eik_tmap2d_f64", "eik_tmap2d_bidir_f64", "eik_tmap2d_batch_f32", "eik_path2d_f64",
     "eik_gradient2d_f64", "eik_fim2d_create", "eik_fim2d_destroy", "eik_fim2d_set_ghosts", "eik_fim2d_start",
     "eik_fim2d_iterate", "eik_fim2d_solve", "eik_fim2d_pack_edges", "eik_fim2d_merge_ghost", "eik_fim2d_active",
-    "eik_fim2d_stats", "eik_path2d_dev", "eik_tmap3d_f32", "eik_tmap3d_f64", "eik_path3d_f64", "eik_fim3d_solve",
+    "eik_fim2d_stats", "eik_path2d_dev", "eik_selftest_walker_math", "eik_tmap3d_f32", "eik_tmap3d_f64", "eik_path3d_f64", "eik_fim3d_solve",
     "eik_path3d_dev", "eik_costmap_f64", "eik_costmap_dev", "eik_surface_normal_f64", "eik_image_fill_u8",
     "eik_load_dem_txt", "eik_io_last_error", "eik_fim2d_live_bind", "eik_fim2d_launch", "eik_fim2d_live_pack",
     "eik_fim2d_live_merge", "eik_fim2d_release", "eik_node_allreduce", "eik_node_shm_open",
