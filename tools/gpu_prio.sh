@@ -1,5 +1,5 @@
-# Walker priority A/B: 2D (tools/path2_prof.hip) and 3D (tools/path3_prof.hip) walkers built with
-# EIK_WALKER_PRIO=0 and 3, alternating.
+# Walker priority A/B (record of a rejected change): the 2D and 3D walkers built with -DEIK_WALKER_PRIO=0 / 3
+# (s_setprio of the walker wave; the hook was removed from gdm.hip with the change, profiles/r02p_walker_prio_ab.log).
 export TMPDIR=/tmp
 for p in 0 3; do
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DP2_NOPROBE -DEIK_WALKER_PRIO=$p tools/path2_prof.hip -o /tmp/p2_$p || exit 1
