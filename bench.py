@@ -187,7 +187,7 @@ def main():
             traffic = None
     roof = {
         "bound": "hbm",
-        "kernel": "fim2d_persist_kernel<float>",
+        "kernel": "fim2d_persist_kernel<float, 1>",
         "achieved": round(achieved, 2) if achieved else None,
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",

@@ -358,11 +358,12 @@ int eik_fim2d_iterate(eik_fim2d* f, int64_t max_iters, int64_t* active) {
             }
             HIPCHK(c, hipEventRecord(f->ev_pool[f->ev_used++], f->stream));
         }
-        if (f->persist_grid == 0) f->persist_grid = fim2d_persist_resident(f->f64, c->cu_count);
+        const bool wide = !f->f64 && f->a.tiles_per_map >= kWideTiles;  // one large raster (a batch of small maps: no gain)
+        if (f->persist_grid == 0) f->persist_grid = fim2d_persist_resident(f->f64, c->cu_count, wide);
         const int g = std::min(grid, f->persist_grid);
         f->a.fresh_first = c->fresh_first;
         f->a.sched = c->sched;
-        HIPCHK(c, fim2d_persist(f->a, f->f64, g, f->stream));
+        HIPCHK(c, fim2d_persist(f->a, f->f64, g, f->stream, wide));
         if (c->timing) HIPCHK(c, hipEventRecord(f->ev_pool[f->ev_used++], f->stream));
         ++f->iterations;
         HIPCHK(c, hipMemcpyAsync(f->h_q, f->qctl.p, kQueueCtlBytes, hipMemcpyDeviceToHost, f->stream));
@@ -525,7 +526,8 @@ int eik_fim2d_launch(eik_fim2d* f, int live) {
         return set_err(c, EIK_ERR_ARG, "eik_fim2d_launch needs the persistent mode (EIK_OPT_MODE)");
     HIPCHK(c, hipSetDevice(c->device));
     const int grid = c->grid > 0 ? c->grid : 4 * c->cu_count;
-    if (f->persist_grid == 0) f->persist_grid = fim2d_persist_resident(f->f64, c->cu_count);
+    const bool wide = !f->f64 && f->a.tiles_per_map >= kWideTiles;  // one large raster (a batch of small maps: no gain)
+    if (f->persist_grid == 0) f->persist_grid = fim2d_persist_resident(f->f64, c->cu_count, wide);
     Fim2dArgs a = f->a;
     if (live) {
         int rc = live_box(f);
@@ -550,7 +552,7 @@ int eik_fim2d_launch(eik_fim2d* f, int live) {
     const int g = std::max(live ? 2 : 1, std::min(grid, f->persist_grid));
     a.fresh_first = c->fresh_first;
     a.sched = c->sched;
-    HIPCHK(c, fim2d_persist(a, f->f64, g, f->stream));
+    HIPCHK(c, fim2d_persist(a, f->f64, g, f->stream, wide));
     if (c->timing) HIPCHK(c, hipEventRecord(f->ev_pool[f->ev_used++], f->stream));
     f->live_on = live != 0;
     ++f->iterations;

@@ -527,8 +527,12 @@ __device__ void live_agent(const Fim2dArgs& a, unsigned* sh) {
     }
 }
 
-template <typename R>
-__global__ __launch_bounds__(kThreads) void fim2d_persist_kernel(Fim2dArgs a) {
+// WPS: the launch-bounds occupancy target in waves per SIMD (1: the compiler's choice, 159
+// VGPRs -> 3 workgroups per CU; 4: <= 128 VGPRs -> 4 per CU, a few spills).  Large rasters
+// (maps of >= kWideTiles tiles: the throughput-bound regime) run the 4-wave form -- 16384^2 on one GPU
+// +10-15 %, 4096^2 -3 % (profiles/r02r_wps_ab.log).
+template <typename R, int WPS>
+__global__ __launch_bounds__(kThreads, WPS) void fim2d_persist_kernel(Fim2dArgs a) {
     __shared__ TileLds<R> L;
     if (a.live && blockIdx.x == gridDim.x - 1) {
         __shared__ unsigned sh[4];
@@ -670,21 +674,23 @@ hipError_t fim2d_sweep(const Fim2dArgs& a, bool f64, int grid, hipStream_t st) {
 
 // Workgroups of the persistent kernel that can be co-resident (a larger grid only adds
 // workgroups that start after the solve ended and leave at once).
-int fim2d_persist_resident(bool f64, int cus) {
+int fim2d_persist_resident(bool f64, int cus, bool wide) {
     int per_cu = 0;
-    const hipError_t e = f64 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fim2d_persist_kernel<double>,
-                                                                            kThreads, 0)
-                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fim2d_persist_kernel<float>,
-                                                                            kThreads, 0);
+    const hipError_t e =
+        f64    ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fim2d_persist_kernel<double, 1>, kThreads, 0)
+        : wide ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fim2d_persist_kernel<float, 4>, kThreads, 0)
+               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fim2d_persist_kernel<float, 1>, kThreads, 0);
     if (e != hipSuccess || per_cu < 1) per_cu = 1;
     return per_cu * cus;
 }
 
-hipError_t fim2d_persist(const Fim2dArgs& a, bool f64, int grid, hipStream_t st) {
+hipError_t fim2d_persist(const Fim2dArgs& a, bool f64, int grid, hipStream_t st, bool wide) {
     if (f64)
-        hipLaunchKernelGGL(fim2d_persist_kernel<double>, dim3(grid), dim3(kThreads), 0, st, a);
+        hipLaunchKernelGGL((fim2d_persist_kernel<double, 1>), dim3(grid), dim3(kThreads), 0, st, a);
+    else if (wide)
+        hipLaunchKernelGGL((fim2d_persist_kernel<float, 4>), dim3(grid), dim3(kThreads), 0, st, a);
     else
-        hipLaunchKernelGGL(fim2d_persist_kernel<float>, dim3(grid), dim3(kThreads), 0, st, a);
+        hipLaunchKernelGGL((fim2d_persist_kernel<float, 1>), dim3(grid), dim3(kThreads), 0, st, a);
     // before anything (merge kernel, next launch) appends again
     hipLaunchKernelGGL(fim2d_qrewind_kernel, dim3(1), dim3(1), 0, st, a);
     return hipGetLastError();
