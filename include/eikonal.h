@@ -82,7 +82,8 @@ typedef enum {
                                 EIK_ERR_NOCONVERGE (0: default 1024 x tiles + 2^20)            */
     EIK_OPT_PASSES = 9,      /* persistent mode: sweep passes a visit may run in place while its
                                 tile keeps changing before it is re-queued (0, the default:
-                                24 for a single map, 2 for a batch of maps)                    */
+                                24 for a single map, 16 for a single fp32 map of >= 16384
+                                tiles, 2 for a batch of maps)                                  */
     EIK_OPT_FRESH_FIRST = 10,/* persistent mode: 1 queues a tile's first activation ahead of
                                 re-visits while the queue has a backlog (default 0: one FIFO)  */
     EIK_OPT_SCHED = 11,      /* persistent mode, bit mask: 1 = a busy tile serves activations that

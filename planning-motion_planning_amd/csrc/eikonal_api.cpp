@@ -312,7 +312,9 @@ int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
     // halos early): C2 2.07-2.09 ms at 8-16 vs 2.23 at 2; C3 6.86 ms at 2 vs 8.0 at 8.  Single map
     // 24 (profiles/r01g_passes_8_16_24.log): C2 2.03-2.04 ms vs 2.05-2.08 at 16 (within noise),
     // C4 at one GPU 16.4-16.6 vs 16.3-16.4 at 16 (within noise); 8 is clearly slower on both.
-    f->a.max_passes = c->passes > 0 ? c->passes : f->B > 1 ? 2 : 24;
+    // A single map large enough for the 4-waves-per-SIMD kernel (>= kWideTiles tiles, 16384^2) is
+    // throughput-bound: 16 passes, 17.1-17.3 -> 18.3-18.9 Gcells/s (profiles/r02w_passes_wide.log).
+    f->a.max_passes = c->passes > 0 ? c->passes : f->B > 1 ? 2 : (!f->f64 && f->a.tiles_per_map >= kWideTiles) ? 16 : 24;
     f->a.qbudget = c->max_visits ? c->max_visits : 1024ull * (unsigned long long)(f->B * f->a.tiles_per_map) + (1ull << 20);
     f->iterations = 0;
     f->host_syncs = 0;

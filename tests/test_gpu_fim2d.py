@@ -174,7 +174,8 @@ def test_stats_count_visits(ctx):
 def test_pass_cap_option(passes):
     """EIK_OPT_PASSES (in-place passes per persistent visit) changes the schedule, not the field:
     a single map and a batch against the oracle at caps other than the defaults (24 for a single
-    map, 2 for a batch; 2 is also run here on the single map and 1 / 16 on the batch)."""
+    map -- 16 for one of >= 16384 tiles --, 2 for a batch; 2 is also run here on the single map and
+    1 / 16 on the batch)."""
     import eikonal
     from eikonal import _lib as L
 
