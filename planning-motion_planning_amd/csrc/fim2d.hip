@@ -66,6 +66,11 @@ struct alignas(2 * sizeof(R)) Cell {
 // convergence -- a visit whose sweeps changed nothing had no concurrent writes, so its reads
 // were exact.
 constexpr int kAhead = 4;
+// Guard rows (+inf T and cost) above and below the tile's halo ring in LDS.  A sweep clamps its
+// LDS row once per group of kAhead steps -- the group's lowest row into [-(kAhead - 1), kTile + 1]
+// -- and addresses the group's steps with immediate offsets, so a group of a lane outside its
+// window may reach kAhead - 1 rows past a halo row (one more for the upstream-x read).
+constexpr int kGuard = kAhead;
 
 template <typename R, int DX, int DY, bool TRACK>
 __device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lane, R keep) {
@@ -75,9 +80,15 @@ __device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lan
     static_assert((2 * kTile) % D == 0, "pipeline depth must divide the step count");
     char* const base = reinterpret_cast<char*>(Ts);
     const int col = (DX > 0 ? lane : kTile - 1 - lane) + 1;
-    const int lo_b = col * S, hi_b = (kLds - 1) * kRow + col * S;  // LDS rows 0 and 65
-    // step s: tile row r = s - lane -> LDS row (DY > 0 ? r + 1 : 64 - r), clamped to [0, 65]
-    int raw = DY > 0 ? (1 - lane) * kRow + col * S : (kTile + lane) * kRow + col * S;
+    // step s: tile row r = s - lane -> LDS row (DY > 0 ? r + 1 : 64 - r).  A group of D steps
+    // covers D consecutive rows; its LOWEST row (step s going south, s + D - 1 going north) is
+    // clamped into [-(D - 1), 65] once per group and its steps are immediate offsets from it:
+    // while the lane's window lies ahead the group reads guard rows and ends on the start-side
+    // halo row (cur = its T, as the per-step clamp gave); past the window it reads the far halo
+    // and guard rows (cost +inf: no update).  Within the window the rows are exact.
+    const int lo_b = -(D - 1) * kRow + col * S, hi_b = (kLds - 1) * kRow + col * S;
+    int raw = DY > 0 ? (1 - lane) * kRow + col * S : (kTile - (D - 1) + lane) * kRow + col * S;
+    auto off = [](int u) { return (DY > 0 ? u : D - 1 - u) * kRow; };
     auto clampb = [&](int x) {  // one v_med3_i32 (the compiler emits min + cmp + cndmask)
         int r;
         asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo_b), "v"(hi_b));
@@ -86,12 +97,11 @@ __device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lan
     bool changed = false;
     // the upstream halo row value is the lane's "previous row" result before it starts
     R cur = reinterpret_cast<const Cell<R>*>(base + (DY > 0 ? 0 : kLds - 1) * kRow + col * S)->t;
-    int q_o[D];
     R q_old[D], q_upx[D], q_c[D];
+    int gb = clampb(raw);  // lowest row of the group being fetched (byte offset from Ts)
+    raw += DY * D * kRow;
     auto fetch = [&](int u) {
-        const int o = clampb(raw);
-        raw += DY * kRow;
-        q_o[u] = o;
+        const int o = gb + off(u);
         const Cell<R> v = *reinterpret_cast<const Cell<R>*>(base + o);
         q_old[u] = v.t;
         q_c[u] = v.c;
@@ -100,6 +110,9 @@ __device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lan
 #pragma unroll
     for (int u = 0; u < D; ++u) fetch(u);
     for (int s = 0; s < 2 * kTile; s += D) {
+        const int gcur = gb;  // this group's rows (its ds_min targets)
+        gb = clampb(raw);     // the next group's (past the last step: guard / halo rows, unused)
+        raw += DY * D * kRow;
 #pragma unroll
         for (int u = 0; u < D; ++u) {
             // x side: lane 0 takes the halo column; lanes 1.. take lane l-1's fresh value (DPP)
@@ -108,7 +121,7 @@ __device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lan
             // the LDS value); the chain to w is godunov2_chain's (see there)
             const R c2x2 = R(2) * (q_c[u] * q_c[u]);
             const R w = godunov2_chain(umin(wave_shr1_umin_id(cur), q_upx[u]), cur, q_c[u], c2x2);
-            lds_min(&reinterpret_cast<Cell<R>*>(base + q_o[u])->t, w);
+            lds_min(&reinterpret_cast<Cell<R>*>(base + gcur + off(u))->t, w);
             if constexpr (TRACK) changed |= w < q_old[u] * keep;
             cur = umin(w, q_old[u]);  // NaN (both-inf case) sorts above every value: keeps old
             fetch(u);  // refill the slot: step s + u + D (past the last step: clamped halo rows)
@@ -123,10 +136,10 @@ __device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lan
 // LDS of one tile visit
 template <typename R>
 struct TileLds {
-    // tile + halo ring (66 x 66 at offset kLds), plus one guard row above and below (the clamped
-    // r = -1 / 64 steps read one row beyond the halo: in-bounds, +inf, and masked by the +inf halo
-    // cost anyway); halo ring cost = +inf
-    Cell<R> Tc[(kLds + 2) * kLds];
+    // tile + halo ring (66 x 66 at offset kGuard * kLds), plus kGuard guard rows above and below
+    // (+inf T and cost: read by the groups of a sweep outside a lane's window, see sweep_quadrant);
+    // halo ring cost = +inf
+    Cell<R> Tc[(kLds + 2 * kGuard) * kLds];
     unsigned round, flags;
     unsigned flags_acc; // persistent mode: neighbour activations deferred to the visit's end
     unsigned pend;      // persistent mode: the tile's state word as the last pass consumed it
@@ -146,7 +159,7 @@ struct TileLds {
 template <typename R, bool COH>
 __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileLds<R>& L, R keep) {
     constexpr R INF = Real<R>::inf();
-    Cell<R>* const Ts = L.Tc + kLds;
+    Cell<R>* const Ts = L.Tc + kGuard * kLds;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int map = tile / a.tiles_per_map;
     const int rem = tile - map * a.tiles_per_map;
@@ -391,9 +404,9 @@ __device__ __forceinline__ void activate_after(const Fim2dArgs& a, int tile, con
 template <typename R>
 __device__ __forceinline__ void init_guard_rows(TileLds<R>& L) {
     const int tid = threadIdx.x;
-    if (tid < kLds) {
-        L.Tc[tid] = Cell<R>{Real<R>::inf(), Real<R>::inf()};
-        L.Tc[(kLds + 1) * kLds + tid] = Cell<R>{Real<R>::inf(), Real<R>::inf()};
+    for (int i = tid; i < kGuard * kLds; i += kThreads) {
+        L.Tc[i] = Cell<R>{Real<R>::inf(), Real<R>::inf()};
+        L.Tc[(kLds + kGuard) * kLds + i] = Cell<R>{Real<R>::inf(), Real<R>::inf()};
     }
 }
 

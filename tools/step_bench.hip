@@ -9,14 +9,14 @@ using namespace eik;
 __global__ __launch_bounds__(256) void kern(const float* cost, float* out, unsigned long long* cyc, int reps) {
     __shared__ TileLds<float> L;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int i = tid; i < (kLds + 2) * kLds; i += 256) {
-        const int row = i / kLds - 1, colx = i % kLds;
+    for (int i = tid; i < (kLds + 2 * kGuard) * kLds; i += 256) {
+        const int row = i / kLds - kGuard, colx = i % kLds;
         const bool inner = row >= 1 && row <= kTile && colx >= 1 && colx <= kTile;
         L.Tc[i].t = (i % 97 == 0 && inner) ? 0.f : __builtin_inff();
         L.Tc[i].c = inner ? cost[(row - 1) * kTile + colx - 1] : __builtin_inff();
     }
     __syncthreads();
-    Cell<float>* Ts = L.Tc + kLds;
+    Cell<float>* Ts = L.Tc + kGuard * kLds;
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     for (int r = 0; r < reps; ++r) {
         if (wave == 0) sweep_quadrant<float, +1, +1, false>(Ts, lane, 1.f);
