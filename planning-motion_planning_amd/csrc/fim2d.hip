@@ -65,12 +65,10 @@ struct alignas(2 * sizeof(R)) Cell {
 // Another wave's concurrent ds_min may make a pre-read value stale (larger): that only delays
 // convergence -- a visit whose sweeps changed nothing had no concurrent writes, so its reads
 // were exact.
-constexpr int kAhead = 4;
-// Guard rows (+inf T and cost) above and below the tile's halo ring in LDS.  A sweep clamps its
-// LDS row once per group of kAhead steps -- the group's lowest row into [-(kAhead - 1), kTile + 1]
-// -- and addresses the group's steps with immediate offsets, so a group of a lane outside its
-// window may reach kAhead - 1 rows past a halo row (one more for the upstream-x read).
-constexpr int kGuard = kAhead;
+// (kAhead, fim_engine.hpp.)  Guard rows (kGuard, +inf T and cost) above and below the tile's halo
+// ring in LDS: a sweep clamps its LDS row once per group of kAhead steps -- the group's lowest row
+// into [-(kAhead - 1), kTile + 1] -- and addresses the group's steps with immediate offsets, so a
+// group of a lane outside its window may reach kAhead - 1 rows past a halo row.
 
 template <typename R, int DX, int DY, bool TRACK>
 __device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lane, R keep) {

@@ -29,14 +29,15 @@ namespace eik {
 constexpr int kMaxLayers = 4;  // float4 per cell in LDS
 
 struct TileLdsL {
-    float4 Tbuf[(kLds + 2) * kLds];  // tile + halo ring (66 x 66 at offset kLds), guard row above and below
+    float4 Tbuf[(kLds + 2 * kGuard) * kLds];  // tile + halo ring (66 x 66 at offset kGuard * kLds), guard rows
+                                              // above and below (fim2d.hip's sweep_quadrant)
     float4 Cs[kLds * kLds];          // same layout as the ring; halo = +inf
     unsigned flags;
     unsigned key[5];
     int tile;
     unsigned dirs;
 };
-static_assert(offsetof(TileLdsL, Cs) == sizeof(float4) * (kLds + 2) * kLds, "Cs must follow Tbuf");
+static_assert(offsetof(TileLdsL, Cs) == sizeof(float4) * (kLds + 2 * kGuard) * kLds, "Cs must follow Tbuf");
 
 __device__ __forceinline__ float f4get(const float4& v, int z) { return z == 0 ? v.x : z == 1 ? v.y : z == 2 ? v.z : v.w; }
 
@@ -67,13 +68,16 @@ __device__ __forceinline__ void sweep_layered(float4* __restrict__ Ts, int lane)
     constexpr float INF = __builtin_inff();
     constexpr int S = (int)sizeof(float4);
     constexpr int kRow = kLds * S;
-    constexpr int kCsB = (kLds + 1) * kLds * S;  // Cs - Ts in bytes
-    constexpr int D = 4;
+    constexpr int kCsB = (kLds + kGuard) * kLds * S;  // Cs - Ts in bytes
+    constexpr int D = kAhead;
     char* const base = reinterpret_cast<char*>(Ts);
     auto ld = [&](int off) { return *reinterpret_cast<const float4*>(base + off); };
     const int col = (DX > 0 ? lane : kTile - 1 - lane) + 1;
-    const int lo_b = col * S, hi_b = (kLds - 1) * kRow + col * S;
-    int raw = DY > 0 ? (1 - lane) * kRow + col * S : (kTile + lane) * kRow + col * S;
+    // the LDS row is clamped once per group of D steps (its lowest row into [-(D - 1), 65]) and the
+    // group's steps are immediate offsets from it, as in fim2d.hip's sweep_quadrant
+    const int lo_b = -(D - 1) * kRow + col * S, hi_b = (kLds - 1) * kRow + col * S;
+    int raw = DY > 0 ? (1 - lane) * kRow + col * S : (kTile - (D - 1) + lane) * kRow + col * S;
+    auto off = [](int u) { return (DY > 0 ? u : D - 1 - u) * kRow; };
     auto clampb = [&](int x) {
         int r;
         asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo_b), "v"(hi_b));
@@ -83,12 +87,11 @@ __device__ __forceinline__ void sweep_layered(float4* __restrict__ Ts, int lane)
     float cur[NL];
 #pragma unroll
     for (int z = 0; z < NL; ++z) cur[z] = f4get(h, z);
-    int q_o[D];
     float4 q_old[D], q_upx[D], q_c[D];
+    int gb = clampb(raw);  // lowest row of the group being fetched
+    raw += DY * D * kRow;
     auto fetch = [&](int u) {
-        const int o = clampb(raw);
-        raw += DY * kRow;
-        q_o[u] = o;
+        const int o = gb + off(u);
         q_old[u] = ld(o);
         q_upx[u] = ld(o - DX * S);
         q_c[u] = ld(o + kCsB);
@@ -96,9 +99,12 @@ __device__ __forceinline__ void sweep_layered(float4* __restrict__ Ts, int lane)
 #pragma unroll
     for (int u = 0; u < D; ++u) fetch(u);
     for (int s = 0; s < 2 * kTile; s += D) {
+        const int gcur = gb;
+        gb = clampb(raw);
+        raw += DY * D * kRow;
 #pragma unroll
         for (int u = 0; u < D; ++u) {
-            float* const cell = reinterpret_cast<float*>(base + q_o[u]);
+            float* const cell = reinterpret_cast<float*>(base + gcur + off(u));
 #pragma unroll
             for (int z = 0; z < NL; ++z) {
                 const float old = f4get(q_old[u], z);
@@ -123,7 +129,7 @@ template <int NL, bool COH>
 __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int tile, TileLdsL& L, float keep) {
     constexpr float INF = __builtin_inff();
     const float4 INF4 = make_float4(INF, INF, INF, INF);
-    float4* const Ts = L.Tbuf + kLds;
+    float4* const Ts = L.Tbuf + kGuard * kLds;
     float4* const Cs = L.Cs;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int map = tile / a.tiles_per_map;
@@ -264,9 +270,9 @@ template <int NL>
 __global__ __launch_bounds__(kThreads) void fim2dl_persist_kernel(Fim2dArgs a) {
     __shared__ TileLdsL L;
     constexpr float INF = __builtin_inff();
-    if (threadIdx.x < kLds) {  // guard rows: read by clamped steps, never written
-        L.Tbuf[threadIdx.x] = make_float4(INF, INF, INF, INF);
-        L.Tbuf[(kLds + 1) * kLds + threadIdx.x] = make_float4(INF, INF, INF, INF);
+    for (int i = threadIdx.x; i < kGuard * kLds; i += kThreads) {  // guard rows: read by sweeps, never lowered
+        L.Tbuf[i] = make_float4(INF, INF, INF, INF);
+        L.Tbuf[(kLds + kGuard) * kLds + i] = make_float4(INF, INF, INF, INF);
     }
     const float keep = a.keep;
     int tile = -1;

@@ -8,6 +8,12 @@
 
 namespace eik {
 
+// quadrant sweeps (fim2d.hip sweep_quadrant, fim2dl.hip sweep_layered): software pipeline depth
+// in steps, and the +inf guard rows above and below the staged tile that its per-group row clamp
+// needs
+constexpr int kAhead = 4;
+constexpr int kGuard = kAhead;
+
 // per-tile queue state (persistent mode): pending / busy, plus what activated the tile since its
 // last visit -- a halo side that improved (its information flows away from that side) or the
 // tile itself (last visit changed it: every direction)
