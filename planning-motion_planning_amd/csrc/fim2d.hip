@@ -52,9 +52,10 @@ struct alignas(2 * sizeof(R)) Cell {
 // -- the same fixed point as reading both neighbours per axis in every sweep (tools/sched_sim.c:
 // identical field, +1 % passes on the 4096^2 DEM), for 2 LDS reads per step instead of 5 (the
 // sweep is LDS-bound at three workgroups per CU: 14 -> 8 LDS cycles per wave-step).
-// Branch- and select-free: r is clamped to [-1, 64] (one add + one med3 on the byte offset);
-// rows -1 and 64 are the halo rows, whose cost is +inf, so a lane outside the tile computes +inf
-// or NaN and its ds_min / min / `<` are no-ops.  TRACK: also report whether any cell decreased by
+// Branch- and select-free: the LDS row is clamped once per group of kAhead steps (one add + one
+// med3 per group, immediate offsets per step); the rows a lane outside the tile reaches are halo
+// and guard rows, whose cost is +inf, so it computes +inf or NaN and its ds_min / min / `<` are
+// no-ops.  TRACK: also report whether any cell decreased by
 // more than the tolerance (only needed for multi-round visits; single-round visits read it off
 // the write-back).
 // Software pipeline depth of a sweep: the LDS reads of step s + kAhead are issued at step s,
