@@ -4,17 +4,20 @@
   torchrun --nproc-per-node N bench.py --gpus N ...                 # driver, N > 1
 
 Workload (BASELINE.json configs): N = 1 -> config[1], a 4096 x 4096 DEM-derived cost raster
-(terrain.py: fractal DEM seed 42 + the planner's cost recipe), single goal at the centre, fp32
-block-FIM.  N > 1 -> weak scaling: every rank owns a 4096 x 4096 block of ONE global raster
-(px x py = 2x1, 2x2, 4x2 -> 8192 x 4096, 8192^2, 16384 x 8192), single goal at the global
-centre, halo exchange over RCCL (eikonal/dd.py).  A "step" = one full solve of the whole raster
-(T init -> converged), inputs resident in HBM.  value = cells of the global raster x steps /
-max-over-ranks wall time (Gcells/s).
+(terrain.py: fractal DEM seed 42 + the planner's cost recipe), single goal at the centre,
+block-FIM in float64 -- the reference's arithmetic type (FastMarching.py:93-95 works on float64
+rasters) and the drop-in's default; `--dtype f32` measures the fp32 solver instead (also reported
+in extra_configs).  N > 1 -> config[3], strong scaling (default): ONE 16384 x 16384 raster
+(terrain seed 7, goal at the centre) split over the ranks (px x py = 2x1, 2x2, 4x2 blocks of
+16384 x 8192, 8192^2, 8192 x 4096); `--scaling weak` gives every rank a --block^2 block of a
+growing raster instead.  A "step" = one full solve of the whole raster (T init -> converged),
+inputs resident in HBM.  value = cells of the global raster x steps / max-over-ranks wall time
+(Gcells/s).
 
 Also reported: roofline of the dominant kernel (fim2d_persist_kernel, one launch per solve:
 hipEvents around it on the solver stream over the timed region; algorithmic bytes = full tile
-visits x 50176 B + in-place passes x 17408 B), ms-to-path (host cost -> host path,
-N = 1), and the CPU baseline (oracle C heap FMM, 1 thread, N = 1).
+visits x 50176 B + in-place passes x 17408 B in fp32, twice that in fp64), ms-to-path
+(host cost -> host path, N = 1), and the CPU baseline (oracle C heap FMM, 1 thread, N = 1).
 """
 import argparse
 import json
@@ -35,8 +38,11 @@ from eikonal import _lib as L  # noqa: E402
 
 METRIC = "Eikonal Gcells/s + ms-to-path, 4k² & 16k² costmap at 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
-BYTES_PER_VISIT = 4 * (3 * 64 * 64 + 4 * 64)  # fp32: cost read + T read + T write + halo read
-BYTES_PER_PASS = 4 * (64 * 64 + 4 * 64)  # fp32 in-place pass: T write + halo re-read
+# per element byte: cost read + T read + T write + halo read per full visit; T write + halo
+# re-read per in-place pass (x 4 for fp32, x 8 for fp64)
+CELLS_PER_VISIT = 3 * 64 * 64 + 4 * 64
+CELLS_PER_PASS = 64 * 64 + 4 * 64
+WIDE_TILES = 16384  # fp32 maps of >= this many tiles run the 4-waves-per-SIMD kernel (csrc kWideTiles)
 
 
 def env_int(k, d):
@@ -48,7 +54,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--block", type=int, default=4096, help="per-rank block side (cells)")
+    ap.add_argument("--dtype", choices=["f64", "f32"], default="f64",
+                    help="solver arithmetic (the reference computes in float64)")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="N > 1: strong = one --c4-size^2 raster split over the ranks (configs[3]); "
+                         "weak = a --block^2 block per rank")
+    ap.add_argument("--c4-size", type=int, default=16384, help="strong scaling: global raster side")
+    ap.add_argument("--block", type=int, default=4096, help="weak scaling / N = 1: block side (cells)")
     ap.add_argument("--exchange-every", type=int, default=8, help="--dd rounds: outer iterations per exchange")
     ap.add_argument("--dd", choices=["live", "rounds"], default="live",
                     help="N > 1: live persistent launches + IPC halo rounds, or relaunch-per-round over RCCL")
@@ -58,8 +70,15 @@ def main():
     ap.add_argument("--no-timing", action="store_true", help="skip per-launch events (roofline)")
     ap.add_argument("--no-extra", action="store_true", help="skip the C3 / C5 secondary measurements")
     ap.add_argument("--extra-steps", type=int, default=5)
-    ap.add_argument("--pmc-traffic", type=str, default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--pmc-traffic", type=str, default=None,
+                    help="PMC summary (tools/pmc_traffic.py); default profiles/pmc_traffic_<dtype>.json")
     args = ap.parse_args()
+    f64 = args.dtype == "f64"
+    tdt = torch.float64 if f64 else torch.float32
+    edt = L.EIK_F64 if f64 else L.EIK_F32
+    esz = 8 if f64 else 4
+    if args.pmc_traffic is None:
+        args.pmc_traffic = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.dtype}.json")
 
     world = env_int("WORLD_SIZE", 1)
     rank = env_int("RANK", 0)
@@ -77,28 +96,34 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=dev)
     px, py = dd.SPLITS[world]
-    H, W = args.block * py, args.block * px
+    strong = world > 1 and args.scaling == "strong"
+    if strong:  # configs[3]: one 16384^2 raster (seed 7), split over the ranks
+        H = W = args.c4_size
+        seed = 7
+    else:
+        H, W = args.block * py, args.block * px
+        seed = 42
     blk = dd.Block(H, W, px, py, rank)
     goal_g = (W // 2, H // 2)
 
-    cost = terrain.cost_block(blk.y0, blk.x0, blk.h, blk.w, H, W, seed=42, device=dev).contiguous()
+    cost = terrain.cost_block(blk.y0, blk.x0, blk.h, blk.w, H, W, seed=seed, device=dev).to(tdt).contiguous()
     T = torch.empty_like(cost)
     stream = torch.cuda.current_stream(dev)
     ctx = eikonal.Context(local_rank)
     ctx.set_option(L.OPT_SYNC_EVERY, args.sync_every)
     if shared and world > 1:
         ctx.set_option(L.OPT_GRID, max(2, 2 * torch.cuda.get_device_properties(dev).multi_processor_count // world))
-    fim = eikonal.Fim2d(ctx, 1, blk.h, blk.w, L.EIK_F32)
+    fim = eikonal.Fim2d(ctx, 1, blk.h, blk.w, edt)
     lgoal = blk.local_goal(*goal_g)
 
     dd_mode = args.dd if world > 1 else None
     if world > 1:
-        send, recv, ghost = dd.make_strips(blk, torch.float32, dev, float("inf"))
+        send, recv, ghost = dd.make_strips(blk, tdt, dev, float("inf"))
         ctrl = dd.control_group()
         halo, live_err, vote = None, None, None
         if dd_mode == "live":  # every rank must agree, or all fall back to rounds
             try:
-                halo = dd.IpcHalo(ctx, blk, 4, group=ctrl)
+                halo = dd.IpcHalo(ctx, blk, esz, group=ctrl)
             except Exception as e:
                 live_err = repr(e)
             if env_int("LOCAL_WORLD_SIZE", world) == world and not live_err:
@@ -177,17 +202,21 @@ def main():
 
     # roofline of the dominant kernel (rank-local: this rank's launches and its event time)
     launches = iters
-    alg_bytes = visits * BYTES_PER_VISIT + passes * BYTES_PER_PASS
+    alg_bytes = esz * (visits * CELLS_PER_VISIT + passes * CELLS_PER_PASS)
     achieved = (alg_bytes / (sweep_ms * 1e-3) / 1e9) if sweep_ms > 0 else None
     traffic = None
-    if os.path.exists(args.pmc_traffic):
+    wide = not f64 and ((blk.h + 63) // 64) * ((blk.w + 63) // 64) >= WIDE_TILES
+    kname = f"fim2d_persist_kernel<{'double' if f64 else 'float'}, {4 if wide else 1}>"
+    if world == 1 and os.path.exists(args.pmc_traffic):  # measured on this workload (profiles/)
         try:
-            traffic = json.load(open(args.pmc_traffic)).get("bytes_per_launch")
+            pm = json.load(open(args.pmc_traffic))
+            if pm.get("dtype", args.dtype) == args.dtype:
+                traffic = pm.get("bytes_per_launch")
         except Exception:
             traffic = None
     roof = {
         "bound": "hbm",
-        "kernel": "fim2d_persist_kernel<float, 1>",
+        "kernel": kname,
         "achieved": round(achieved, 2) if achieved else None,
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
@@ -195,8 +224,8 @@ def main():
         "traffic": traffic,
         "alg_bytes_per_launch": round(alg_bytes / max(launches, 1)),
         # one read of cost + one write of T per cell, and the FIM redundancy over it
-        "lower_bound_gbs": round(8 * H * W / (el / args.steps) / 1e9, 2),
-        "redundancy": round(alg_bytes / max(launches, 1) / (8 * H * W), 2) if launches else None,
+        "lower_bound_gbs": round(2 * esz * H * W / (el / args.steps) / 1e9, 2),
+        "redundancy": round(alg_bytes / max(launches, 1) / (2 * esz * blk.h * blk.w), 2) if launches else None,
         "avg_launch_us": round(sweep_ms * 1e3 / max(launches, 1), 2),
         "instrumented_ms_per_step": round(el_i / args.steps * 1e3, 4),
         "launches_per_solve": round(launches / args.steps, 1),
@@ -213,21 +242,26 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic (fractal DEM seed 42 -> planner cost recipe, eikonal/terrain.py)",
+        "dtype": args.dtype,
+        "data": f"synthetic (fractal DEM seed {seed} -> planner cost recipe, eikonal/terrain.py)",
         "config": {
             "workload": ("C2: 4096x4096 DEM-derived cost raster, single goal, FIM on 1 MI355X" if world == 1 else
-                         f"C4-weak: {H}x{W} DEM-derived raster, {px}x{py} blocks of {args.block}^2, halo: "
-                         + ("live persistent launches + IPC peer stores" if dd_mode == "live" else "RCCL rounds")),
-            "H": H, "W": W, "split": f"{px}x{py}", "goal": list(goal_g), "tile": 64,
+                         (f"C4: {H}x{W} DEM-derived raster (seed 7), goal at the centre, {px}x{py} split over "
+                          f"{world} GPUs" if strong else
+                          f"C4-weak: {H}x{W} DEM-derived raster, {px}x{py} blocks of {args.block}^2")
+                         + ", halo: " + ("live persistent launches + IPC peer stores over xGMI"
+                                         if dd_mode == "live" else "RCCL point-to-point rounds")),
+            "H": H, "W": W, "split": f"{px}x{py}", "block": [blk.h, blk.w], "goal": list(goal_g), "tile": 64,
             "parallelism": "single-gpu" if world == 1 else f"domain-decomposition {px}x{py}",
         },
         "roofline": roof,
     }
     if world > 1:
         out["config"]["dd_mode"] = dd_mode + (" (shm vote)" if dd_mode == "live" and vote is not None else "")
+        out["config"]["halo_transport"] = ("hipIpc peer stores (xGMI) + node vote" if dd_mode == "live"
+                                           else "RCCL batch_isend_irecv + all_reduce")
         out["config"]["dd_halo_consistent"] = dd_ok
         rr = dd_rounds[-args.steps:]
         out["config"]["dd_rounds_per_solve"] = round(sum(rr) / max(len(rr), 1), 1)
@@ -236,18 +270,28 @@ def main():
             out["config"]["dd_live_error"] = live_err[:200]
 
     if rank == 0 and world == 1 and not args.no_path:
-        out.update(ms_to_path(cost, ctx, fim, dev, stream, goal_g))
+        out.update(ms_to_path(cost, ctx, fim, dev, stream, goal_g, edt))
+
+    if world > 1 and not args.no_extra:  # configs[2] sharded: 128 / N maps per rank, no collective
+        c3 = bench_batch(ctx, dev, stream, args.extra_steps, tdt, edt, rank=rank, world=world, group=ctrl)
+        if rank == 0:
+            out["extra_configs"] = {"C3_sharded": c3}
 
     if rank == 0 and world == 1 and not args.no_extra:
         del T
         torch.cuda.empty_cache()
+        other = "f32" if f64 else "f64"
         out["extra_configs"] = {
-            "C3": bench_batch(ctx, dev, stream, args.extra_steps),
-            "C5": bench_layers(ctx, dev, stream, cost, goal_g, args.extra_steps),
+            f"C2_{other}": bench_c2(ctx, dev, stream, cost, goal_g, args.extra_steps, other),
+            "C3": bench_batch(ctx, dev, stream, args.extra_steps, tdt, edt),
+            "C5": bench_layers(ctx, dev, stream, cost.float(), goal_g, args.extra_steps),
             "costmap": bench_costmap(ctx, dev, stream, args.extra_steps, goal_g),
-            "C4_1gpu": bench_c4(ctx, dev, stream, max(2, args.extra_steps // 2)),
+            "C4_1gpu": bench_c4(ctx, dev, stream, max(2, args.extra_steps // 2), tdt, edt),
             "arm": bench_arm(ctx, args.extra_steps),
         }
+        if f64:
+            out["extra_configs"]["C4_1gpu_f32"] = bench_c4(ctx, dev, stream, max(2, args.extra_steps // 2),
+                                                            torch.float32, L.EIK_F32)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cost, goal_g)
@@ -258,7 +302,7 @@ def main():
         dist.destroy_process_group()
 
 
-def ms_to_path(cost, ctx, fim, dev, stream, goal, start=(256, 256), reps=3):
+def ms_to_path(cost, ctx, fim, dev, stream, goal, edt, start=(256, 256), reps=3):
     """host cost (pageable numpy) -> H2D -> solve -> path kernel -> D2H path."""
     host_cost = cost.cpu().numpy()
     cap = 30004
@@ -276,7 +320,7 @@ def ms_to_path(cost, ctx, fim, dev, stream, goal, start=(256, 256), reps=3):
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         fim.solve(c.data_ptr(), T.data_ptr(), [goal], stream.cuda_stream)
-        ctx._chk(L.lib().eik_path2d_dev(ctx._h, T.data_ptr(), L.EIK_F32, H, W, np.array(start, np.float64),
+        ctx._chk(L.lib().eik_path2d_dev(ctx._h, T.data_ptr(), edt, H, W, np.array(start, np.float64),
                                         np.array(goal, np.float64), 0.5, out_d.data_ptr(), cap, n_d.data_ptr(),
                                         st_d.data_ptr(), stream.cuda_stream))
         e1.record(stream)
@@ -301,40 +345,80 @@ def timed_loop(fn, steps, warmup=1):
     return (time.perf_counter() - t0) / steps
 
 
-def bench_batch(ctx, dev, stream, steps, B=128, N=1024):
+def c3_goal(cost_b, b, N):
+    """A goal on a finite, low-cost cell of map b (its own generator: any rank can draw it)."""
+    rng = np.random.default_rng(1000 + b)
+    while True:
+        gx, gy = (int(v) for v in rng.integers(N // 8, N - N // 8, 2))
+        if float(cost_b[gy, gx]) < 50:
+            return gx, gy
+
+
+def bench_batch(ctx, dev, stream, steps, tdt, edt, B=128, N=1024, rank=0, world=1, group=None):
     """configs[2]: 128 maps of 1024^2 (terrain seeds 1000..1127, one goal per map), ONE batched
-    persistent solve (tiles of all maps share the device FIFO).  A step = the whole batch."""
-    cost = torch.empty((B, N, N), dtype=torch.float32, device=dev)
+    persistent solve (tiles of all maps share the device FIFO).  A step = the whole batch.  With
+    world > 1 the batch is sharded (maps [rank * B / world, (rank + 1) * B / world) per rank, no
+    collective in the solve); the time is the max over ranks."""
+    lo, hi = rank * B // world, (rank + 1) * B // world
+    nb = hi - lo
+    cost = torch.empty((nb, N, N), dtype=tdt, device=dev)
     goals = []
-    rng = np.random.default_rng(1000)
-    for b in range(B):
-        cost[b] = terrain.cost_block(0, 0, N, N, N, N, seed=1000 + b, device=dev)
-        while True:  # a goal on a finite, low-cost cell
-            gx, gy = (int(v) for v in rng.integers(N // 8, N - N // 8, 2))
-            if float(cost[b, gy, gx]) < 50:
-                break
-        goals.append((gx, gy))
+    for i, b in enumerate(range(lo, hi)):
+        cost[i] = terrain.cost_block(0, 0, N, N, N, N, seed=1000 + b, device=dev).to(tdt)
+        goals.append(c3_goal(cost[i], b, N))
     T = torch.empty_like(cost)
-    fim = eikonal.Fim2d(ctx, B, N, N, L.EIK_F32)
+    fim = eikonal.Fim2d(ctx, nb, N, N, edt)
+    if world > 1:
+        dist.barrier()
     sec = timed_loop(lambda: fim.solve(cost.data_ptr(), T.data_ptr(), goals, stream.cuda_stream), steps)
+    if world > 1:
+        tt = torch.tensor([sec], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=group)
+        sec = tt.item()
     st = fim.stats()
     reach = float(torch.isfinite(T).float().mean())
     fim.close()
     del cost, T
     torch.cuda.empty_cache()
-    return {"workload": f"configs[2]: batch {B} x {N}x{N} terrain maps (seeds 1000..{1000 + B - 1}), one goal each",
+    return {"workload": f"configs[2]: batch {B} x {N}x{N} terrain maps (seeds 1000..{1000 + B - 1}), one goal each"
+                        + (f", sharded {nb} maps per rank over {world} GPUs" if world > 1 else ""),
+            "dtype": "f64" if edt == L.EIK_F64 else "f32",
             "value": round(B * N * N / sec / 1e9, 4), "unit": "Gcells/s", "ms_per_step": round(sec * 1e3, 4),
             "steps": steps, "tile_visits_per_solve": st["tile_visits"], "inplace_passes_per_solve": st["inplace_passes"],
             "reached_fraction": round(reach, 4)}
 
 
-def bench_c4(ctx, dev, stream, steps, N=16384):
+def bench_c2(ctx, dev, stream, cost, goal, steps, dtype):
+    """configs[1] in the other arithmetic type (same raster), with its kernel's event time."""
+    f64 = dtype == "f64"
+    c = cost.to(torch.float64 if f64 else torch.float32).contiguous()
+    T = torch.empty_like(c)
+    fim = eikonal.Fim2d(ctx, 1, c.shape[0], c.shape[1], L.EIK_F64 if f64 else L.EIK_F32)
+    sec = timed_loop(lambda: fim.solve(c.data_ptr(), T.data_ptr(), [goal], stream.cuda_stream), steps)
+    ctx.set_option(L.OPT_TIMING, 1)
+    fim.solve(c.data_ptr(), T.data_ptr(), [goal], stream.cuda_stream)
+    st = fim.stats()
+    ctx.set_option(L.OPT_TIMING, 0)
+    esz = 8 if f64 else 4
+    alg = esz * (st["tile_visits"] * CELLS_PER_VISIT + st["inplace_passes"] * CELLS_PER_PASS)
+    fim.close()
+    del c, T
+    torch.cuda.empty_cache()
+    return {"workload": f"configs[1] in {dtype}: the same 4096x4096 raster and goal",
+            "dtype": dtype, "value": round(cost.numel() / sec / 1e9, 4), "unit": "Gcells/s",
+            "ms_per_step": round(sec * 1e3, 4), "steps": steps,
+            "kernel_ms": round(st["sweep_ms"], 4), "alg_bytes_per_launch": int(alg),
+            "roofline_frac": round(alg / (st["sweep_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if st["sweep_ms"] else None,
+            "tile_visits_per_solve": st["tile_visits"], "inplace_passes_per_solve": st["inplace_passes"]}
+
+
+def bench_c4(ctx, dev, stream, steps, tdt, edt, N=16384):
     """configs[3] on ONE GPU: the 16384^2 DEM-derived raster (terrain seed 7), goal at the centre,
     solved whole (1 GiB cost + 1 GiB T in HBM).  The N = 4 / 8 driver runs measure the split
     versions; this line is the single-GPU reference point of the same raster size."""
-    cost = terrain.cost_block(0, 0, N, N, N, N, seed=7, device=dev).contiguous()
+    cost = terrain.cost_block(0, 0, N, N, N, N, seed=7, device=dev).to(tdt).contiguous()
     T = torch.empty_like(cost)
-    fim = eikonal.Fim2d(ctx, 1, N, N, L.EIK_F32)
+    fim = eikonal.Fim2d(ctx, 1, N, N, edt)
     goal = (N // 2, N // 2)
     sec = timed_loop(lambda: fim.solve(cost.data_ptr(), T.data_ptr(), [goal], stream.cuda_stream), steps)
     st = fim.stats()
@@ -343,7 +427,7 @@ def bench_c4(ctx, dev, stream, steps, N=16384):
     del cost, T
     torch.cuda.empty_cache()
     return {"workload": f"configs[3] at 1 GPU: {N}x{N} DEM-derived raster (seed 7), single goal at the centre, 1x1",
-            "value": round(N * N / sec / 1e9, 4), "unit": "Gcells/s", "ms_per_step": round(sec * 1e3, 4),
+            "dtype": "f64" if edt == L.EIK_F64 else "f32", "value": round(N * N / sec / 1e9, 4), "unit": "Gcells/s", "ms_per_step": round(sec * 1e3, 4),
             "steps": steps, "tile_visits_per_solve": st["tile_visits"], "inplace_passes_per_solve": st["inplace_passes"],
             "reached_fraction": round(reach, 4)}
 
@@ -436,7 +520,7 @@ def bench_layers(ctx, dev, stream, cost2d, goal, steps, Lz=3):
     res = {"workload": f"configs[4]: coupled {H}x{W}x{Lz} layered costmap (x, y, locomotion mode), FM3D semantics, "
                        f"z padded with +inf layers ({Lm} in memory)",
            "reached_fraction": round(float(torch.isfinite(T[:, :, 1:1 + Lz]).float().mean()), 4),
-           "solve_ms_device": round(st.get("solve_ms", 0.0), 4),
+           "dtype": "f32", "solve_ms_device": round(st.get("solve_ms", 0.0), 4),
            "value": round(H * W * Lz / sec / 1e9, 4), "unit": "Gcells/s", "ms_per_step": round(sec * 1e3, 4),
            "steps": steps, "launches_per_solve": st.get("iterations"), "tile_visits_per_solve": st.get("tile_visits"),
            "path_ms_device": round(e0.elapsed_time(e1), 3), "path_points": int(n_d.item()),

@@ -516,8 +516,16 @@ static int update3d(fmm3d_t *f, int64_t nx, int64_t ny, int64_t nz) {
 }
 
 /* FM3D computeTmap :126-145 (early exit when start is popped, :141) */
+int orc_fmm3d_trace(const double *cost, int64_t H, int64_t W, int64_t L, const int64_t *goal, const int64_t *start,
+                    double *T, int64_t *popidx);
 int orc_fmm3d(const double *cost, int64_t H, int64_t W, int64_t L, const int64_t *goal, const int64_t *start,
               double *T) {
+    return orc_fmm3d_trace(cost, H, W, L, goal, start, T, NULL);
+}
+/* same, optionally recording the pop order (popidx[cell] = 0 for the goal, k for the k-th pop,
+   -1 for cells never popped) -- test instrumentation for the early-exit reconstruction */
+int orc_fmm3d_trace(const double *cost, int64_t H, int64_t W, int64_t L, const int64_t *goal, const int64_t *start,
+                    double *T, int64_t *popidx) {
     if (!cost || !T || !goal || H < 1 || W < 1 || L < 1) return ORC_ERR_ARG;
     int64_t gx = goal[0], gy = goal[1], gz = goal[2];
     if (gx < 0 || gy < 0 || gz < 0 || gx >= W || gy >= H || gz >= L) return ORC_ERR_ARG;
@@ -527,14 +535,18 @@ int orc_fmm3d(const double *cost, int64_t H, int64_t W, int64_t L, const int64_t
     for (int64_t i = 0; i < N; ++i) {
         T[i] = INFINITY;
         f.closed[i] = (cost[i] == INFINITY);
+        if (popidx) popidx[i] = -1;
     }
     int64_t g = (gy * W + gx) * L + gz;
     T[g] = 0;
     f.closed[g] = 1;
+    if (popidx) popidx[g] = 0;
+    int64_t npop = 0;
     int rc = update3d(&f, gx, gy, gz);
     while (rc == ORC_OK && heap_clean(&f.hp)) {
         int64_t node = heap_pop(&f.hp);
         f.closed[node] = 1;
+        if (popidx) popidx[node] = ++npop;
         int64_t z = node % L, xy = node / L, x = xy % W, y = xy / W;
         rc = update3d(&f, x, y, z);
         if (start && x == start[0] && y == start[1] && z == start[2]) break;

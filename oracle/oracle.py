@@ -47,6 +47,7 @@ def lib():
         L.orc_interp3.argtypes = [C.c_double] * 3 + [_dp, i64, i64, i64, C.POINTER(C.c_int)]
         L.orc_gdm2d.argtypes = [_dp, i64, i64] + [C.c_double] * 5 + [_dp, i64, C.POINTER(i64), C.POINTER(C.c_int)]
         L.orc_fmm3d.argtypes = [_dp, i64, i64, i64, _ip, C.c_void_p, _dp]
+        L.orc_fmm3d_trace.argtypes = [_dp, i64, i64, i64, _ip, C.c_void_p, _dp, _ip]
         L.orc_gdm3d.argtypes = [_dp, i64, i64, i64, _dp, _dp, C.c_double, _dp, i64, C.POINTER(i64),
                                 C.POINTER(C.c_int)]
         L.orc_set_strict.argtypes = [C.c_int]
@@ -158,6 +159,19 @@ def fmm3d(cost, goal, start=None):
     s = None if start is None else np.ascontiguousarray(start, dtype=np.int64)
     _chk(lib().orc_fmm3d(cost, H, W, L, g, None if s is None else s.ctypes.data, T))
     return T
+
+
+def fmm3d_trace(cost, goal, start=None):
+    """fmm3d plus the pop order: (T, popidx) with popidx = 0 at the goal, k for the k-th pop of
+    getMinNB (FastMarching3D.py:138), -1 for cells never popped."""
+    cost = _f64(cost)
+    H, W, L = cost.shape
+    T = np.empty_like(cost)
+    pop = np.empty(cost.shape, np.int64)
+    g = np.ascontiguousarray(goal, dtype=np.int64)
+    s = None if start is None else np.ascontiguousarray(start, dtype=np.int64)
+    _chk(lib().orc_fmm3d_trace(cost, H, W, L, g, None if s is None else s.ctypes.data, T, pop))
+    return T, pop
 
 
 def gdm3d(T, init, end, tau=0.5, max_out=None):

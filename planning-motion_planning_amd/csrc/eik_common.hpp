@@ -116,13 +116,42 @@ __device__ __forceinline__ float godunov2_chain(float a, float b, float c, float
     const float q = __builtin_fmaf(-d, d, c2x2);
     return __builtin_fmaf(0.5f, d + __builtin_amdgcn_sqrtf(q), lo);
 }
+// fp64 sweep step (the headline arithmetic: the reference computes in float64).  Two savings over
+// the generic form, 45 -> 28 instructions per step:
+//  * minimum of two values that are >= 0, +inf or a quiet NaN (the only NaNs a sweep makes: inf - inf
+//    and the all-ones lane-0 identity) as ONE v_min_f64: in IEEE mode it is minNum -- a quiet-NaN
+//    operand yields the other one, exactly as the unsigned umin, which takes v_cmp_lt_u64 + 2
+//    v_cndmask for 64-bit values;
+//  * the square root of q = 2c^2 - d^2 in [c^2, 2c^2] without the range scaling of the compiler's
+//    sequence (sqrt_sweep).
+__device__ __forceinline__ double fmin_nn(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// sqrt(q) for q >= 0: v_rsq_f64, one Goldschmidt step and one Newton correction -- the compiler's
+// correctly rounded sequence minus its ldexp range scaling (an identity for q in [2^-1000, 2^1000],
+// so q is clamped below to 2^-1000: a zero-cost cell, q = 0, gives 2^-500, which vanishes against lo)
+// and minus its last correction (result within ~1 ulp; the field tolerance is 1e-9 absolute).
+// q = +inf or NaN (a +inf cost) gives NaN: no update, as sqrt's +inf / NaN did.
+__device__ __forceinline__ double sqrt_sweep(double q) {
+    double qc;
+    asm("v_max_f64 %0, %1, %2" : "=v"(qc) : "v"(q), "v"(0x1p-1000));
+    const double y = __builtin_amdgcn_rsq(qc);
+    double g = qc * y, h = 0.5 * y;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    const double e = __builtin_fma(-g, g, qc);
+    return __builtin_fma(e, h, g);
+}
 __device__ __forceinline__ double godunov2_chain(double a, double b, double c, double c2x2) {
-    const double lo = umin(a, b);
+    const double lo = fmin_nn(a, b);
     const double diff = a - b;
     double d;
     asm("v_min_f64 %0, |%1|, %2" : "=v"(d) : "v"(diff), "v"(c));
     const double q = __builtin_fma(-d, d, c2x2);
-    return __builtin_fma(0.5, d + __builtin_sqrt(q), lo);
+    return __builtin_fma(0.5, d + sqrt_sweep(q), lo);
 }
 
 // Whole-wave shift by one lane (lane i <- lane i-1) on the DPP path: v_mov_b32_dpp wave_shr:1.

@@ -119,10 +119,21 @@ __device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lan
             // one v_min_u32_dpp serves both (lane 0, whose shift source is out of range, keeps
             // the LDS value); the chain to w is godunov2_chain's (see there)
             const R c2x2 = R(2) * (q_c[u] * q_c[u]);
-            const R w = godunov2_chain(umin(wave_shr1_umin_id(cur), q_upx[u]), cur, q_c[u], c2x2);
-            lds_min(&reinterpret_cast<Cell<R>*>(base + gcur + off(u))->t, w);
-            if constexpr (TRACK) changed |= w < q_old[u] * keep;
-            cur = umin(w, q_old[u]);  // NaN (both-inf case) sorts above every value: keeps old
+            R w;
+            if constexpr (sizeof(R) == 8) {
+                // fp64: the DPP move cannot fold into a 64-bit min, so lanes 1.. take lane l-1's
+                // fresh value alone (it is at most the prefetched LDS value of the same cell, read
+                // one step earlier) and lane 0 keeps the halo column's LDS value (the DPP's old)
+                w = godunov2_chain(wave_shr1(cur, q_upx[u]), cur, q_c[u], c2x2);
+                lds_min(&reinterpret_cast<Cell<R>*>(base + gcur + off(u))->t, w);
+                if constexpr (TRACK) changed |= w < q_old[u] * keep;
+                cur = fmin_nn(w, q_old[u]);  // NaN (both-inf case): keeps old
+            } else {
+                w = godunov2_chain(umin(wave_shr1_umin_id(cur), q_upx[u]), cur, q_c[u], c2x2);
+                lds_min(&reinterpret_cast<Cell<R>*>(base + gcur + off(u))->t, w);
+                if constexpr (TRACK) changed |= w < q_old[u] * keep;
+                cur = umin(w, q_old[u]);  // NaN (both-inf case) sorts above every value: keeps old
+            }
             fetch(u);  // refill the slot: step s + u + D (past the last step: clamped halo rows)
             // keep each step's instructions in place: hoisting a later step's use of a slot
             // above this point would make the compiler wait for the newest reads (lgkmcnt(0))

@@ -1,15 +1,21 @@
 # One GPU-box pass of the round's evidence: GPU tests, smoke, the bench line, kernel-trace stats
 # and the two PMC passes (FETCH_SIZE / WRITE_SIZE in separate runs), reduced to small summaries.
-#   ROUND=r01 bash tools/gpu_round.sh      (outputs under gpurun_out/)
+#   ROUND=r03 DTYPE=f64 bash tools/gpu_round.sh      (outputs under gpurun_out/)
+#   SKIP_TESTS=1 skips the GPU test suite and smoke.
 export TMPDIR=/tmp
-R=${ROUND:-r01}
+R=${ROUND:-r03}
+D=${DTYPE:-f64}
+K=$([ "$D" = f64 ] && echo "fim2d_persist_kernel<double" || echo "fim2d_persist_kernel<float")
 O=gpurun_out
+mkdir -p $O
+if [ -z "$SKIP_TESTS" ]; then
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/t_all.log 2>&1 || { echo "tests rc=$?"; tail -n 30 $O/t_all.log; exit 1; }
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke rc=$?"; exit 1; }
-timeout -k 10 600 python bench.py > $O/bench_$R.json 2> $O/bench_$R.err || { echo "bench rc=$?"; tail -n 20 $O/bench_$R.err; exit 1; }
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_$R -o prof -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extra > $O/prof_$R.out 2> $O/prof_$R.err || { echo "prof rc=$?"; exit 1; }
+fi
+timeout -k 10 600 python bench.py --dtype $D > $O/bench_$R.json 2> $O/bench_$R.err || { echo "bench rc=$?"; tail -n 20 $O/bench_$R.err; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_$R -o prof -- python bench.py --dtype $D --steps 10 --warmup 2 --no-cpu-baseline --no-extra > $O/prof_$R.out 2> $O/prof_$R.err || { echo "prof rc=$?"; exit 1; }
 find /tmp/prof_$R -name "*kernel_stats.csv" -exec cp {} $O/${R}_kernel_stats.csv \;
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d /tmp/pmc_fetch_$R -o f -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-path --no-timing --no-extra > $O/pmc_fetch.out 2> $O/pmc_fetch.err || { echo "pmc fetch rc=$?"; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d /tmp/pmc_write_$R -o w -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-path --no-timing --no-extra > $O/pmc_write.out 2> $O/pmc_write.err || { echo "pmc write rc=$?"; exit 1; }
-python tools/pmc_traffic.py /tmp/pmc_fetch_$R /tmp/pmc_write_$R > $O/pmc_traffic_$R.json 2> $O/pmc_traffic.err
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d /tmp/pmc_fetch_$R -o f -- python bench.py --dtype $D --steps 3 --warmup 1 --no-cpu-baseline --no-path --no-timing --no-extra > $O/pmc_fetch.out 2> $O/pmc_fetch.err || { echo "pmc fetch rc=$?"; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d /tmp/pmc_write_$R -o w -- python bench.py --dtype $D --steps 3 --warmup 1 --no-cpu-baseline --no-path --no-timing --no-extra > $O/pmc_write.out 2> $O/pmc_write.err || { echo "pmc write rc=$?"; exit 1; }
+python tools/pmc_traffic.py /tmp/pmc_fetch_$R /tmp/pmc_write_$R "$K" $D > $O/pmc_traffic_${R}_$D.json 2> $O/pmc_traffic.err
 echo ALLOK

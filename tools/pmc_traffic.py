@@ -2,7 +2,7 @@
 
   rocprofv3 --pmc FETCH_SIZE --kernel-trace -d <dir_f> -- python bench.py ...
   rocprofv3 --pmc WRITE_SIZE --kernel-trace -d <dir_w> -- python bench.py ...
-  python tools/pmc_traffic.py <dir_f> <dir_w> [kernel substring] > profiles/pmc_traffic.json
+  python tools/pmc_traffic.py <dir_f> <dir_w> [kernel substring] [dtype] > profiles/pmc_traffic_<dtype>.json
 
 FETCH_SIZE / WRITE_SIZE are kilobytes at the L2's memory side (TCC_EA0_RDREQ / _WRREQ;
 Infinity-Cache hits included).  gfx950 correction (MI355X_MICROARCH.md, HBM section):
@@ -37,12 +37,14 @@ def per_dispatch(d, counter, kernel):
 def main():
     dir_f, dir_w = sys.argv[1], sys.argv[2]
     kernel = sys.argv[3] if len(sys.argv) > 3 else "fim2d_persist_kernel"
+    dtype = sys.argv[4] if len(sys.argv) > 4 else ("f64" if "double" in kernel else "f32")
     f = per_dispatch(dir_f, "FETCH_SIZE", kernel)
     w = per_dispatch(dir_w, "WRITE_SIZE", kernel)
     fetch_kb = sum(f.values()) / len(f)
     write_kb = sum(w.values()) / len(w)
     out = {
         "kernel": kernel,
+        "dtype": dtype,
         "dispatches": {"fetch_pass": len(f), "write_pass": len(w)},
         "fetch_size_kb_raw": round(fetch_kb, 1),
         "write_size_kb_raw": round(write_kb, 1),
