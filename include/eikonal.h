@@ -136,12 +136,23 @@ int eik_gradient2d_f64(eik_ctx* ctx, const double* T, int64_t H, int64_t W, doub
 
 /* ---- host-buffer drop-ins of FastMarching3D.py ----------------------------------------- */
 
-/* FastMarching3D.computeTmap(costMap, goal, start) :126-145 -> full field T (the reference
- * stops once `start` is popped; every value it closes is identical here).  cost, T: H*W*L
- * row-major [y][x][z]; goal = (x, y, z). */
+/* FastMarching3D.computeTmap :126-145 without its early exit -> the full field T (what the
+ * reference returns when `start` is never popped).  cost, T: H*W*L row-major [y][x][z];
+ * goal = (x, y, z). */
 int eik_tmap3d_f32(eik_ctx* ctx, const float* cost, int64_t H, int64_t W, int64_t L, const int64_t goal[3], float* T);
 int eik_tmap3d_f64(eik_ctx* ctx, const double* cost, int64_t H, int64_t W, int64_t L, const int64_t goal[3],
                    double* T);
+
+/* FastMarching3D.computeTmap(costMap, goal, start) :126-145 as the planner calls it
+ * (Coupled_motion_planner.py:1636): the loop breaks once `start` is popped (:141), so T is the
+ * PARTIAL field -- cells popped before `start` (T < T[start]) and `start` at their final values,
+ * the narrow band at its local solve over the closed cells, +inf elsewhere (eik_fim3d_early_exit).
+ * start == goal, a start outside the volume or an unreachable start -> the full field, as in the
+ * reference (it never pops such a start). */
+int eik_tmap3d_early_f32(eik_ctx* ctx, const float* cost, int64_t H, int64_t W, int64_t L, const int64_t goal[3],
+                         const int64_t start[3], float* T);
+int eik_tmap3d_early_f64(eik_ctx* ctx, const double* cost, int64_t H, int64_t W, int64_t L, const int64_t goal[3],
+                         const int64_t start[3], double* T);
 
 /* FastMarching3D.getPathGDM(T, init, end, tau) :198-271 on an fp64 field: out cap x 3 rows. */
 int eik_path3d_f64(eik_ctx* ctx, const double* T, int64_t H, int64_t W, int64_t L, const double init[3],
@@ -227,6 +238,11 @@ int eik_path2d_dev(eik_ctx* ctx, const void* d_T, int dtype, int64_t H, int64_t 
  * eik_get_stats). */
 int eik_fim3d_solve(eik_ctx* ctx, const void* d_cost, void* d_T, int64_t H, int64_t W, int64_t L, int dtype,
                     const int64_t goal[3], void* stream);
+
+/* FastMarching3D.computeTmap's early exit at `start` (:141) on device buffers: d_T (a converged
+ * full field from eik_fim3d_solve) -> d_Te (a different buffer), async on `stream`. */
+int eik_fim3d_early_exit(eik_ctx* ctx, const void* d_cost, const void* d_T, void* d_Te, int64_t H, int64_t W,
+                         int64_t L, int dtype, const int64_t goal[3], const int64_t start[3], void* stream);
 
 /* FastMarching3D.getPathGDM on a device-resident field. */
 int eik_path3d_dev(eik_ctx* ctx, const void* d_T, int dtype, int64_t H, int64_t W, int64_t L, const double init[3],
@@ -323,7 +339,8 @@ int eik_arm_tunnel_cost_f64(eik_ctx* ctx, const double* gamma2D, const double* h
 /* :1562-1593 on the GPU: Cmap = finalMap * tunnel on the device -> FM3D.computeTmap(Cmap,
  * finalWayPointArm, initialWayPointArm) -> FM3D.getPathGDM(T, initialWayPointArm, finalWayPointArm,
  * tau) -> path (cap x 3 node coordinates, before the planner's scaling and smoothing, :1588-1598).
- * cost_out / T_out (nullable): the volume and the arrival field, sY*sX*sZ. */
+ * The field is computeTmap's early-exit field at initialWayPointArm (eik_tmap3d_early_f64).
+ * cost_out / T_out (nullable): the volume and that arrival field, sY*sX*sZ. */
 int eik_arm_path_f64(eik_ctx* ctx, const double* ZsMap, const double* newObstMap, int64_t m, int64_t n,
                      const double* gamma2D, const double* heading, int64_t npts, const eik_arm_volume* vol, double tau,
                      double* path, int64_t cap, int64_t* n_out, int* status, double* cost_out, double* T_out);

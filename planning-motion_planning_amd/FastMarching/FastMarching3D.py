@@ -1,13 +1,18 @@
 """Drop-in ``FastMarching.FastMarching3D`` (reference: src/FastMarching/FastMarching3D.py).
 
-  computeTmap(costMap, goal, start)   FastMarching3D.py:126-145 -> GPU 3D block-FIM (full field)
+  computeTmap(costMap, goal, start)   FastMarching3D.py:126-145 -> GPU 3D block-FIM + early exit
   getPathGDM(T, init, end, tau)       FastMarching3D.py:198-271 -> GPU path kernel
 Host-side scalar/list helpers keep their reference semantics: updateNode :19-101,
 sumlist :103-107, getMinNB :109-123, interpolatePoint :275-314.
 
-Layout as in the reference: cost[y, x, z], nodes (x, y, z).  computeTmap returns the full
-field; the reference stops when `start` is popped, and every value it has closed by then is the
-same here (so the 3D path, which only descends through closed nodes, is unchanged).
+Layout as in the reference: cost[y, x, z], nodes (x, y, z).  computeTmap returns the reference's
+PARTIAL field: its loop breaks once `start` is popped (:141), so cells popped before `start`
+(T < T[start]) and `start` hold their final values (same as the full field, <= 1e-9), the narrow
+band holds a tentative value (here: the local solve over the closed cells; the reference's value
+also depends on its sequential update order) and every other cell +inf.  getPathGDM's np.gradient
+(:200) sees those +inf cells, which is why the planner's end-effector path needs this field and
+not the full one (tests/golden/fm3d_early.npz: identical paths on cubes and arm volumes).
+start == goal, outside the volume or unreachable: the reference never pops it -> full field.
 """
 import bisect
 import os
@@ -105,10 +110,12 @@ def interpolatePoint(point, mapI):
 
 
 def computeTmap(costMap, goal, start=None):
-    """FastMarching3D.py:126-145 -> T[y, x, z] (float64, inf = unreached)."""
+    """FastMarching3D.py:126-145 -> T[y, x, z] (float64, inf = unreached), early exit at `start`
+    (:141); start=None (no reference counterpart) returns the full field."""
     cost = np.ascontiguousarray(costMap, dtype=_DTYPE)
     g = np.asarray(goal, dtype=np.int64).reshape(-1)[:3]
-    return _ctx().tmap3d(cost, g, dtype=_DTYPE).astype(np.float64, copy=False)
+    s = None if start is None else np.asarray(start, dtype=np.int64).reshape(-1)[:3]
+    return _ctx().tmap3d(cost, g, dtype=_DTYPE, start=s).astype(np.float64, copy=False)
 
 
 def getPathGDM(totalCostMap, initWaypoint, endWaypoint, tau):

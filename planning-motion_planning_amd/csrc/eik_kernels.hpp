@@ -101,6 +101,10 @@ struct Fim3dArgs {
 hipError_t fim3d_init(const Fim3dArgs& a, bool f64, const int64_t* d_goals, int B, hipStream_t st);
 hipError_t fim3d_sweep(const Fim3dArgs& a, bool f64, int grid, hipStream_t st);
 void fim3d_tile_shape(int64_t L, int* tx, int* ty, int* tz);
+// FastMarching3D.computeTmap's early exit at `start` (:141) from a converged field Tf into Te
+// (a separate buffer); ts_off = start's linear index, or -1 for no early exit (fim3d.hip).
+hipError_t fim3d_early(const void* cost, const void* Tf, void* Te, int64_t H, int64_t W, int64_t L, int64_t ts_off,
+                       bool f64, hipStream_t st);
 
 // Gradient-descent path extraction (getPathGDM, FastMarching.py:164-236), one wave.
 struct Gdm2dArgs {

@@ -1000,8 +1000,19 @@ int eik_fim3d_solve(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, int64_
 
 }  // extern "C"
 
+// Linear index of `start` for the early exit of FastMarching3D.computeTmap (:141), or -1 when the
+// reference never pops it: start == goal (the goal is closed without a pop, :132-134) or outside
+// the volume.  A start on +inf cost is never popped either; the kernel sees T[start] = +inf then.
+static int64_t early_offset(const int64_t goal[3], const int64_t start[3], int64_t H, int64_t W, int64_t L) {
+    if (!start) return -1;
+    if (start[0] < 0 || start[1] < 0 || start[2] < 0 || start[0] >= W || start[1] >= H || start[2] >= L) return -1;
+    if (start[0] == goal[0] && start[1] == goal[1] && start[2] == goal[2]) return -1;
+    return (start[1] * W + start[0]) * L + start[2];
+}
+
 template <typename R>
-static int tmap3d_host(eik_ctx* c, const R* cost, int64_t H, int64_t W, int64_t L, const int64_t goal[3], R* T) {
+static int tmap3d_host(eik_ctx* c, const R* cost, int64_t H, int64_t W, int64_t L, const int64_t goal[3],
+                       const int64_t* start, R* T) {
     if (!c || !cost || !T || !goal) return c ? set_err(c, EIK_ERR_ARG, "NULL argument") : EIK_ERR_ARG;
     const int64_t n = H * W * L;
     int rc = check_cost(c, cost, n);
@@ -1010,22 +1021,52 @@ static int tmap3d_host(eik_ctx* c, const R* cost, int64_t H, int64_t W, int64_t 
     HIPCHK(c, c->cost.ensure(sizeof(R) * n));
     HIPCHK(c, c->T.ensure(sizeof(R) * n));
     HIPCHK(c, hipMemcpyAsync(c->cost.p, cost, sizeof(R) * n, hipMemcpyHostToDevice, c->stream));
-    rc = eik_fim3d_solve(c, c->cost.p, c->T.p, H, W, L, sizeof(R) == 8 ? EIK_F64 : EIK_F32, goal, c->stream);
+    const int dt = sizeof(R) == 8 ? EIK_F64 : EIK_F32;
+    rc = eik_fim3d_solve(c, c->cost.p, c->T.p, H, W, L, dt, goal, c->stream);
     if (rc) return rc;
-    HIPCHK(c, hipMemcpyAsync(T, c->T.p, sizeof(R) * n, hipMemcpyDeviceToHost, c->stream));
+    const void* src = c->T.p;
+    if (start) {
+        HIPCHK(c, c->T2.ensure(sizeof(R) * n));
+        rc = eik_fim3d_early_exit(c, c->cost.p, c->T.p, c->T2.p, H, W, L, dt, goal, start, c->stream);
+        if (rc) return rc;
+        src = c->T2.p;
+    }
+    HIPCHK(c, hipMemcpyAsync(T, src, sizeof(R) * n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return EIK_OK;
 }
 
 extern "C" {
 
+int eik_fim3d_early_exit(eik_ctx* c, const void* d_cost, const void* d_T, void* d_Te, int64_t H, int64_t W, int64_t L,
+                         int dtype, const int64_t goal[3], const int64_t start[3], void* stream) {
+    if (!c || !d_cost || !d_T || !d_Te || !goal || !start || H < 1 || W < 1 || L < 1 || d_T == d_Te)
+        return c ? set_err(c, EIK_ERR_ARG, "bad early-exit arguments") : EIK_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, fim3d_early(d_cost, d_T, d_Te, H, W, L, early_offset(goal, start, H, W, L), dtype == EIK_F64,
+                          (hipStream_t)stream));
+    return EIK_OK;
+}
+
 int eik_tmap3d_f32(eik_ctx* c, const float* cost, int64_t H, int64_t W, int64_t L, const int64_t goal[3], float* T) {
-    return tmap3d_host<float>(c, cost, H, W, L, goal, T);
+    return tmap3d_host<float>(c, cost, H, W, L, goal, nullptr, T);
 }
 
 int eik_tmap3d_f64(eik_ctx* c, const double* cost, int64_t H, int64_t W, int64_t L, const int64_t goal[3],
                    double* T) {
-    return tmap3d_host<double>(c, cost, H, W, L, goal, T);
+    return tmap3d_host<double>(c, cost, H, W, L, goal, nullptr, T);
+}
+
+int eik_tmap3d_early_f32(eik_ctx* c, const float* cost, int64_t H, int64_t W, int64_t L, const int64_t goal[3],
+                         const int64_t start[3], float* T) {
+    if (!start) return c ? set_err(c, EIK_ERR_ARG, "NULL start") : EIK_ERR_ARG;
+    return tmap3d_host<float>(c, cost, H, W, L, goal, start, T);
+}
+
+int eik_tmap3d_early_f64(eik_ctx* c, const double* cost, int64_t H, int64_t W, int64_t L, const int64_t goal[3],
+                         const int64_t start[3], double* T) {
+    if (!start) return c ? set_err(c, EIK_ERR_ARG, "NULL start") : EIK_ERR_ARG;
+    return tmap3d_host<double>(c, cost, H, W, L, goal, start, T);
 }
 
 int eik_path3d_dev(eik_ctx* c, const void* d_T, int dtype, int64_t H, int64_t W, int64_t L, const double init[3],
@@ -1538,14 +1579,15 @@ int eik_arm_path_f64(eik_ctx* c, const double* Z, const double* obst, int64_t m,
     const int64_t nc = v->sX * v->sY * v->sZ, nz = m * n;
     const int64_t steps = (int64_t)std::nearbyint(15000.0 / tau);
     const int64_t pcap = std::min<int64_t>(cap, steps + 4);
-    // Z | obst | fmap | tunnel | cost | T | path | n_out | status
-    HIPCHK(c, c->T2.ensure(sizeof(double) * (2 * nz + 4 * nc + 3 * pcap) + 64));
+    // Z | obst | fmap | tunnel | cost | T (full) | T (early exit) | path | n_out | status
+    HIPCHK(c, c->T2.ensure(sizeof(double) * (2 * nz + 5 * nc + 3 * pcap) + 64));
     double* dZ = (double*)c->T2.p;
     double* dO = dZ + nz;
     double* dF = dO + nz;
     double* dTun = dF + nc;
     double* dC = dTun + nc;
-    double* dT = dC + nc;
+    double* dTf = dC + nc;
+    double* dT = dTf + nc;
     double* dP = dT + nc;
     int64_t* dn = (int64_t*)(dP + 3 * pcap);
     int* dst = (int*)(dn + 1);
@@ -1554,8 +1596,12 @@ int eik_arm_path_f64(eik_ctx* c, const double* Z, const double* obst, int64_t m,
     rc = arm_volume_dev(c, dZ, dO, m, n, gamma2D, heading, npts, v, dF, nullptr, nullptr, dTun, dC, st);
     if (rc) return rc;
     // FM3D.computeTmap(Cmap, finalWayPointArm, initialWayPointArm) :1585; H = sY rows, W = sX columns
+    // with its early exit once initialWayPointArm is popped (FastMarching3D.py:141)
     const int64_t goal[3] = {v->final_wp[0], v->final_wp[1], v->final_wp[2]};
-    rc = eik_fim3d_solve(c, dC, dT, v->sY, v->sX, v->sZ, EIK_F64, goal, st);
+    const int64_t start[3] = {v->initial_wp[0], v->initial_wp[1], v->initial_wp[2]};
+    rc = eik_fim3d_solve(c, dC, dTf, v->sY, v->sX, v->sZ, EIK_F64, goal, st);
+    if (rc) return rc;
+    rc = eik_fim3d_early_exit(c, dC, dTf, dT, v->sY, v->sX, v->sZ, EIK_F64, goal, start, st);
     if (rc) return rc;
     // FM3D.getPathGDM(Tmap3D, initialWayPointArm, finalWayPointArm, 0.5) :1588
     const double init[3] = {(double)v->initial_wp[0], (double)v->initial_wp[1], (double)v->initial_wp[2]};

@@ -39,6 +39,57 @@ __device__ __forceinline__ R godunov3(R a, R b, R c, R C) {
     return a + C;
 }
 
+// FastMarching3D.py:59-75 in the reference's own arithmetic, for the fp64 solver: Tarray =
+// [Tx, Ty, Tz]; Tmax = the FIRST largest entry (Python max); sumT = left fold of (Tmax - Ta)^2 from
+// 0; accept when C^2 > sumT with Tr = (S + sqrt(n C^2 + S^2 - n Q)) / n, S and Q right-associated
+// sums (sumlist, :103-107) in list order; else remove that Tmax (list.remove: first occurrence)
+// and retry.  No contraction, correctly rounded sqrt and division: the same bits as the reference
+// on the same neighbours, so exact ties stay exact ties (FastMarching3D.computeTmap's early exit
+// compares against T[start], fim3d_early_kernel).  All +inf -> +inf (the reference never solves
+// a cell without a popped neighbour).
+__device__ __forceinline__ double solve3_ref(double tx, double ty, double tz, double C) {
+#pragma clang fp contract(off)
+    double v0 = tx, v1 = ty, v2 = tz;
+    const double C2 = C * C;
+    int n = 3;
+    for (int it = 0; it < 3; ++it) {
+        double tmax = v0;
+        int im = 0;
+        if (n > 1 && v1 > tmax) { tmax = v1; im = 1; }
+        if (n > 2 && v2 > tmax) { tmax = v2; im = 2; }
+        double d = tmax - v0;
+        double sumT = d * d;
+        if (n > 1) { d = tmax - v1; sumT = sumT + d * d; }
+        if (n > 2) { d = tmax - v2; sumT = sumT + d * d; }
+        if (C2 > sumT) {
+            double S, Q;
+            if (n == 3) {
+                S = v0 + (v1 + v2);
+                Q = v0 * v0 + (v1 * v1 + v2 * v2);
+            } else if (n == 2) {
+                S = v0 + v1;
+                Q = v0 * v0 + v1 * v1;
+            } else {
+                S = v0;
+                Q = v0 * v0;
+            }
+            const double nn = (double)n;
+            return (S + __builtin_sqrt((nn * C2 + S * S) - nn * Q)) / nn;
+        }
+        if (im == 0) { v0 = v1; v1 = v2; }
+        else if (im == 1) { v1 = v2; }
+        --n;
+    }
+    return Real<double>::inf();
+}
+
+// the solver's local update: the reference's arithmetic in fp64, the cancellation-free form in fp32
+template <typename R>
+__device__ __forceinline__ R local3(R a, R b, R c, R C) {
+    if constexpr (sizeof(R) == 8) return solve3_ref(a, b, c, C);
+    else return godunov3<R>(a, b, c, C);
+}
+
 __device__ __forceinline__ void enqueue3(const Fim3dArgs& a, int tile, int list, unsigned stamp) {
     if (atomicMax(&a.mark[tile], stamp) < stamp) {
         const int pos = atomicAdd(&a.counts[list], 1);
@@ -121,7 +172,7 @@ __global__ __launch_bounds__(256) void fim3d_sweep_kernel(Fim3dArgs a) {
                 const R tx_ = fmin(Ts[h - sx], Ts[h + sx]);
                 const R ty_ = fmin(Ts[h - sy], Ts[h + sy]);
                 const R tz_ = fmin(Ts[h - 1], Ts[h + 1]);
-                const R nv = cst[k] == INF ? INF : godunov3<R>(tx_, ty_, tz_, cst[k]);
+                const R nv = cst[k] == INF ? INF : local3<R>(tx_, ty_, tz_, cst[k]);
                 if (nv < v) {
                     Ts[h] = nv;  // owner-only write; concurrent readers see old or new (both bounds)
                     ch = true;
@@ -215,6 +266,63 @@ hipError_t fim3d_sweep(const Fim3dArgs& a, bool f64, int grid, hipStream_t st) {
         hipLaunchKernelGGL(fim3d_sweep_kernel<double>, dim3(grid), dim3(256), 0, st, a);
     else
         hipLaunchKernelGGL(fim3d_sweep_kernel<float>, dim3(grid), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+// FastMarching3D.computeTmap's early exit (:137-142: the loop breaks right after popping
+// `start`) restated on a converged full field Tf.  The reference pops in nondecreasing T, so the
+// closed set is {T < T[start]} plus `start` itself; closed cells keep their final values.  Ties:
+// the reference pops equal T in LIFO insertion order, which a field does not record; cells exactly
+// tied with `start` are taken as not yet popped (the fp64 solver computes in the reference's
+// arithmetic, solve3_ref, so ties of the reference are ties here).  Every other finite-cost cell with a closed
+// 6-neighbour is in the narrow band: it holds the local solve (:44-75) over its CLOSED neighbours
+// (cells of the band and beyond read +inf).  The reference's band value also mixes in the tentative
+// values other band cells held when each update ran -- an order-dependent quantity of the
+// sequential pop sequence with no parallel form; the path the planner descends from `start`
+// (:1639) is the same on every reference fixture (tests/golden/fm3d_early.npz).  The rest is +inf.
+// ts_off: -1 = no early exit (start == goal, outside the volume: the reference never pops it).
+template <typename R>
+__global__ __launch_bounds__(256) void fim3d_early_kernel(const R* __restrict__ cost, const R* __restrict__ Tf,
+                                                          R* __restrict__ Te, int64_t H, int64_t W, int64_t L,
+                                                          int64_t ts_off) {
+    constexpr R INF = Real<R>::inf();
+    const R ts = ts_off >= 0 ? Tf[ts_off] : INF;  // +inf: no early exit
+    const int64_t n = H * W * L;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const R v = Tf[i];
+        if (v < ts || i == ts_off) {
+            Te[i] = v;
+            continue;
+        }
+        const R C = cost[i];
+        if (!(C < INF)) {
+            Te[i] = INF;
+            continue;
+        }
+        const int64_t z = i % L, xy = i / L, x = xy % W, y = xy / W;
+        auto nb = [&](bool in, int64_t j) -> R {
+            if (!in) return INF;
+            const R t = Tf[j];
+            return (t < ts || j == ts_off) ? t : INF;
+        };
+        const R tx = fmin(nb(x > 0, i - L), nb(x + 1 < W, i + L));
+        const R ty = fmin(nb(y > 0, i - W * L), nb(y + 1 < H, i + W * L));
+        const R tz = fmin(nb(z > 0, i - 1), nb(z + 1 < L, i + 1));
+        Te[i] = local3<R>(tx, ty, tz, C);  // all +inf (no closed neighbour) -> +inf
+    }
+}
+
+hipError_t fim3d_early(const void* cost, const void* Tf, void* Te, int64_t H, int64_t W, int64_t L, int64_t ts_off,
+                       bool f64, hipStream_t st) {
+    const int64_t n = H * W * L;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(8192, (n + 255) / 256));
+    if (f64)
+        hipLaunchKernelGGL(fim3d_early_kernel<double>, dim3(grid), dim3(256), 0, st, static_cast<const double*>(cost),
+                           static_cast<const double*>(Tf), static_cast<double*>(Te), H, W, L, ts_off);
+    else
+        hipLaunchKernelGGL(fim3d_early_kernel<float>, dim3(grid), dim3(256), 0, st, static_cast<const float*>(cost),
+                           static_cast<const float*>(Tf), static_cast<float*>(Te), H, W, L, ts_off);
     return hipGetLastError();
 }
 

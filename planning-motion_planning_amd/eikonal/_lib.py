@@ -121,6 +121,9 @@ def lib():
         L.eik_path2d_dev.argtypes = [vp, vp, C.c_int, i64, i64, _f64p, _f64p, C.c_double, vp, i64, vp, vp, vp]
         L.eik_tmap3d_f32.argtypes = [vp, _f32p, i64, i64, i64, _i64p, _f32p]
         L.eik_tmap3d_f64.argtypes = [vp, _f64p, i64, i64, i64, _i64p, _f64p]
+        L.eik_tmap3d_early_f32.argtypes = [vp, _f32p, i64, i64, i64, _i64p, _i64p, _f32p]
+        L.eik_tmap3d_early_f64.argtypes = [vp, _f64p, i64, i64, i64, _i64p, _i64p, _f64p]
+        L.eik_fim3d_early_exit.argtypes = [vp, vp, vp, vp, i64, i64, i64, C.c_int, _i64p, _i64p, vp]
         L.eik_path3d_f64.argtypes = [vp, _f64p, i64, i64, i64, _f64p, _f64p, C.c_double, _f64p, i64, P(i64),
                                      P(C.c_int)]
         L.eik_fim3d_solve.argtypes = [vp, vp, vp, i64, i64, i64, C.c_int, _i64p, vp]
@@ -162,7 +165,8 @@ EXPORTED = [
     "eik_tmap2d_f32", "eik_tmap2d_f64", "eik_tmap2d_bidir_f64", "eik_tmap2d_batch_f32", "eik_path2d_f64",
     "eik_gradient2d_f64", "eik_fim2d_create", "eik_fim2d_destroy", "eik_fim2d_set_ghosts", "eik_fim2d_start",
     "eik_fim2d_iterate", "eik_fim2d_solve", "eik_fim2d_pack_edges", "eik_fim2d_merge_ghost", "eik_fim2d_active",
-    "eik_fim2d_stats", "eik_path2d_dev", "eik_selftest_walker_math", "eik_tmap3d_f32", "eik_tmap3d_f64", "eik_path3d_f64", "eik_fim3d_solve",
+    "eik_fim2d_stats", "eik_path2d_dev", "eik_selftest_walker_math", "eik_tmap3d_f32", "eik_tmap3d_f64",
+    "eik_tmap3d_early_f32", "eik_tmap3d_early_f64", "eik_fim3d_early_exit", "eik_path3d_f64", "eik_fim3d_solve",
     "eik_path3d_dev", "eik_costmap_f64", "eik_costmap_dev", "eik_surface_normal_f64", "eik_image_fill_u8",
     "eik_load_dem_txt", "eik_io_last_error", "eik_fim2d_live_bind", "eik_fim2d_launch", "eik_fim2d_live_pack",
     "eik_fim2d_live_merge", "eik_fim2d_release", "eik_node_allreduce", "eik_node_shm_open",
@@ -278,12 +282,21 @@ class Context:
                                        C.byref(st)))
         return out[: n.value].copy(), st.value
 
-    def tmap3d(self, cost, goal, dtype=np.float64):
+    def tmap3d(self, cost, goal, dtype=np.float64, start=None):
+        """FastMarching3D.computeTmap: the full field, or with `start` (x, y, z) the reference's
+        early-exit field (break once `start` is popped, FastMarching3D.py:141)."""
         cost = np.ascontiguousarray(cost, dtype=dtype)
         H, W, Lz = cost.shape
         T = np.empty_like(cost)
-        fn = lib().eik_tmap3d_f64 if cost.dtype == np.float64 else lib().eik_tmap3d_f32
-        self._chk(fn(self._h, cost, H, W, Lz, np.ascontiguousarray(np.asarray(goal)[:3], np.int64), T))
+        g = np.ascontiguousarray(np.asarray(goal).reshape(-1)[:3], np.int64)
+        f64 = cost.dtype == np.float64
+        if start is None:
+            fn = lib().eik_tmap3d_f64 if f64 else lib().eik_tmap3d_f32
+            self._chk(fn(self._h, cost, H, W, Lz, g, T))
+        else:
+            s = np.ascontiguousarray(np.asarray(start).reshape(-1)[:3], np.int64)
+            fn = lib().eik_tmap3d_early_f64 if f64 else lib().eik_tmap3d_early_f32
+            self._chk(fn(self._h, cost, H, W, Lz, g, s, T))
         return T
 
     def path3d(self, T, init, end, tau=0.5):

@@ -84,8 +84,10 @@ def test_gpu_dropin_3d(golden):
     p = "v0_"
     cost = v[p + "cost"].astype(np.float64)
     T = FM3D.computeTmap(cost, np.uint32(v[p + "goal"]), np.uint32(v[p + "start"]))
-    R = v[p + "T"]
-    fin = np.isfinite(R)
-    assert np.array_equal(np.isfinite(T), fin) and np.abs(T[fin] - R[fin]).max() <= 1e-9
-    path = FM3D.getPathGDM(v[p + "T_early"], np.uint32(v[p + "start"]), np.uint32(v[p + "goal"]), 0.5)
-    assert np.abs(path - v[p + "path"]).max() <= 1e-9
+    R = v[p + "T_early"]  # the reference breaks once start is popped (FastMarching3D.py:141)
+    assert T.dtype == np.float64 and np.array_equal(np.isfinite(T), np.isfinite(R))
+    path = FM3D.getPathGDM(T, np.uint32(v[p + "start"]), np.uint32(v[p + "goal"]), 0.5)
+    assert path.shape == v[p + "path"].shape and np.abs(path - v[p + "path"]).max() <= 1e-9
+    Tf = FM3D.computeTmap(cost, np.uint32(v[p + "goal"]), None)  # start=None: the full field
+    fin = np.isfinite(v[p + "T"])
+    assert np.array_equal(np.isfinite(Tf), fin) and np.abs(Tf[fin] - v[p + "T"][fin]).max() <= 1e-9

@@ -52,14 +52,12 @@ def test_path3d(ctx, golden, i):
     path, st = ctx.path3d(d[p + "T_early"], s, g)
     ref = d[p + "path"]
     assert st == 0 and path.shape == ref.shape and np.abs(path - ref).max() <= 1e-9
-    # end to end on the layered (z-padded) volumes: np.gradient is NaN next to the inf layers, so
-    # every step is the integer descent through closed nodes and the full GPU field gives the
-    # reference path exactly.  (On cubes the reference descends its PARTIAL early-exit field,
-    # whose unclosed cells feed the trilinear gradient -- not reproducible from a full field.)
-    if str(d[p + "path_err"]) == "" and i < 2:
-        T = ctx.tmap3d(d[p + "cost"].astype(np.float64), d[p + "goal"], dtype=np.float64)
-        path2, _ = ctx.path3d(T, s, g)
-        assert path2.shape == ref.shape and np.abs(path2 - ref).max() <= 1e-9
+    # end to end, layered and cube volumes alike: the GPU's early-exit field (computeTmap breaks
+    # once `start` is popped, FastMarching3D.py:141) descended by the GPU path kernel
+    assert str(d[p + "path_err"]) == ""
+    T = ctx.tmap3d(d[p + "cost"].astype(np.float64), d[p + "goal"], dtype=np.float64, start=d[p + "start"])
+    path2, _ = ctx.path3d(T, s, g)
+    assert path2.shape == ref.shape and np.abs(path2 - ref).max() <= 1e-9
 
 
 @pytest.mark.parametrize("shape,seed", [((200, 230, 5), 1), ((40, 44, 36), 2), ((64, 64, 3), 3), ((33, 70, 9), 4)])
