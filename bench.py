@@ -109,7 +109,7 @@ def main():
     cost = terrain.cost_block(blk.y0, blk.x0, blk.h, blk.w, H, W, seed=seed, device=dev).to(tdt).contiguous()
     T = torch.empty_like(cost)
     stream = torch.cuda.current_stream(dev)
-    ctx = eikonal.Context(local_rank)
+    ctx = eikonal.Context(local_rank, options=eikonal._lib.options_from_env())  # A/B hook, opt-in
     ctx.set_option(L.OPT_SYNC_EVERY, args.sync_every)
     if shared and world > 1:
         ctx.set_option(L.OPT_GRID, max(2, 2 * torch.cuda.get_device_properties(dev).multi_processor_count // world))

@@ -117,8 +117,11 @@ int eik_tmap2d_f32(eik_ctx* ctx, const float* cost, int64_t H, int64_t W, int64_
 int eik_tmap2d_f64(eik_ctx* ctx, const double* cost, int64_t H, int64_t W, int64_t gx, int64_t gy, double* T);
 
 /* biComputeTmap(costMap, goal, start) FastMarching.py:114-162 -> (TmapG, TmapS, nodeJoin).
- * Both fields are FULL fields (fp64); nodeJoin is the first node popped by one front that the
- * other front had already closed, evaluated on the device from the two fields' pop ranks. */
+ * nodeJoin is the first node popped by one front that the other front had already closed,
+ * evaluated on the device from the two fields' pop ranks (the meeting iteration k).  TmapG/TmapS
+ * are the fronts' PARTIAL fields at that iteration, as the reference returns them: the source and
+ * its k first pops (rank <= k) and the narrow band around them at their values, +inf elsewhere
+ * (fp64; exact ties of T are ranked by node index, the reference pops them LIFO). */
 int eik_tmap2d_bidir_f64(eik_ctx* ctx, const double* cost, int64_t H, int64_t W, int64_t gx, int64_t gy,
                          int64_t sx, int64_t sy, double* TG, double* TS, uint32_t join[2]);
 

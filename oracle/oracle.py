@@ -174,28 +174,11 @@ def fmm3d_trace(cost, goal, start=None):
     return T, pop
 
 
-def solve3_np(tx, ty, tz, C):
-    """FastMarching3D.py:59-75 (drop the largest neighbour while C^2 <= sum (Tmax - Ti)^2),
-    vectorised over arrays; all-inf neighbours give +inf."""
-    A = np.sort(np.stack([tx, ty, tz]), axis=0)
-    out = np.full(np.shape(C), np.inf)
-    with np.errstate(invalid="ignore", over="ignore"):
-        for n in (3, 2, 1):
-            a = A[:n]
-            tmax = a[-1]
-            ok = np.isfinite(tmax) & (C * C > ((tmax - a) ** 2).sum(0)) & ~np.isfinite(out)
-            S, Q = a.sum(0), (a * a).sum(0)
-            tr = (S + np.sqrt(n * C * C + S * S - n * Q)) / n
-            out = np.where(ok, tr, out)
-    return out
-
-
 def fm3d_early_from_full(cost, Tf, goal, start):
     """The GPU's restatement of FastMarching3D.computeTmap's early exit (:141) on a converged full
-    field Tf (eikonal_api.cpp eik_fim3d_early_exit): closed = {Tf < Tf[start]} + start at Tf
-    (exact ties with start count as not yet popped); the
-    narrow band (finite cost, a closed 6-neighbour) at the local solve (:44-75) over its closed
-    neighbours; +inf elsewhere.  start == goal / outside the volume -> Tf itself."""
+    field Tf (eikonal_api.cpp eik_fim3d_early_exit): closed = {Tf < Tf[start]} + start (exact ties
+    with start count as not yet popped) and the narrow band (finite cost, a closed 6-neighbour)
+    keep Tf; +inf elsewhere.  start == goal / outside the volume -> Tf itself."""
     cost = _f64(cost)
     Tf = _f64(Tf)
     H, W, L = Tf.shape
@@ -205,13 +188,11 @@ def fm3d_early_from_full(cost, Tf, goal, start):
     ts = Tf[sy, sx, sz]
     closed = Tf < ts
     closed[sy, sx, sz] = True
-    Cl = np.pad(np.where(closed, Tf, np.inf), 1, constant_values=np.inf)
-    tx = np.minimum(Cl[1:-1, :-2, 1:-1], Cl[1:-1, 2:, 1:-1])
-    ty = np.minimum(Cl[:-2, 1:-1, 1:-1], Cl[2:, 1:-1, 1:-1])
-    tz = np.minimum(Cl[1:-1, 1:-1, :-2], Cl[1:-1, 1:-1, 2:])
-    band = solve3_np(tx, ty, tz, np.where(np.isfinite(cost), cost, np.inf))
-    band[~np.isfinite(cost)] = np.inf
-    return np.where(closed, Tf, band)
+    P = np.pad(closed, 1, constant_values=False)
+    nb = (P[1:-1, :-2, 1:-1] | P[1:-1, 2:, 1:-1] | P[:-2, 1:-1, 1:-1] | P[2:, 1:-1, 1:-1] |
+          P[1:-1, 1:-1, :-2] | P[1:-1, 1:-1, 2:])
+    keep = closed | (nb & np.isfinite(cost))
+    return np.where(keep, Tf, np.inf)
 
 
 def gdm3d(T, init, end, tau=0.5, max_out=None):

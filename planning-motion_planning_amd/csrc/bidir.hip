@@ -87,6 +87,39 @@ hipError_t bidir_join(const double* d_TG, const double* d_TS, int64_t n, void* d
     return hipGetLastError();
 }
 
+// biComputeTmap returns the PARTIAL fields of the two fronts at the meeting iteration k
+// (FastMarching.py:141-162): front f has popped its source and the next k nodes, i.e. the cells of
+// rank <= k in its field (rank 0 = the source).  Those keep their final values; a cell of the
+// narrow band (finite, not popped, a popped 4-neighbour) keeps its value too -- the reference's
+// tentative band value is >= the final value, equal when its last update saw final neighbours,
+// and the paths descended from nodeJoin (:1225-1226) then match the reference's
+// (tests/test_gpu_path.py); every other cell is +inf, as the reference leaves it.  In place: a
+// cell's own value changes only to +inf, its neighbours' closedness comes from the ranks.
+__global__ void bidir_partial_kernel(double* __restrict__ T, const unsigned* __restrict__ rank, int64_t H, int64_t W,
+                                     const unsigned long long* __restrict__ best) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned long long b = *best;
+    if (i >= H * W || b == ~0ull) return;  // fronts never met: the reference raises, fields unused
+    const unsigned k = (unsigned)(b >> 30);
+    if (rank[i] <= k) return;
+    const int64_t y = i / W, x = i - y * W;
+    const bool band = (x > 0 && rank[i - 1] <= k) || (x + 1 < W && rank[i + 1] <= k) ||
+                      (y > 0 && rank[i - W] <= k) || (y + 1 < H && rank[i + W] <= k);
+    if (!band) T[i] = Real<double>::inf();
+}
+
+hipError_t bidir_partial(double* d_TG, double* d_TS, int64_t H, int64_t W, const void* d_work,
+                         const unsigned long long* d_best, hipStream_t st) {
+    const int64_t n = H * W;
+    const char* p = static_cast<const char*>(d_work);
+    const unsigned* rg = reinterpret_cast<const unsigned*>(p + (size_t)n * (2 * 8 + 2 * 4));
+    const unsigned* rs = rg + n;
+    const unsigned grid = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(bidir_partial_kernel, dim3(grid), dim3(256), 0, st, d_TG, rg, H, W, d_best);
+    hipLaunchKernelGGL(bidir_partial_kernel, dim3(grid), dim3(256), 0, st, d_TS, rs, H, W, d_best);
+    return hipGetLastError();
+}
+
 size_t bidir_join_work_bytes(int64_t n) {
     size_t cub_bytes = 0;
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (unsigned long long*)nullptr, (unsigned long long*)nullptr,

@@ -22,6 +22,9 @@ namespace eik {
 hipError_t bidir_join(const double* d_TG, const double* d_TS, int64_t n, void* d_work, size_t work_bytes,
                       unsigned long long* d_best, hipStream_t st);
 size_t bidir_join_work_bytes(int64_t n);
+// after bidir_join on the same work buffer: the two fields -> biComputeTmap's partial fields
+hipError_t bidir_partial(double* d_TG, double* d_TS, int64_t H, int64_t W, const void* d_work,
+                         const unsigned long long* d_best, hipStream_t st);
 }  // namespace eik
 
 using namespace eik;
@@ -744,11 +747,14 @@ int eik_tmap2d_bidir_f64(eik_ctx* c, const double* cost, int64_t H, int64_t W, i
     HIPCHK(c, c->misc.ensure(64));
     HIPCHK(c, bidir_join((const double*)c->T.p, (const double*)c->T.p + n, n, c->work.p, c->work.bytes,
                          (unsigned long long*)c->misc.p, c->stream));
+    // the fronts' partial fields at the meeting iteration (FastMarching.py:141-162)
+    HIPCHK(c, bidir_partial((double*)c->T.p, (double*)c->T.p + n, H, W, c->work.p,
+                            (const unsigned long long*)c->misc.p, c->stream));
     unsigned long long best = 0;
     HIPCHK(c, hipMemcpyAsync(&best, c->misc.p, sizeof best, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(TG, c->T.p, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(TS, (double*)c->T.p + n, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    std::memcpy(TG, T2.data(), sizeof(double) * n);
-    std::memcpy(TS, T2.data() + n, sizeof(double) * n);
     if (best == ~0ull) return set_err(c, EIK_ERR_UNREACHABLE, "goal and start are not connected");
     const int64_t node = (int64_t)(best & ((1ull << 29) - 1));
     join[0] = (uint32_t)(node % W);
@@ -1299,6 +1305,7 @@ int eik_rover_path_f64(eik_ctx* c, const double* Z, int64_t H, int64_t W, const 
     HIPCHK(c, c->work.ensure(wb));
     HIPCHK(c, c->misc.ensure(64));
     HIPCHK(c, bidir_join(dT, dT + n, n, c->work.p, c->work.bytes, (unsigned long long*)c->misc.p, st));
+    HIPCHK(c, bidir_partial(dT, dT + n, H, W, c->work.p, (const unsigned long long*)c->misc.p, st));  // :141-162
     unsigned long long best = 0;
     HIPCHK(c, hipMemcpyAsync(&best, c->misc.p, sizeof best, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));

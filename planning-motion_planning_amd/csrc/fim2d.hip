@@ -259,6 +259,13 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
             }
         }
         store_tile(cr, load_halo());
+        // a cut tile's halo sits inside the tile: the ring's own row 65 / column 65, where DY < 0
+        // sweeps start and lane 0 of DX < 0 sweeps reads its upstream x, would keep a previous
+        // visit's values -- make them +inf (the moved halo row / column is <= 64, no overlap)
+        if (tid < kLds) {
+            if (sy - y0 < kTile) Ts[(kLds - 1) * kLds + tid] = Cell<R>{INF, INF};
+            if (sx - x0 < kTile) Ts[tid * kLds + (kLds - 1)] = Cell<R>{INF, INF};
+        }
     }
     if (lane < 4) Ts[(lane >> 1) * (kLds - 1) * kLds + (lane & 1) * (kLds - 1)].c = INF;  // corners
     __syncthreads();

@@ -31,13 +31,18 @@ constexpr int kMaxLayers = 4;  // float4 per cell in LDS
 struct TileLdsL {
     float4 Tbuf[(kLds + 2 * kGuard) * kLds];  // tile + halo ring (66 x 66 at offset kGuard * kLds), guard rows
                                               // above and below (fim2d.hip's sweep_quadrant)
-    float4 Cs[kLds * kLds];          // same layout as the ring; halo = +inf
+    float4 Cbuf[(kLds + 2 * kGuard) * kLds];  // costs in the same layout; halo ring and guard rows = +inf
     unsigned flags;
     unsigned key[5];
     int tile;
     unsigned dirs;
 };
-static_assert(offsetof(TileLdsL, Cs) == sizeof(float4) * (kLds + 2 * kGuard) * kLds, "Cs must follow Tbuf");
+// A sweep's 4-step group spans rows [-(kAhead - 1), kLds - 1 + kAhead - 1]: every row it reads (T
+// and cost alike) is inside the guard rows of both arrays, and a guard row's +inf cost keeps its T
+// at +inf (the Godunov update of an infinite cost never lowers a cell).
+static_assert(kGuard >= kAhead - 1, "guard rows must cover a group's overshoot");
+static_assert(offsetof(TileLdsL, Cbuf) == sizeof(float4) * (kLds + 2 * kGuard) * kLds, "Cbuf must follow Tbuf");
+static_assert(sizeof(TileLdsL) <= 160 * 1024, "one layered tile per CU (160 KB LDS)");
 
 __device__ __forceinline__ float f4get(const float4& v, int z) { return z == 0 ? v.x : z == 1 ? v.y : z == 2 ? v.z : v.w; }
 
@@ -68,7 +73,7 @@ __device__ __forceinline__ void sweep_layered(float4* __restrict__ Ts, int lane)
     constexpr float INF = __builtin_inff();
     constexpr int S = (int)sizeof(float4);
     constexpr int kRow = kLds * S;
-    constexpr int kCsB = (kLds + kGuard) * kLds * S;  // Cs - Ts in bytes
+    constexpr int kCsB = (kLds + 2 * kGuard) * kLds * S;  // Cs - Ts in bytes (Cbuf - Tbuf)
     constexpr int D = kAhead;
     char* const base = reinterpret_cast<char*>(Ts);
     auto ld = [&](int off) { return *reinterpret_cast<const float4*>(base + off); };
@@ -130,7 +135,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
     constexpr float INF = __builtin_inff();
     const float4 INF4 = make_float4(INF, INF, INF, INF);
     float4* const Ts = L.Tbuf + kGuard * kLds;
-    float4* const Cs = L.Cs;
+    float4* const Cs = L.Cbuf + kGuard * kLds;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int map = tile / a.tiles_per_map;
     const int rem = tile - map * a.tiles_per_map;
@@ -273,6 +278,8 @@ __global__ __launch_bounds__(kThreads) void fim2dl_persist_kernel(Fim2dArgs a) {
     for (int i = threadIdx.x; i < kGuard * kLds; i += kThreads) {  // guard rows: read by sweeps, never lowered
         L.Tbuf[i] = make_float4(INF, INF, INF, INF);
         L.Tbuf[(kLds + kGuard) * kLds + i] = make_float4(INF, INF, INF, INF);
+        L.Cbuf[i] = make_float4(INF, INF, INF, INF);
+        L.Cbuf[(kLds + kGuard) * kLds + i] = make_float4(INF, INF, INF, INF);
     }
     const float keep = a.keep;
     int tile = -1;

@@ -274,12 +274,12 @@ hipError_t fim3d_sweep(const Fim3dArgs& a, bool f64, int grid, hipStream_t st) {
 // closed set is {T < T[start]} plus `start` itself; closed cells keep their final values.  Ties:
 // the reference pops equal T in LIFO insertion order, which a field does not record; cells exactly
 // tied with `start` are taken as not yet popped (the fp64 solver computes in the reference's
-// arithmetic, solve3_ref, so ties of the reference are ties here).  Every other finite-cost cell with a closed
-// 6-neighbour is in the narrow band: it holds the local solve (:44-75) over its CLOSED neighbours
-// (cells of the band and beyond read +inf).  The reference's band value also mixes in the tentative
-// values other band cells held when each update ran -- an order-dependent quantity of the
-// sequential pop sequence with no parallel form; the path the planner descends from `start`
-// (:1639) is the same on every reference fixture (tests/golden/fm3d_early.npz).  The rest is +inf.
+// arithmetic, solve3_ref, so ties of the reference are ties here).  Every other finite-cost cell
+// with a closed 6-neighbour is in the narrow band and keeps its value too: the reference's
+// tentative band value (:77-95) is >= the final value, equal when its last update saw final
+// neighbours, and depends on the sequential update order beyond that; the path the planner
+// descends from `start` (:1639) is the reference's on every fixture (tests/golden/fm3d_early.npz).
+// The rest is +inf, as the reference leaves it (np.gradient at :200 sees those cells).
 // ts_off: -1 = no early exit (start == goal, outside the volume: the reference never pops it).
 template <typename R>
 __global__ __launch_bounds__(256) void fim3d_early_kernel(const R* __restrict__ cost, const R* __restrict__ Tf,
@@ -295,21 +295,15 @@ __global__ __launch_bounds__(256) void fim3d_early_kernel(const R* __restrict__ 
             Te[i] = v;
             continue;
         }
-        const R C = cost[i];
-        if (!(C < INF)) {
+        if (!(cost[i] < INF)) {
             Te[i] = INF;
             continue;
         }
         const int64_t z = i % L, xy = i / L, x = xy % W, y = xy / W;
-        auto nb = [&](bool in, int64_t j) -> R {
-            if (!in) return INF;
-            const R t = Tf[j];
-            return (t < ts || j == ts_off) ? t : INF;
-        };
-        const R tx = fmin(nb(x > 0, i - L), nb(x + 1 < W, i + L));
-        const R ty = fmin(nb(y > 0, i - W * L), nb(y + 1 < H, i + W * L));
-        const R tz = fmin(nb(z > 0, i - 1), nb(z + 1 < L, i + 1));
-        Te[i] = local3<R>(tx, ty, tz, C);  // all +inf (no closed neighbour) -> +inf
+        auto closed = [&](bool in, int64_t j) { return in && (Tf[j] < ts || j == ts_off); };
+        const bool band = closed(x > 0, i - L) || closed(x + 1 < W, i + L) || closed(y > 0, i - W * L) ||
+                          closed(y + 1 < H, i + W * L) || closed(z > 0, i - 1) || closed(z + 1 < L, i + 1);
+        Te[i] = band ? v : INF;
     }
 }
 

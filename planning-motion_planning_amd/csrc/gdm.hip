@@ -119,11 +119,13 @@ __device__ __forceinline__ double interp2_general(double a, double b, double g00
     const double a10 = g01 - g00, a01 = g10 - g00, a11 = g11 + g00 - g01 - g10;
     return g00 + a10 * a + a01 * b + a11 * a * b;
 }
-// The step's operands leave the domain of sqrt_core / div_core: |g|^2 below 2^-767 or not
-// finite, or an interpolated component that is nonzero but below 2^-900 in magnitude.  (With
-// |g|^2 >= 2^-767 every divisor is >= 2^-383; in the |g| >= 0.01 branch dx_n^2 + dy^2 >= 5e-5.)
+// The step's operands leave the domain of sqrt_core / div_core: |g|^2 outside [2^-767, 2^200]
+// or not finite, or an interpolated component that is nonzero but below 2^-900 in magnitude.
+// (With |g|^2 >= 2^-767 every divisor is >= 2^-383; with |g|^2 <= 2^200 both divisors, |g| and
+// sqrt(dx_n^2 + dy^2) <= |g| + 1, stay <= 2^100, the range div_core's argument and the self-test
+// cover; in the |g| >= 0.01 branch dx_n^2 + dy^2 >= 5e-5.)
 __device__ __forceinline__ bool walk_odd(double dx, double dy, double s1) {
-    const double lo = 0x1p-767, big = 0x1p1000, tiny = 0x1p-900;
+    const double lo = 0x1p-767, big = 0x1p200, tiny = 0x1p-900;
     return !(s1 >= lo && s1 <= big) | ((dx != 0.0) & (__builtin_fabs(dx) < tiny)) |
            ((dy != 0.0) & (__builtin_fabs(dy) < tiny));
 }

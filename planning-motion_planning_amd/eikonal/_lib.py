@@ -207,10 +207,39 @@ def load_dem_txt(path, nthreads=0):
     return out
 
 
+def parse_options(options):
+    """{name: value} from a dict or an "A=1,B=2" string; unknown names raise ValueError."""
+    if not options:
+        return {}
+    if isinstance(options, str):
+        items = {}
+        for item in filter(None, (x.strip() for x in options.split(","))):
+            name, eq, val = item.partition("=")
+            if not eq:
+                raise ValueError(f"solver option {item!r}: expected NAME=VALUE")
+            items[name.strip()] = float(val)
+        options = items
+    out = {}
+    for name, val in options.items():
+        if "OPT_" + name not in globals():
+            known = sorted(k[4:] for k in globals() if k.startswith("OPT_"))
+            raise ValueError(f"unknown solver option {name!r} (known: {', '.join(known)})")
+        out[name] = float(val)
+    return out
+
+
+def options_from_env(var="EIK_OPTIONS"):
+    """The A/B hook of bench.py and tools/: EIK_OPTIONS="PASSES=16,SCHED=1" (opt-in, explicit)."""
+    return os.environ.get(var, "")
+
+
 class Context:
     """One eik_ctx (device state + HIP stream); use one per host thread."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, options=None):
+        """options: solver options applied at creation, a dict {name: value} or a string
+        "PASSES=16,SCHED=1" (names of the OPT_* constants without the prefix).  Nothing is read
+        from the environment here: benches and tools pass options_from_env() explicitly."""
         L = lib()
         h = vp()
         rc = L.eik_create(int(device), C.byref(h))
@@ -218,10 +247,8 @@ class Context:
             raise EikError(rc, L.eik_last_error(None).decode())
         self._h = h
         self.device = device
-        # A/B hook for tools and benches: EIK_OPTIONS="FRESH_FIRST=0,PASSES=16" sets OPT_<name>
-        for item in filter(None, os.environ.get("EIK_OPTIONS", "").split(",")):
-            name, _, val = item.partition("=")
-            self.set_option(globals()["OPT_" + name.strip()], float(val))
+        for name, val in parse_options(options).items():
+            self.set_option(globals()["OPT_" + name], float(val))
 
     def _chk(self, rc):
         if rc != EIK_OK:

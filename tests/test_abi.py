@@ -36,3 +36,16 @@ def test_no_device_fails_loudly():
     with pytest.raises(eikonal.EikError) as e:
         eikonal.Context(0)
     assert e.value.code == L.EIK_ERR_NODEVICE
+
+
+def test_solver_options_parse():
+    """Context(options=...) input handling (no GPU needed): names of the OPT_* constants, unknown
+    names rejected with the list of known ones; nothing is taken from the environment."""
+    from eikonal import _lib as L
+
+    assert L.parse_options(None) == {} and L.parse_options("") == {}
+    assert L.parse_options("PASSES=16, SCHED=1") == {"PASSES": 16.0, "SCHED": 1.0}
+    assert L.parse_options({"PASSES": 8}) == {"PASSES": 8.0}
+    for bad in ("PASES=16", "PASSES", {"NOPE": 1}):
+        with pytest.raises(ValueError):
+            L.parse_options(bad)

@@ -3,9 +3,10 @@
 (:1639), end to end through the drop-in and through eik_arm_path_f64, against the reference's own
 outputs (tests/golden/fm3d_early.npz: cubes + end-effector volumes; fmm3d.npz: layered + cubes).
 
-Tolerances: finite masks equal; closed cells (reference T < T[start]) <= 1e-9; band cells
-bracketed reference <= GPU <= 1.05 x reference (the reference's band value depends on its
-sequential update order; measured <= 4.2 %, tests/test_oracle_golden.py); paths <= 1e-9."""
+Tolerances: finite masks equal; closed cells (reference T < T[start]) <= 1e-9; band cells hold
+their final value, bracketed GPU <= reference <= 1.05 x GPU (the reference's tentative band value
+depends on its sequential update order; measured <= 1.5 % on the fixtures, <= 2.6 % on the
+random arm areas of tests/test_gpu_arm.py); paths <= 1e-9."""
 import numpy as np
 import pytest
 
@@ -34,7 +35,7 @@ def check_early(T, R, s):
     assert np.abs(T[closed] - R[closed]).max() <= 1e-9
     assert abs(T[s[1], s[0], s[2]] - ts) <= 1e-9
     band = np.isfinite(R) & ~closed
-    assert np.all(T[band] >= R[band] - 1e-9) and np.all(T[band] <= 1.05 * R[band] + 1e-9)
+    assert np.all(T[band] <= R[band] + 1e-9) and np.all(R[band] <= 1.05 * T[band] + 1e-9)
 
 
 @pytest.mark.parametrize("name,p", CASES)

@@ -69,32 +69,38 @@ def hausdorff(a, b):
 
 @pytest.mark.parametrize("i", range(6))
 def test_bidirectional(ctx, golden, i):
+    """biComputeTmap (FastMarching.py:114-162) and the planner's two descents from nodeJoin
+    (Coupled_motion_planner.py:1225-1232) against the reference's own outputs: nodeJoin, the
+    fronts' PARTIAL fields (finite masks; closed values equal, band values at their final value,
+    bracketed GPU <= reference <= 1.05 x GPU) and the rover path, truncated or not, as the
+    reference returns it.  Maps with exact ties of T (uniform, b0/b1): the reference pops ties
+    LIFO, the GPU by node index, so a few tied cells at the fronts' edges may differ."""
     d = golden("fmm2d_bidir")
     p = f"b{i}_"
+    ties = i < 2
     cost = d[p + "cost"].astype(np.float64)
     goal, start = d[p + "goal"], d[p + "start"]
     TG, TS, join = ctx.tmap2d_bidir(cost, goal, start)
-    O.set_strict(False)
-    try:
-        RG, RS = O.fmm2d(cost, goal), O.fmm2d(cost, start)
-    finally:
-        O.set_strict(True)
-    for T, R in ((TG, RG), (TS, RS)):
-        fin = np.isfinite(R)
-        assert np.array_equal(np.isfinite(T), fin) and np.abs(T[fin] - R[fin]).max() <= 1e-9
     assert join.dtype == np.uint32
-    # the join is read from pop ranks; ties (uniform maps) may pick a different node of the
-    # same iteration, so check it is within a couple of cells of the reference's
-    assert np.abs(join.astype(int) - d[p + "join"].astype(int)).max() <= 2
-    if str(d[p + "pathS_err"]) or str(d[p + "pathG_err"]):
-        return
+    if ties:
+        assert np.abs(join.astype(int) - d[p + "join"].astype(int)).max() <= 2
+    else:
+        assert np.array_equal(join, d[p + "join"])
+    for T, R in ((TG, d[p + "TG"]), (TS, d[p + "TS"])):
+        assert int((np.isfinite(T) != np.isfinite(R)).sum()) <= (4 if ties else 0)
+        f = np.isfinite(T) & np.isfinite(R)
+        assert np.all(T[f] <= R[f] + 1e-9) and np.all(R[f] <= 1.05 * T[f] + 1e-9)
     pg, sg = ctx.path2d(TG, _f(join), _f(goal))
     ps, ss = ctx.path2d(TS, _f(join), _f(start))
-    if sg != 0 or ss != 0:
-        pytest.skip("fallback-truncated path on full field")
+    for got, st, key in ((pg, sg, "pathG"), (ps, ss, "pathS")):
+        ref = d[p + key]
+        _, rst = O.gdm2d(d[p + ("TG" if key == "pathG" else "TS")], _f(d[p + "join"]),
+                         _f(goal if key == "pathG" else start))
+        assert st == rst, (key, st, rst)  # b4: the reference's start-side walk is truncated (numpy-2 fallback)
+        assert got.shape == ref.shape and np.abs(got - ref).max() <= 0.01, (key, got.shape, ref.shape)
     rover = np.vstack((np.flipud(ps), pg[1:]))
     ref = np.vstack((np.flipud(d[p + "pathS"]), d[p + "pathG"][1:]))
-    assert hausdorff(rover, ref) <= 3.0
+    assert hausdorff(rover, ref) <= 0.01
 
 
 def test_path_device_fp32_field(ctx):

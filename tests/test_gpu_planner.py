@@ -4,9 +4,10 @@
 reference's biComputeTmap) -> C GDM -> numpy assembly of Coupled_motion_planner.py:1228-1252).
 
 Tolerances: the cost raster within 1e-12 relative (blur summation order, tests/test_gpu_costmap.py);
-the join from pop ranks within 2 cells (ties, tests/test_gpu_path.py::test_bidirectional); the
-rover path within 3 cells Hausdorff (paths descend full fields from a join that may differ by
-those cells); z and heading exactly as the assembly defines them on the GPU path."""
+the join equal (no exact ties of T on terrain costs); the rover path of the same length within 0.01
+cells Hausdorff (both chains descend the fronts' partial fields, whose band values differ,
+tests/test_gpu_path.py::test_bidirectional); z and heading exactly as the assembly defines them
+on the GPU path."""
 import math
 
 import numpy as np
@@ -48,9 +49,11 @@ def test_rover_path_matches_oracle_chain(n, seed):
     fin = np.isfinite(cT)
     assert np.array_equal(np.isfinite(cost), fin)
     assert np.abs(cost[fin] - cT[fin]).max() <= 1e-12 * np.abs(cT[fin]).max()
-    assert got_j.dtype == np.uint32 and np.abs(got_j.astype(int) - ref_j.astype(int)).max() <= 2
+    assert got_j.dtype == np.uint32 and np.array_equal(got_j, ref_j)
     assert len(got_p) > 10 and got_p.shape[1] == 3
-    assert hausdorff(got_p[:, :2] / RES, ref_p[:, :2] / RES) <= 3.0
+    # both descend the fronts' partial fields (FastMarching.py:141-162) from the same join
+    h = hausdorff(got_p[:, :2] / RES, ref_p[:, :2] / RES)
+    assert got_p.shape == ref_p.shape and h <= 0.01, (got_p.shape, ref_p.shape, h)
     # z and heading of the GPU path follow :1246-1252 on its own waypoints
     Zs = Z - Z.min()
     iy = np.round(got_p[:, 1] / RES).astype(np.int64)

@@ -60,7 +60,7 @@ def main():
     dev = torch.device("cuda", 0)
     for opts in ("", "SCHED=0", "PASSES=1"):
         os.environ["EIK_OPTIONS"] = opts
-        ctx = eikonal.Context(0)
+        ctx = eikonal.Context(0, options=eikonal._lib.options_from_env())
         ctx.set_option(L.OPT_MODE, L.MODE_PERSISTENT)
         c = torch.from_numpy(c32).to(dev, torch.float32)
         T = torch.empty_like(c)
