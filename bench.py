@@ -70,6 +70,8 @@ def main():
     ap.add_argument("--no-timing", action="store_true", help="skip per-launch events (roofline)")
     ap.add_argument("--no-extra", action="store_true", help="skip the C3 / C5 secondary measurements")
     ap.add_argument("--extra-steps", type=int, default=5)
+    ap.add_argument("--extras", type=str, default="all",
+                    help="comma list of extra_configs to run at N = 1 (C2_other,C3,C5,costmap,C4_1gpu,arm) or all")
     ap.add_argument("--pmc-traffic", type=str, default=None,
                     help="PMC summary (tools/pmc_traffic.py); default profiles/pmc_traffic_<dtype>.json")
     args = ap.parse_args()
@@ -281,17 +283,20 @@ def main():
         del T
         torch.cuda.empty_cache()
         other = "f32" if f64 else "f64"
-        out["extra_configs"] = {
-            f"C2_{other}": bench_c2(ctx, dev, stream, cost, goal_g, args.extra_steps, other),
-            "C3": bench_batch(ctx, dev, stream, args.extra_steps, tdt, edt),
-            "C5": bench_layers(ctx, dev, stream, cost.float(), goal_g, args.extra_steps),
-            "costmap": bench_costmap(ctx, dev, stream, args.extra_steps, goal_g),
-            "C4_1gpu": bench_c4(ctx, dev, stream, max(2, args.extra_steps // 2), tdt, edt),
-            "arm": bench_arm(ctx, args.extra_steps),
+        want = set(args.extras.split(",")) if args.extras != "all" else None
+        xs = {
+            f"C2_{other}": lambda: bench_c2(ctx, dev, stream, cost, goal_g, args.extra_steps, other),
+            "C3": lambda: bench_batch(ctx, dev, stream, args.extra_steps, tdt, edt),
+            "C5": lambda: bench_layers(ctx, dev, stream, cost.float(), goal_g, args.extra_steps),
+            "costmap": lambda: bench_costmap(ctx, dev, stream, args.extra_steps, goal_g),
+            "C4_1gpu": lambda: bench_c4(ctx, dev, stream, max(2, args.extra_steps // 2), tdt, edt),
+            "arm": lambda: bench_arm(ctx, args.extra_steps),
         }
         if f64:
-            out["extra_configs"]["C4_1gpu_f32"] = bench_c4(ctx, dev, stream, max(2, args.extra_steps // 2),
-                                                            torch.float32, L.EIK_F32)
+            xs["C4_1gpu_f32"] = lambda: bench_c4(ctx, dev, stream, max(2, args.extra_steps // 2), torch.float32,
+                                                 L.EIK_F32)
+        out["extra_configs"] = {k: fn() for k, fn in xs.items()
+                                if want is None or k in want or (k.startswith("C2_") and "C2_other" in want)}
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cost, goal_g)
@@ -459,11 +464,9 @@ def bench_arm(ctx, steps, half=30, m=40, K=16, res=0.05):
     sec_t = timed_loop(lambda: ctx.arm_tunnel_cost(base, heading, vol), steps)
     out = {}
 
-    def full():
-        out["r"] = ctx.arm_path(Z, obst, base, heading, vol, 0.5, want_fields=True)
-
-    sec_p = timed_loop(full, steps)
-    path, st, cost, _ = out["r"]
+    # the planner's call: host DEM area -> volume -> early-exit field -> path (no field copies back)
+    sec_p = timed_loop(lambda: ctx.arm_path(Z, obst, base, heading, vol, 0.5), steps)
+    path, st, cost, _ = ctx.arm_path(Z, obst, base, heading, vol, 0.5, want_fields=True)
     # K candidate fetch poses: the sample node moved around the last base point
     goals = []
     for k in range(K):
@@ -505,6 +508,11 @@ def bench_layers(ctx, dev, stream, cost2d, goal, steps, Lz=3):
                                          stream.cuda_stream))
 
     sec = timed_loop(solve, steps)
+    # per-launch event time of the layered kernel over the timed solves (one launch per solve)
+    ms_l = []
+    for _ in range(steps):
+        solve()
+        ms_l.append(ctx.stats()["solve_ms"])
     st = ctx.stats()
     cap = 30004
     out_d = torch.empty((cap, 3), dtype=torch.float64, device=dev)
@@ -525,6 +533,21 @@ def bench_layers(ctx, dev, stream, cost2d, goal, steps, Lz=3):
            "steps": steps, "launches_per_solve": st.get("iterations"), "tile_visits_per_solve": st.get("tile_visits"),
            "path_ms_device": round(e0.elapsed_time(e1), 3), "path_points": int(n_d.item()),
            "path_status": int(st_d.item())}
+    # roofline of fim2dl_persist_kernel<3> (algorithmic bytes: 4 B x 3 layers per cell of cost read,
+    # T read and T write per full visit + halo, T write + halo per in-place pass)
+    ms_k = float(np.mean(ms_l))
+    ach = st["bytes_alg"] / (ms_k * 1e-3) / 1e9 if ms_k > 0 else None
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic_c5.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get("bytes_per_launch")
+        except Exception:
+            traffic = None
+    res["roofline"] = {"bound": "hbm", "kernel": f"fim2dl_persist_kernel<{Lz}>", "achieved": round(ach, 2) if ach else None,
+                       "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None,
+                       "traffic": traffic, "alg_bytes_per_launch": round(st["bytes_alg"]),
+                       "avg_launch_us": round(ms_k * 1e3, 2), "inplace_passes_per_solve": st.get("inplace_passes")}
     del cost, T
     torch.cuda.empty_cache()
     return res

@@ -96,7 +96,14 @@ struct Fim3dArgs {
     int max_passes;        // relaxation passes per tile visit
     unsigned long long* visits;
     int tpv;               // tiles per volume (B volumes: tile = volume * tpv + tile in volume)
+    // early exit at `start` (FastMarching3D.py:141; one volume): a cell is lowered only to values
+    // <= T[stop_off] + *stop_slack (the largest finite cost), the bound of every value the
+    // early-exit field keeps (fim3d_early_kernel).  stop_off = -1: no bound.
+    int64_t stop_off;
+    const void* stop_slack;  // device R
 };
+// the largest finite cost of n values (non-negative or +inf) -> *d_max (device R, zeroed here)
+hipError_t max_finite(const void* cost, int64_t n, bool f64, void* d_max, hipStream_t st);
 // T = inf for B volumes, goal cell of volume b = d_goals[3b..3b+2] (x, y, z) set to 0 and listed
 hipError_t fim3d_init(const Fim3dArgs& a, bool f64, const int64_t* d_goals, int B, hipStream_t st);
 hipError_t fim3d_sweep(const Fim3dArgs& a, bool f64, int grid, hipStream_t st);

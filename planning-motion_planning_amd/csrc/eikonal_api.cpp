@@ -913,14 +913,23 @@ static int layered_plan(eik_ctx* c, const void* d_cost, int64_t H, int64_t W, in
 
 // B independent volumes of one shape (list mode; the tiles of all volumes share the lists).
 // goals: B x (x, y, z), host memory.
+// stop_off >= 0 (B = 1): FastMarching3D.computeTmap's early exit at that cell follows, so cells are
+// only lowered to values the early-exit field keeps (Fim3dArgs::stop_off)
 static int fim3d_solve_batch(eik_ctx* c, const void* d_cost, void* d_T, int64_t B, int64_t H, int64_t W, int64_t L,
-                             int dtype, const int64_t* goals, hipStream_t st) {
+                             int dtype, const int64_t* goals, hipStream_t st, int64_t stop_off = -1) {
     Fim3dArgs a{};
     a.cost = d_cost;
     a.T = d_T;
     a.H = H;
     a.W = W;
     a.L = L;
+    a.stop_off = -1;
+    if (stop_off >= 0 && B == 1) {
+        HIPCHK(c, c->misc.ensure(64));
+        HIPCHK(c, max_finite(d_cost, H * W * L, dtype == EIK_F64, (char*)c->misc.p + 32, st));
+        a.stop_off = stop_off;
+        a.stop_slack = (char*)c->misc.p + 32;
+    }
     fim3d_tile_shape(L, &a.tx, &a.ty, &a.tz);
     a.ntx = (int)((W + a.tx - 1) / a.tx);
     a.nty = (int)((H + a.ty - 1) / a.ty);
@@ -984,15 +993,23 @@ static int fim3d_solve_batch(eik_ctx* c, const void* d_cost, void* d_T, int64_t 
     return rc;
 }
 
+static int fim3d_solve_one(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, int64_t W, int64_t L, int dtype,
+                           const int64_t goal[3], hipStream_t st, int64_t stop_off);
+
 int eik_fim3d_solve(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, int64_t W, int64_t L, int dtype,
                     const int64_t goal[3], void* stream) {
+    return fim3d_solve_one(c, d_cost, d_T, H, W, L, dtype, goal, (hipStream_t)stream, -1);
+}
+
+// one volume; stop_off >= 0: the caller applies the early exit at that cell afterwards
+static int fim3d_solve_one(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, int64_t W, int64_t L, int dtype,
+                           const int64_t goal[3], hipStream_t st, int64_t stop_off) {
     if (!c || !d_cost || !d_T || !goal || H < 1 || W < 1 || L < 1)
         return c ? set_err(c, EIK_ERR_ARG, "bad 3D arguments") : EIK_ERR_ARG;
     if (goal[0] < 0 || goal[1] < 0 || goal[2] < 0 || goal[0] >= W || goal[1] >= H || goal[2] >= L)
         return set_err(c, EIK_ERR_ARG, "goal (%ld,%ld,%ld) outside %ldx%ldx%ld", (long)goal[0], (long)goal[1],
                        (long)goal[2], (long)H, (long)W, (long)L);
     HIPCHK(c, hipSetDevice(c->device));
-    hipStream_t st = (hipStream_t)stream;
     if (dtype == EIK_F32 && c->mode == kModePersistent && c->max_rounds == 1 && H * W * L * 4 < (int64_t)UINT32_MAX) {
         int z0 = 0, nl = 0;
         int rc = layered_plan(c, d_cost, H, W, L, st, &z0, &nl);
@@ -1001,7 +1018,7 @@ int eik_fim3d_solve(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, int64_
             return solve_layered(c, d_cost, d_T, H, W, L, z0, nl, goal, st);
         }
     }
-    return fim3d_solve_batch(c, d_cost, d_T, 1, H, W, L, dtype, goal, st);
+    return fim3d_solve_batch(c, d_cost, d_T, 1, H, W, L, dtype, goal, st, stop_off);
 }
 
 }  // extern "C"
@@ -1028,7 +1045,7 @@ static int tmap3d_host(eik_ctx* c, const R* cost, int64_t H, int64_t W, int64_t 
     HIPCHK(c, c->T.ensure(sizeof(R) * n));
     HIPCHK(c, hipMemcpyAsync(c->cost.p, cost, sizeof(R) * n, hipMemcpyHostToDevice, c->stream));
     const int dt = sizeof(R) == 8 ? EIK_F64 : EIK_F32;
-    rc = eik_fim3d_solve(c, c->cost.p, c->T.p, H, W, L, dt, goal, c->stream);
+    rc = fim3d_solve_one(c, c->cost.p, c->T.p, H, W, L, dt, goal, c->stream, early_offset(goal, start, H, W, L));
     if (rc) return rc;
     const void* src = c->T.p;
     if (start) {
@@ -1606,7 +1623,8 @@ int eik_arm_path_f64(eik_ctx* c, const double* Z, const double* obst, int64_t m,
     // with its early exit once initialWayPointArm is popped (FastMarching3D.py:141)
     const int64_t goal[3] = {v->final_wp[0], v->final_wp[1], v->final_wp[2]};
     const int64_t start[3] = {v->initial_wp[0], v->initial_wp[1], v->initial_wp[2]};
-    rc = eik_fim3d_solve(c, dC, dTf, v->sY, v->sX, v->sZ, EIK_F64, goal, st);
+    rc = fim3d_solve_one(c, dC, dTf, v->sY, v->sX, v->sZ, EIK_F64, goal, st,
+                         early_offset(goal, start, v->sY, v->sX, v->sZ));
     if (rc) return rc;
     rc = eik_fim3d_early_exit(c, dC, dTf, dT, v->sY, v->sX, v->sZ, EIK_F64, goal, start, st);
     if (rc) return rc;

@@ -43,6 +43,31 @@ struct alignas(2 * sizeof(R)) Cell {
     R t, c;
 };
 
+// LDS bank swizzle (EIK_SWZ, default on): a cell of an LDS column with bit 4 set holds (cost, T)
+// instead of (T, cost).  The sweeps' T-only accesses (ds_min, the upstream-x read, the start-row
+// read) of a skewed anti-diagonal put lane l at byte -(kLds - 1) * sizeof(Cell) * l from lane 0:
+// with T always the cell's first half that is bank -2l mod 32 (fp32, b32 banking) / -4l mod 64
+// (fp64, b64), so lanes l and l + 16 -- in the same 32-lane group -- collide on every step (53 %
+// of the sweep's LDS cycles were conflict cycles, profiles/r02_sq_counters.json).  Their columns
+// always differ in bit 4, so with the swap one of the two reads the other half of its cell: every
+// T access of a step is conflict-free.  Every LDS accessor of a tile cell goes through these.
+#ifndef EIK_SWZ
+#define EIK_SWZ 1
+#endif
+__device__ __forceinline__ constexpr int cell_swz(int col) { return EIK_SWZ ? (col >> 4) & 1 : 0; }
+template <typename R>
+__device__ __forceinline__ R& cell_t(Cell<R>* Ts, int idx, int col) {
+    return reinterpret_cast<R*>(Ts + idx)[cell_swz(col)];
+}
+template <typename R>
+__device__ __forceinline__ R& cell_c(Cell<R>* Ts, int idx, int col) {
+    return reinterpret_cast<R*>(Ts + idx)[1 - cell_swz(col)];
+}
+template <typename R>
+__device__ __forceinline__ Cell<R> make_cell(R t, R c, int col) {
+    return cell_swz(col) ? Cell<R>{c, t} : Cell<R>{t, c};
+}
+
 // One quadrant sweep of the staged tile.  DX/DY = +-1: direction of propagation.
 // Lane l owns column x; at step s it updates row r = s - l (skewed Gauss-Seidel), so its
 // upstream x neighbour is lane l-1's previous result (DPP) and its upstream y neighbour its own.
@@ -85,8 +110,13 @@ __device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lan
     // while the lane's window lies ahead the group reads guard rows and ends on the start-side
     // halo row (cur = its T, as the per-step clamp gave); past the window it reads the far halo
     // and guard rows (cost +inf: no update).  Within the window the rows are exact.
-    const int lo_b = -(D - 1) * kRow + col * S, hi_b = (kLds - 1) * kRow + col * S;
-    int raw = DY > 0 ? (1 - lane) * kRow + col * S : (kTile - (D - 1) + lane) * kRow + col * S;
+    // byte offsets within a row: this lane's T, its cost relative to it, and the upstream column's T
+    constexpr int RB = (int)sizeof(R);
+    const int colT = col * S + cell_swz(col) * RB;
+    const int dC = (1 - 2 * cell_swz(col)) * RB;
+    const int dU = (col - DX) * S + cell_swz(col - DX) * RB - colT;
+    const int lo_b = -(D - 1) * kRow + colT, hi_b = (kLds - 1) * kRow + colT;
+    int raw = DY > 0 ? (1 - lane) * kRow + colT : (kTile - (D - 1) + lane) * kRow + colT;
     auto off = [](int u) { return (DY > 0 ? u : D - 1 - u) * kRow; };
     auto clampb = [&](int x) {  // one v_med3_i32 (the compiler emits min + cmp + cndmask)
         int r;
@@ -95,16 +125,21 @@ __device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lan
     };
     bool changed = false;
     // the upstream halo row value is the lane's "previous row" result before it starts
-    R cur = reinterpret_cast<const Cell<R>*>(base + (DY > 0 ? 0 : kLds - 1) * kRow + col * S)->t;
+    R cur = *reinterpret_cast<const R*>(base + (DY > 0 ? 0 : kLds - 1) * kRow + colT);
     R q_old[D], q_upx[D], q_c[D];
     int gb = clampb(raw);  // lowest row of the group being fetched (byte offset from Ts)
     raw += DY * D * kRow;
     auto fetch = [&](int u) {
         const int o = gb + off(u);
-        const Cell<R> v = *reinterpret_cast<const Cell<R>*>(base + o);
+#if EIK_SWZ
+        q_old[u] = *reinterpret_cast<const R*>(base + o);
+        q_c[u] = *reinterpret_cast<const R*>(base + o + dC);
+#else
+        const Cell<R> v = *reinterpret_cast<const Cell<R>*>(base + o);  // one ds_read_b64 / b128
         q_old[u] = v.t;
         q_c[u] = v.c;
-        q_upx[u] = reinterpret_cast<const Cell<R>*>(base + o - DX * S)->t;
+#endif
+        q_upx[u] = *reinterpret_cast<const R*>(base + o + dU);
     };
 #pragma unroll
     for (int u = 0; u < D; ++u) fetch(u);
@@ -125,12 +160,12 @@ __device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lan
                 // fresh value alone (it is at most the prefetched LDS value of the same cell, read
                 // one step earlier) and lane 0 keeps the halo column's LDS value (the DPP's old)
                 w = godunov2_chain(wave_shr1(cur, q_upx[u]), cur, q_c[u], c2x2);
-                lds_min(&reinterpret_cast<Cell<R>*>(base + gcur + off(u))->t, w);
+                lds_min(reinterpret_cast<R*>(base + gcur + off(u)), w);
                 if constexpr (TRACK) changed |= w < q_old[u] * keep;
                 cur = fmin_nn(w, q_old[u]);  // NaN (both-inf case): keeps old
             } else {
                 w = godunov2_chain(umin(wave_shr1_umin_id(cur), q_upx[u]), cur, q_c[u], c2x2);
-                lds_min(&reinterpret_cast<Cell<R>*>(base + gcur + off(u))->t, w);
+                lds_min(reinterpret_cast<R*>(base + gcur + off(u)), w);
                 if constexpr (TRACK) changed |= w < q_old[u] * keep;
                 cur = umin(w, q_old[u]);  // NaN (both-inf case) sorts above every value: keeps old
             }
@@ -194,11 +229,11 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
     // the ring's own row / column is never an upstream value of a finite-cost cell).
     const int64_t sy = y0 + kTile < a.H ? y0 + kTile : a.H;
     const int64_t sx = x0 + kTile < a.W ? x0 + kTile : a.W;
-    int h;
-    if (wave == 0)      h = 0 * kLds + lane + 1;
-    else if (wave == 1) h = (int)(sy - y0 + 1) * kLds + lane + 1;
-    else if (wave == 2) h = (lane + 1) * kLds + 0;
-    else                h = (lane + 1) * kLds + (int)(sx - x0 + 1);
+    int h, hcol;  // this lane's halo cell and its LDS column
+    if (wave == 0)      { hcol = lane + 1;              h = 0 * kLds + hcol; }
+    else if (wave == 1) { hcol = lane + 1;              h = (int)(sy - y0 + 1) * kLds + hcol; }
+    else if (wave == 2) { hcol = 0;                     h = (lane + 1) * kLds + hcol; }
+    else                { hcol = (int)(sx - x0 + 1);    h = (lane + 1) * kLds + hcol; }
     // this lane's halo cell; in range of the raster: one unconditional load (no branch, so it
     // issues together with the staging loads), else a ghost strip or +inf
     const int64_t hy = wave == 0 ? y0 - 1 : wave == 1 ? sy : y0 + lane;
@@ -222,9 +257,10 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
         for (int k = 0; k < 4; ++k) {
             const int ry = (tid >> 4) + 16 * k;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) Ts[(ry + 1) * kLds + cx + e + 1] = Cell<R>{told[4 * k + e], cr[4 * k + e]};
+            for (int e = 0; e < 4; ++e)
+                Ts[(ry + 1) * kLds + cx + e + 1] = make_cell<R>(told[4 * k + e], cr[4 * k + e], cx + e + 1);
         }
-        Ts[h] = Cell<R>{hv, INF};
+        Ts[h] = make_cell<R>(hv, INF, hcol);
     };
     if (full) {
         R cr[16];
@@ -267,7 +303,7 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
             if (sx - x0 < kTile) Ts[tid * kLds + (kLds - 1)] = Cell<R>{INF, INF};
         }
     }
-    if (lane < 4) Ts[(lane >> 1) * (kLds - 1) * kLds + (lane & 1) * (kLds - 1)].c = INF;  // corners
+    if (lane < 4) cell_c(Ts, (lane >> 1) * (kLds - 1) * kLds + (lane & 1) * (kLds - 1), (lane & 1) * (kLds - 1)) = INF;  // corners
     __syncthreads();
     EIK_PROBE(1);
 
@@ -325,7 +361,7 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
             bool any = false;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                nv[e] = Ts[(ry + 1) * kLds + cx + e + 1].t;
+                nv[e] = cell_t(Ts, (ry + 1) * kLds + cx + e + 1, cx + e + 1);
                 any |= nv[e] < told[4 * k + e];
                 // (a ghost cell inside a cut tile is lowered by the halo reload, never by a sweep)
                 if (nv[e] < told[4 * k + e] * keep && (full || (gy < a.H && x0 + cx + e < a.W))) {
@@ -334,10 +370,10 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
                     // A neighbour can only improve if this edge value undercuts the neighbour's
                     // adjacent cell (the halo value, stale => larger => conservative).
                     const int lx = cx + e + 1, ly = ry + 1;
-                    if (ry == 0 && nv[e] < Ts[lx].t) { fl |= 1u; kmin[0] = umin(kmin[0], nv[e]); }
-                    if (ry == kTile - 1 && nv[e] < Ts[(kLds - 1) * kLds + lx].t) { fl |= 2u; kmin[1] = umin(kmin[1], nv[e]); }
-                    if (cx + e == 0 && nv[e] < Ts[ly * kLds].t) { fl |= 4u; kmin[2] = umin(kmin[2], nv[e]); }
-                    if (cx + e == kTile - 1 && nv[e] < Ts[ly * kLds + kLds - 1].t) { fl |= 8u; kmin[3] = umin(kmin[3], nv[e]); }
+                    if (ry == 0 && nv[e] < cell_t(Ts, lx, lx)) { fl |= 1u; kmin[0] = umin(kmin[0], nv[e]); }
+                    if (ry == kTile - 1 && nv[e] < cell_t(Ts, (kLds - 1) * kLds + lx, lx)) { fl |= 2u; kmin[1] = umin(kmin[1], nv[e]); }
+                    if (cx + e == 0 && nv[e] < cell_t(Ts, ly * kLds, 0)) { fl |= 4u; kmin[2] = umin(kmin[2], nv[e]); }
+                    if (cx + e == kTile - 1 && nv[e] < cell_t(Ts, ly * kLds + kLds - 1, kLds - 1)) { fl |= 8u; kmin[3] = umin(kmin[3], nv[e]); }
                     const int64_t gx = x0 + cx + e;  // subdomain edges inside a partial tile (DD)
                     if (gy == a.H - 1 && ry != kTile - 1) fl |= 32u;
                     if (gx == a.W - 1 && cx + e != kTile - 1) fl |= 64u;
@@ -386,7 +422,7 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
             activate_neighbours(a, tile, defer ? 0u : f, L.key, 0, 0u);  // lanes 0..4 (T already drained)
             if (defer && tid == 0) L.flags_acc |= f & 0x6fu;
             dirs = self ? 0xFu : sweep_dirs(pend);  // a self revisit: every direction
-            Ts[h].t = hv;
+            cell_t(Ts, h, hcol) = hv;
             __syncthreads();  // every wave has read L.flags and its halo side is in
             if (tid == 0) {
                 L.flags = 0;  // next OR-ed after the next sweep barrier

@@ -115,6 +115,14 @@ __global__ __launch_bounds__(256) void fim3d_sweep_kernel(Fim3dArgs a) {
     const int TX = a.tx, TY = a.ty, TZ = a.tz;
     const int HX = TX + 2, HY = TY + 2, HZ = TZ + 2;  // halo box, index ((y*HX)+x)*HZ+z
     const int ncell = TX * TY * TZ;
+    // early-exit bound (see Fim3dArgs::stop_off): T[start] only decreases, so a stale read only
+    // prunes less; every cell whose final value is <= the final bound is still reached exactly
+    // (its upstream cells have smaller values), and nothing above it is kept by the early exit
+    R bound = INF;
+    if (a.stop_off >= 0) {
+        const R ts = static_cast<const R*>(a.T)[a.stop_off];
+        bound = (ts + *static_cast<const R*>(a.stop_slack)) * R(1.000001);
+    }
 
     for (int it = blockIdx.x; it < cnt; it += gridDim.x) {
         const int tile = a.lists[(int64_t)cur * a.capacity + it];
@@ -173,7 +181,7 @@ __global__ __launch_bounds__(256) void fim3d_sweep_kernel(Fim3dArgs a) {
                 const R ty_ = fmin(Ts[h - sy], Ts[h + sy]);
                 const R tz_ = fmin(Ts[h - 1], Ts[h + 1]);
                 const R nv = cst[k] == INF ? INF : local3<R>(tx_, ty_, tz_, cst[k]);
-                if (nv < v) {
+                if (nv < v && nv <= bound) {
                     Ts[h] = nv;  // owner-only write; concurrent readers see old or new (both bounds)
                     ch = true;
                 }
@@ -317,6 +325,40 @@ hipError_t fim3d_early(const void* cost, const void* Tf, void* Te, int64_t H, in
     else
         hipLaunchKernelGGL(fim3d_early_kernel<float>, dim3(grid), dim3(256), 0, st, static_cast<const float*>(cost),
                            static_cast<const float*>(Tf), static_cast<float*>(Te), H, W, L, ts_off);
+    return hipGetLastError();
+}
+
+template <typename R>
+__global__ __launch_bounds__(256) void max_finite_kernel(const R* __restrict__ c, int64_t n, R* __restrict__ out) {
+    R m = R(0);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const R v = c[i];
+        if (v < Real<R>::inf() && v > m) m = v;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const R o = __shfl_xor(m, off, 64);
+        m = o > m ? o : m;
+    }
+    // non-negative IEEE values order as unsigned integers of their bits
+    if ((threadIdx.x & 63) == 0) {
+        if constexpr (sizeof(R) == 8)
+            atomicMax(reinterpret_cast<unsigned long long*>(out), (unsigned long long)__double_as_longlong(m));
+        else
+            atomicMax(reinterpret_cast<unsigned*>(out), __float_as_uint(m));
+    }
+}
+
+hipError_t max_finite(const void* cost, int64_t n, bool f64, void* d_max, hipStream_t st) {
+    hipError_t e = hipMemsetAsync(d_max, 0, 8, st);
+    if (e != hipSuccess) return e;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (n + 255) / 256));
+    if (f64)
+        hipLaunchKernelGGL(max_finite_kernel<double>, dim3(grid), dim3(256), 0, st, static_cast<const double*>(cost),
+                           n, static_cast<double*>(d_max));
+    else
+        hipLaunchKernelGGL(max_finite_kernel<float>, dim3(grid), dim3(256), 0, st, static_cast<const float*>(cost), n,
+                           static_cast<float*>(d_max));
     return hipGetLastError();
 }
 

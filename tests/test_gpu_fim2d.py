@@ -68,6 +68,23 @@ def test_golden_fields(ctx, golden, i, f64):
     check_field(T, R, goal, f64)
 
 
+@pytest.mark.parametrize("name", ["uniform", "random"])
+@pytest.mark.parametrize("f64", [False, True])
+def test_c1_config(ctx, golden, name, f64):
+    """BASELINE configs[0] (C1): 256^2 uniform / U(1, 10) seed 0, goal (128, 128) -- the field
+    against the reference's own (tests/golden/c1.npz) and, end to end on the GPU (its field, its
+    path kernel), the reference's getPathGDM path from (30, 40)."""
+    d = golden("c1")
+    cost = d[name + "_cost"].astype(np.float64)
+    goal, start = d["goal"], d["start"]
+    T = ctx.tmap2d(cost, goal, dtype=np.float64 if f64 else np.float32)
+    check_field(T, d[name + "_T"], goal, f64)
+    if f64:
+        path, st = ctx.path2d(T, start.astype(np.float64), goal.astype(np.float64))
+        ref = d[name + "_path"]
+        assert st == 0 and path.shape == ref.shape and np.abs(path - ref).max() <= 1e-6
+
+
 @pytest.mark.parametrize("shape,kind,seed", [
     ((517, 1031), "obst", 1),      # ragged: neither side a multiple of the 64-cell tile
     ((1024, 1024), "random", 2),

@@ -1,8 +1,10 @@
 """GPU parity at BASELINE.json's full sizes (configs[1..4]), on the bench's own synthetic rasters.
 
-* C2, 4096^2 DEM raster: the fp32 field against the oracle's heap FMM (fp64, the reference's
-  algorithm, ~3 s on one core) -- masks equal, max relative error <= 2e-5; the path
-  kernel on that field against the oracle's walk on the same field, <= 1e-9 cells.
+* C2, 4096^2 DEM raster: the fp64 field (the headline arithmetic) against the oracle's heap FMM
+  (fp64, the reference's algorithm, ~3 s on one core) -- masks equal, max abs <= 1e-9 -- and its
+  path against the oracle's walk on the oracle's field; the fp32 field -- masks equal, max
+  relative error <= 2e-5 -- and the path kernel on it against the oracle's walk on
+  the same field, <= 1e-9 cells.
 * C3, 128 x 1024^2 batch: one batched solve, four of its maps against the oracle.
 * C4, 16384^2 DEM raster on one GPU: too large for the oracle inside a test, so size-independent
   properties of the converged field, evaluated on the device in fp64: T[goal] = 0; every reached
@@ -81,6 +83,37 @@ def check_properties(torch, T32, c32, goal, rows=2048):
         assert not bool(torch.isfinite(nmin[open_]).any()), "an unreached cell next to a reached one"
     assert worst <= 2e-5, worst
     return worst
+
+
+def test_c2_full_size_fp64_vs_oracle(env):
+    """The headline configuration in the headline arithmetic (bench.py --dtype f64, the reference's
+    float64): the device-resident fp64 solve of the 4096^2 C2 raster against the oracle's fp64 heap
+    FMM, masks equal and max abs <= 1e-9; then the end-to-end path (fp64 field -> path kernel,
+    device-resident, the bench's ms-to-path route) against the oracle's walk on the ORACLE's field."""
+    torch, eikonal, L, terrain, dev, ctx = env
+    N = 4096
+    cost = terrain.cost_block(0, 0, N, N, N, N, seed=42, device=dev).double().contiguous()
+    T = torch.empty_like(cost)
+    fim = eikonal.Fim2d(ctx, 1, N, N, L.EIK_F64)
+    goal, start = (N // 2, N // 2), (256, 256)
+    stream = torch.cuda.current_stream(dev)
+    fim.solve(cost.data_ptr(), T.data_ptr(), [goal], stream.cuda_stream)
+    torch.cuda.synchronize()
+    fim.close()
+    Tg = T.cpu().numpy()
+    O.set_strict(False)
+    try:
+        R = O.fmm2d(cost.cpu().numpy(), goal)
+    finally:
+        O.set_strict(True)
+    fin = np.isfinite(R)
+    assert np.array_equal(np.isfinite(Tg), fin)
+    err = np.abs(Tg[fin] - R[fin]).max()
+    assert err <= 1e-9, err
+    path, st = ctx.path2d(Tg, start, goal)
+    ref, rst = O.gdm2d(R, np.array(start, float), np.array(goal, float))
+    assert st == rst == 0 and path.shape == ref.shape and len(path) > 1000
+    assert np.abs(path - ref).max() <= 1e-6
 
 
 def test_c2_full_size_vs_oracle(env):
