@@ -51,8 +51,13 @@ struct alignas(2 * sizeof(R)) Cell {
 // of the sweep's LDS cycles were conflict cycles, profiles/r02_sq_counters.json).  Their columns
 // always differ in bit 4, so with the swap one of the two reads the other half of its cell: every
 // T access of a step is conflict-free.  Every LDS accessor of a tile cell goes through these.
+// Measured and OFF by default (profiles/r03h_swizzle_ab.log, r03h_sq_counters_swizzle_ab.json): the
+// swapped halves cost a third ds_read per step (T and cost can no longer come in one b64 / b128
+// read), LDS instructions +33 %; the conflict share fell 0.53 -> 0.30 (fp32) / 0.48 -> 0.42 (fp64),
+// but C2 got 2-4 % slower -- the conflicted accesses are off the step's dependency chain (reads
+// prefetched 4 steps ahead, ds_min not waited on), so their extra cycles were hidden anyway.
 #ifndef EIK_SWZ
-#define EIK_SWZ 1
+#define EIK_SWZ 0
 #endif
 __device__ __forceinline__ constexpr int cell_swz(int col) { return EIK_SWZ ? (col >> 4) & 1 : 0; }
 template <typename R>
