@@ -108,13 +108,20 @@ __device__ __forceinline__ double godunov2_fast(double a, double b, double c) {
 // Special values as godunov2_fast: a = b = +inf gives |a - b| = NaN, which v_min turns into c,
 // and w = +inf; c = +inf with one finite side gives NaN (no update).  v_min_f32 is written in
 // asm so that no NaN canonicalisation is inserted (IEEE minNum: a NaN operand yields the other).
+// EIK_CHAIN (fp64, default on): w = (lo + d/2) + sqrt(q)/2 with lo + d/2 formed beside the square
+// root, one dependent operation fewer on the step's chain than lo + (d + sqrt(q))/2, at the price of
+// one more rounding at T's magnitude (fp32 cannot afford it: the 4096^2 field then drifts past 2e-5
+// relative; fp64 stays within the 1e-9 tolerance, tests/test_gpu_fullsize.py).
+#ifndef EIK_CHAIN
+#define EIK_CHAIN 1
+#endif
 __device__ __forceinline__ float godunov2_chain(float a, float b, float c, float c2x2) {
     const float lo = umin(a, b);
     const float diff = a - b;
     float d;
     asm("v_min_f32 %0, |%1|, %2" : "=v"(d) : "v"(diff), "v"(c));
     const float q = __builtin_fmaf(-d, d, c2x2);
-    return __builtin_fmaf(0.5f, d + __builtin_amdgcn_sqrtf(q), lo);
+    return __builtin_fmaf(0.5f, d + __builtin_amdgcn_sqrtf(q), lo);  // one rounding at T's magnitude
 }
 // fp64 sweep step (the headline arithmetic: the reference computes in float64).  Two savings over
 // the generic form, 45 -> 28 instructions per step:
@@ -135,8 +142,13 @@ __device__ __forceinline__ double fmin_nn(double a, double b) {
 // and minus its last correction (result within ~1 ulp; the field tolerance is 1e-9 absolute).
 // q = +inf or NaN (a +inf cost) gives NaN: no update, as sqrt's +inf / NaN did.
 __device__ __forceinline__ double sqrt_sweep(double q) {
+#if EIK_CHAIN
+    // the staged costs are >= 2^-500 (fim2d.hip stage_cost), so q = 2c^2 - d^2 >= c^2 >= 2^-1000
+    const double qc = q;
+#else
     double qc;
     asm("v_max_f64 %0, %1, %2" : "=v"(qc) : "v"(q), "v"(0x1p-1000));
+#endif
     const double y = __builtin_amdgcn_rsq(qc);
     double g = qc * y, h = 0.5 * y;
     const double r = __builtin_fma(-h, g, 0.5);
@@ -151,7 +163,11 @@ __device__ __forceinline__ double godunov2_chain(double a, double b, double c, d
     double d;
     asm("v_min_f64 %0, |%1|, %2" : "=v"(d) : "v"(diff), "v"(c));
     const double q = __builtin_fma(-d, d, c2x2);
+#if EIK_CHAIN
+    return __builtin_fma(0.5, sqrt_sweep(q), __builtin_fma(0.5, d, lo));
+#else
     return __builtin_fma(0.5, d + sqrt_sweep(q), lo);
+#endif
 }
 
 // Whole-wave shift by one lane (lane i <- lane i-1) on the DPP path: v_mov_b32_dpp wave_shr:1.

@@ -36,6 +36,15 @@
 
 namespace eik {
 
+// A cost as the sweep keeps it in LDS.  fp64 with EIK_CHAIN: at least 2^-500, the domain of the
+// step's square root without a range clamp on its chain (eik_common.hpp sqrt_sweep); a zero-cost
+// cell then rises by at most 2^-500 over its upstream value, far below the 1e-9 field tolerance.
+template <typename R>
+__device__ __forceinline__ R stage_cost(R c) {
+    if constexpr (sizeof(R) == 8 && EIK_CHAIN) return __builtin_fmax(c, 0x1p-500);
+    else return c;
+}
+
 // ------------------------------------------------------------------------- quadrant sweep
 // A tile cell in LDS: arrival time and cost side by side, so one ds_read_b64 (fp32) fetches both.
 template <typename R>
@@ -263,7 +272,7 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
             const int ry = (tid >> 4) + 16 * k;
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-                Ts[(ry + 1) * kLds + cx + e + 1] = make_cell<R>(told[4 * k + e], cr[4 * k + e], cx + e + 1);
+                Ts[(ry + 1) * kLds + cx + e + 1] = make_cell<R>(told[4 * k + e], stage_cost(cr[4 * k + e]), cx + e + 1);
         }
         Ts[h] = make_cell<R>(hv, INF, hcol);
     };

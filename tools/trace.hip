@@ -42,8 +42,16 @@ int main(int argc, char** argv) {
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_ev), &ev, sizeof ev));
     Fim2dArgs a{};
     int ntx = (N + 63) / 64, tiles = ntx * ntx;
-    float *cost, *T; CK(hipMalloc(&cost, 4ull * N * N)); CK(hipMalloc(&T, 4ull * N * N));
-    CK(hipMemcpy(cost, hc.data(), 4ull * N * N, hipMemcpyHostToDevice));
+    // EIK_TRACE_F64=1: the fp64 kernel (the bench headline) on the same (float32-exact) costs
+    const bool f64 = getenv("EIK_TRACE_F64") && atoi(getenv("EIK_TRACE_F64")) == 1;
+    const size_t esz = f64 ? 8 : 4;
+    void *cost, *T; CK(hipMalloc(&cost, esz * N * N)); CK(hipMalloc(&T, esz * N * N));
+    if (f64) {
+        std::vector<double> hd(hc.begin(), hc.end());
+        CK(hipMemcpy(cost, hd.data(), 8ull * N * N, hipMemcpyHostToDevice));
+    } else {
+        CK(hipMemcpy(cost, hc.data(), 4ull * N * N, hipMemcpyHostToDevice));
+    }
     a.cost = cost; a.T = T; a.H = N; a.W = N; a.ntx = ntx; a.nty = ntx; a.tiles_per_map = tiles;
     CK(hipMalloc(&a.lists, 12ull * tiles)); CK(hipMalloc(&a.counts, 256)); CK(hipMalloc(&a.mark, 4ull * tiles));
     a.capacity = tiles; a.max_rounds = 1; a.keep = 1.f; CK(hipMalloc(&a.key, 4ull * tiles)); a.minkey = (unsigned*)a.counts + 16;
@@ -61,16 +69,16 @@ int main(int argc, char** argv) {
     float ms = 0;
     for (int rep = 0; rep < 4; ++rep) {
         CK(hipMemset(a.visits, 0, 16)); CK(hipMemset(ev, 0, 8ull * kCap * grid));
-        CK(fim2d_init(a, false, 1, goals, 0));
+        CK(fim2d_init(a, f64, 1, goals, 0));
         CK(hipEventRecord(e0, 0));
-        CK(fim2d_persist(a, false, grid, 0));
+        CK(fim2d_persist(a, f64, grid, 0));
         CK(hipEventRecord(e1, 0));
         CK(hipEventSynchronize(e1));
         CK(hipEventElapsedTime(&ms, e0, e1));
     }
     unsigned hq[64]; CK(hipMemcpy(hq, q, 256, hipMemcpyDeviceToHost));
     unsigned long long vv[2]; CK(hipMemcpy(vv, a.visits, 16, hipMemcpyDeviceToHost));
-    printf("N=%d grid=%d passes=%d: kernel %.3f ms, visits %llu (+%llu in place), err %u\n", N, grid, passes, ms, vv[0], vv[1], hq[48]);
+    printf("%s N=%d grid=%d passes=%d: kernel %.3f ms, visits %llu (+%llu in place), err %u\n", f64 ? "f64" : "f32", N, grid, passes, ms, vv[0], vv[1], hq[48]);
     std::vector<unsigned long long> he(1ull * kCap * grid);
     CK(hipMemcpy(he.data(), ev, 8ull * kCap * grid, hipMemcpyDeviceToHost));
     FILE* o = fopen(argv[4], "wb");
