@@ -45,6 +45,13 @@ __device__ __forceinline__ R stage_cost(R c) {
     else return c;
 }
 
+// EIK_EDGE_FIRST (see the write-back in process_tile): measured and OFF -- C2 2-7 % slower in fp64
+// and fp32 (profiles/r03l_edge_first_ab.log): the drain before the activations is latency, not the
+// number of stores, and the extra per-visit barrier and edge-column stores cost more than it saves.
+#ifndef EIK_EDGE_FIRST
+#define EIK_EDGE_FIRST 0
+#endif
+
 // ------------------------------------------------------------------------- quadrant sweep
 // A tile cell in LDS: arrival time and cost side by side, so one ds_read_b64 (fp32) fetches both.
 template <typename R>
@@ -364,8 +371,15 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
         // visit.  Issued now, awaited with the write-back's drain.
         unsigned pend_old = 0;
         if (COH && (a.sched & 1) && tid == 0) pend_old = atomicAnd(&a.qstate[tile], kBusy | kVisited);
-        // ---- write back changed cells, collect side flags (and entering values, ordered mode)
+        // ---- write back changed cells, collect side flags (and entering values, ordered mode).
+        // EIK_EDGE_FIRST (persistent mode, full tiles): only the tile's edge cells -- the values a
+        // neighbour's halo reads -- are stored and drained before the activations; the interior
+        // row chunks (bit k of defer_rows: this thread's row chunk k) are stored after the pass's
+        // halo has come in and drain during the next sweep, or before the visit's finish (the
+        // persistent loop drains every wave before qfinish).  Nobody else reads a busy tile's
+        // interior: its next visit starts after that finish.
         unsigned fl = 0;
+        unsigned defer_rows = 0;
         R kmin_self = INF, kmin[4] = {INF, INF, INF, INF};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -394,7 +408,11 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
                 }
             }
             if (any) {
-                if (full) {
+                if (COH && EIK_EDGE_FIRST && full && ry != 0 && ry != kTile - 1) {
+                    if (cx == 0 && nv[0] < told[4 * k]) T.st(gy * a.W + x0, nv[0]);
+                    if (cx == kTile - 4 && nv[3] < told[4 * k + 3]) T.st(gy * a.W + x0 + kTile - 1, nv[3]);
+                    defer_rows |= 1u << k;
+                } else if (full) {
                     T.st4(gy * a.W + x0 + cx, nv);
                 } else {
 #pragma unroll
@@ -421,11 +439,25 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
         if constexpr (COH) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
         __syncthreads();
         EIK_PROBE(7);
+        // the deferred interior row chunks (told holds what they store)
+        auto store_deferred = [&]() {
+            asm volatile("" ::: "memory");  // not above the halo / activation round trips
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (defer_rows & (1u << k)) {
+                    const R v[4] = {told[4 * k], told[4 * k + 1], told[4 * k + 2], told[4 * k + 3]};
+                    T.st4((y0 + (tid >> 4) + 16 * k) * a.W + x0 + cx, v);
+                }
+            }
+        };
         if (COH) {
             const unsigned f = L.flags;  // uniform
             const unsigned pend = L.pend & (kPending | kFromN | kFromS | kFromW | kFromE);
             const bool self = (f & 128u) != 0u;
-            if ((!self && !pend) || pass + 1 >= a.max_passes || a.max_rounds != 1) break;
+            if ((!self && !pend) || pass + 1 >= a.max_passes || a.max_rounds != 1) {
+                store_deferred();  // drained by the persistent loop before the finish
+                break;
+            }
             // the halo reload is issued first and the budget charge goes to wave 1, so wave 0's
             // activation atomics are the only round trips the next pass waits for
             const R hv = load_halo();
@@ -437,6 +469,7 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
             if (defer && tid == 0) L.flags_acc |= f & 0x6fu;
             dirs = self ? 0xFu : sweep_dirs(pend);  // a self revisit: every direction
             cell_t(Ts, h, hcol) = hv;
+            store_deferred();  // after the halo value is in: they drain during the next sweep
             __syncthreads();  // every wave has read L.flags and its halo side is in
             if (tid == 0) {
                 L.flags = 0;  // next OR-ed after the next sweep barrier
@@ -625,6 +658,10 @@ __global__ __launch_bounds__(kThreads, WPS) void fim2d_persist_kernel(Fim2dArgs 
     int tile = -1;
     unsigned nvis = 0;  // wave 0 lane 0: visits not yet added to the global counter
     for (;;) {
+        if (EIK_EDGE_FIRST && tile >= 0) {  // uniform: every wave's deferred interior stores
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // complete before the finish
+            __syncthreads();
+        }
         // wave 0 retires the previous tile (lanes 0..4 activate, then lane 0 finishes) while
         // wave 1 takes the next one; waves 2 and 3 go straight to the barrier
         if (threadIdx.x < 64) {
