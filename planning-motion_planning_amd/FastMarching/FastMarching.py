@@ -16,10 +16,12 @@ semantics on the host (they operate on Python scalars and lists the caller owns)
 Differences from the reference, by design:
   * computeTmap returns the full converged field (the reference raises ValueError at :107);
     with a `start` the values of every cell the reference would have closed are identical.
-  * biComputeTmap returns FULL goal/start fields (the reference's are partial: closed cells
-    exact, the rest tentative or inf) and the join read from the two fields' pop ranks.
+  * biComputeTmap returns the reference's PARTIAL goal/start fields (closed cells at their
+    final values, the band at its final value where the reference holds a tentative one, the
+    rest inf) and the join read from the two fronts' pop ranks.
   * the reference raises StopIteration on some tied decrease-keys (:72-73); the GPU solver has
-    no narrow band and returns the intended field.
+    no narrow band and returns the intended field.  The host helper updateNode keeps that
+    behaviour (and the IndexError of a search that runs past the band's end).
   * dtype: fields are computed in float64 by default (EIKONAL_DTYPE=float32 for fp32 speed).
 """
 import bisect
@@ -61,6 +63,18 @@ def getNeighbours(nodeTarget, closedMap):
     return out
 
 
+def _band_index(nbNodes, lo, c):
+    """The band search of FastMarching.py:73: enumerate(nbNodes[lo-1:], lo) visits the indices
+    lo .. lo + len(nbNodes[lo-1:]) - 1.  For lo >= 1 that is lo .. len(nbNodes) (the last one is
+    past the end: IndexError if c was not found before it); for lo == 0 the slice [-1:] holds one
+    entry, so only index 0 is tested (StopIteration if c is not first)."""
+    count = min(1, len(nbNodes)) if lo == 0 else len(nbNodes) - lo + 1
+    for k in range(lo, lo + count):
+        if np.array_equal(c, nbNodes[k]):
+            return k
+    raise StopIteration
+
+
 def updateNode(nodeTarget, costMap, Tmap, nbT, nbNodes, closedMap):
     """FastMarching.py:44-80: narrow-band update of the four children of nodeTarget.
     Host bookkeeping on the caller's lists; the GPU solver does not use a narrow band."""
@@ -77,9 +91,7 @@ def updateNode(nodeTarget, costMap, Tmap, nbT, nbNodes, closedMap):
             nbNodes.insert(i, c)
             Tmap[c[1], c[0]] = T
         elif T < Tmap[c[1], c[0]]:
-            old = Tmap[c[1], c[0]]
-            lo = bisect.bisect_left(nbT, old)
-            i = next(k for k in range(lo, len(nbNodes)) if np.array_equal(c, nbNodes[k]))
+            i = _band_index(nbNodes, bisect.bisect_left(nbT, Tmap[c[1], c[0]]), c)
             del nbT[i]
             del nbNodes[i]
             i = bisect.bisect_left(nbT, T)

@@ -51,6 +51,17 @@ def _solve(Tx, Ty, Tz, C):
     return Tr
 
 
+def _band_index(nbNodes, lo, c):
+    """The band search of FastMarching3D.py:89 (same form as FastMarching.py:73): indices
+    lo .. len(nbNodes) for lo >= 1 (IndexError past the end), only index 0 for lo == 0
+    (StopIteration if c is not first)."""
+    count = min(1, len(nbNodes)) if lo == 0 else len(nbNodes) - lo + 1
+    for k in range(lo, lo + count):
+        if np.array_equal(c, nbNodes[k]):
+            return k
+    raise StopIteration
+
+
 def updateNode(nodeTarget, costMap, Tmap, nbT, nbNodes, closedMap):
     """FastMarching3D.py:19-101 narrow-band update (host bookkeeping on the caller's lists)."""
     for d in ([0, 0, -1], [0, 0, 1], [-1, 0, 0], [1, 0, 0], [0, 1, 0], [0, -1, 0]):
@@ -66,8 +77,7 @@ def updateNode(nodeTarget, costMap, Tmap, nbT, nbNodes, closedMap):
             nbNodes.insert(i, c)
             Tmap[c[1], c[0], c[2]] = T
         elif T < Tmap[c[1], c[0], c[2]]:
-            lo = bisect.bisect_left(nbT, Tmap[c[1], c[0], c[2]])
-            i = next(k for k in range(lo, len(nbNodes)) if np.array_equal(c, nbNodes[k]))
+            i = _band_index(nbNodes, bisect.bisect_left(nbT, Tmap[c[1], c[0], c[2]]), c)
             del nbT[i]
             del nbNodes[i]
             i = bisect.bisect_left(nbT, T)

@@ -25,24 +25,70 @@ def test_scalar_helpers_match_fixtures(golden):
     assert np.array_equal(got, h["interp3_out"], equal_nan=True)
 
 
-def test_narrow_band_helpers_reproduce_reference_field(golden):
-    """updateNode/getMinNB driven like FastMarching.py:92-112 give the reference field."""
-    d = golden("fmm2d_fields")
-    p = "c0_"
-    cost = d[p + "cost"].astype(np.float64)
-    goal = [int(v) for v in d[p + "goal"]]
+def _drive_helpers(M, cost, goal, start=None):
+    """updateNode/getMinNB of module M driven like FastMarching.py:92-112 /
+    FastMarching3D.py:126-145 (break once `start` is popped)."""
+    nd = cost.ndim
     closed = np.zeros_like(cost)
     closed[cost == np.inf] = 1
     T = np.ones_like(cost) * np.inf
     nbT, nbN = [], []
-    T[goal[1], goal[0]] = 0
-    closed[goal[1], goal[0]] = 1
-    T, nbT, nbN = FM.updateNode(goal, cost, T, nbT, nbN, closed)
+    gi = (goal[1], goal[0]) + ((goal[2],) if nd == 3 else ())
+    T[gi] = 0
+    closed[gi] = 1
+    T, nbT, nbN = M.updateNode(goal, cost, T, nbT, nbN, closed)
     while nbT:
-        node, nbT, nbN = FM.getMinNB(nbT, nbN)
-        closed[node[1], node[0]] = 1
-        T, nbT, nbN = FM.updateNode(node, cost, T, nbT, nbN, closed)
-    assert np.array_equal(T, d[p + "T"])
+        node, nbT, nbN = M.getMinNB(nbT, nbN)
+        closed[(node[1], node[0]) + ((node[2],) if nd == 3 else ())] = 1
+        T, nbT, nbN = M.updateNode(node, cost, T, nbT, nbN, closed)
+        if start is not None and np.array_equal(node, start):
+            break
+    return T
+
+
+@pytest.mark.parametrize("ci", [0, 1, 2, 3, 12])
+def test_narrow_band_helpers_reproduce_reference_field(golden, ci):
+    """The host helpers reproduce the reference's fields bit for bit, full and early-exit, and
+    its failure: c12's tied decrease-key raises StopIteration (FastMarching.py:73)."""
+    d = golden("fmm2d_fields")
+    p = f"c{ci}_"
+    cost = d[p + "cost"].astype(np.float64)
+    goal = [int(v) for v in d[p + "goal"]]
+    start = [int(v) for v in d[p + "start"]]
+    if str(d[p + "err"]) == "StopIteration":
+        with pytest.raises(StopIteration):
+            _drive_helpers(FM, cost, goal)
+    else:
+        assert np.array_equal(_drive_helpers(FM, cost, goal), d[p + "T"])
+    if str(d[p + "early_err"]) == "StopIteration":
+        with pytest.raises(StopIteration):
+            _drive_helpers(FM, cost, goal, start)
+    else:
+        assert np.array_equal(_drive_helpers(FM, cost, goal, start), d[p + "T_early"])
+
+
+@pytest.mark.parametrize("vi", range(4))
+def test_narrow_band_helpers_3d_reproduce_reference_field(golden, vi):
+    d = golden("fmm3d")
+    p = f"v{vi}_"
+    cost = d[p + "cost"].astype(np.float64)
+    goal, start = d[p + "goal"].astype(np.uint32), d[p + "start"].astype(np.uint32)
+    assert np.array_equal(_drive_helpers(FM3D, cost, goal), d[p + "T"])
+    assert np.array_equal(_drive_helpers(FM3D, cost, goal, start), d[p + "T_early"])
+
+
+def test_band_search_window_matches_reference():
+    """FastMarching.py:73 searches indices lo..len(band) (IndexError past the end) and, for
+    lo == 0, only index 0 (StopIteration if the node is not first)."""
+    c = np.array([5, 5])
+    band = [np.array([1, 1]), np.array([5, 5]), np.array([2, 2])]
+    assert FM._band_index(band, 1, c) == 1 and FM3D._band_index(band, 1, c) == 1
+    with pytest.raises(StopIteration):
+        FM._band_index(band, 0, c)
+    with pytest.raises(IndexError):
+        FM._band_index([np.array([1, 1]), np.array([2, 2])], 1, c)
+    with pytest.raises(StopIteration):
+        FM3D._band_index([], 0, np.array([1, 1, 1]))
 
 
 @pytest.mark.gpu
