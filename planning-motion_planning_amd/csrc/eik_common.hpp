@@ -111,9 +111,12 @@ __device__ __forceinline__ double godunov2_fast(double a, double b, double c) {
 // EIK_CHAIN (fp64, default on): w = (lo + d/2) + sqrt(q)/2 with lo + d/2 formed beside the square
 // root, one dependent operation fewer on the step's chain than lo + (d + sqrt(q))/2, at the price of
 // one more rounding at T's magnitude (fp32 cannot afford it: the 4096^2 field then drifts past 2e-5
-// relative; fp64 stays within the 1e-9 tolerance, tests/test_gpu_fullsize.py).
+// relative; fp64 stays within the 1e-9 tolerance, tests/test_gpu_fullsize.py).  EIK_CHAIN 2 and 3 are
+// the two fp64 forms below (one dependent operation fewer / one instruction fewer); all three ran
+// within noise on C2 (profiles/r03n_chain_variants_ab.log) -- the fp64 solve is bound by its tile
+// hops, not by the step -- and 3, the fewest instructions, is the default.
 #ifndef EIK_CHAIN
-#define EIK_CHAIN 1
+#define EIK_CHAIN 3
 #endif
 __device__ __forceinline__ float godunov2_chain(float a, float b, float c, float c2x2) {
     const float lo = umin(a, b);
@@ -163,7 +166,31 @@ __device__ __forceinline__ double godunov2_chain(double a, double b, double c, d
     double d;
     asm("v_min_f64 %0, |%1|, %2" : "=v"(d) : "v"(diff), "v"(c));
     const double q = __builtin_fma(-d, d, c2x2);
-#if EIK_CHAIN
+#if EIK_CHAIN >= 3
+    // two Newton steps from v_rsq_f64 (relative error ~2^-23 -> ~2^-47 -> ~2^-70), the second one's
+    // correction applied with the unrefined h = y/2 (its error multiplies a residual of ~2^-47):
+    // 9 instructions from q to w instead of 10, the same 6 dependent ones after v_rsq as EIK_CHAIN 1
+    const double base = __builtin_fma(0.5, d, lo);
+    const double y = __builtin_amdgcn_rsq(q);
+    const double g = q * y, h = 0.5 * y;
+    const double s1 = __builtin_fma(__builtin_fma(-g, g, q), h, g);
+    const double e2 = __builtin_fma(-s1, s1, q);
+    return __builtin_fma(0.5, __builtin_fma(e2, h, s1), base);
+#elif EIK_CHAIN >= 2
+    // sqrt_sweep's Newton correction folded into the result: w = (lo + d/2 + g1/2) + e * y/4, with
+    // lo + d/2 + g1/2 formed beside e = q - g1^2.  The correction's multiplier is the unrefined
+    // y/4 (h/2) instead of the Goldschmidt-refined h'/2: its relative error (v_rsq_f64, ~2^-23)
+    // multiplies e, itself ~2^-44 of g1, so the correction is still exact to ~2^-67 of sqrt(q).
+    // Chain after v_rsq: mul, fma, fma, fma, fma (one fewer than sqrt_sweep + the final fma), same
+    // instruction count; one more rounding at T's magnitude.
+    const double base = __builtin_fma(0.5, d, lo);
+    const double y = __builtin_amdgcn_rsq(q);
+    const double g = q * y, h = 0.5 * y, hq = 0.25 * y;
+    const double r = __builtin_fma(-h, g, 0.5);
+    const double g1 = __builtin_fma(g, r, g);
+    const double e = __builtin_fma(-g1, g1, q);
+    return __builtin_fma(e, hq, __builtin_fma(0.5, g1, base));
+#elif EIK_CHAIN
     return __builtin_fma(0.5, sqrt_sweep(q), __builtin_fma(0.5, d, lo));
 #else
     return __builtin_fma(0.5, d + sqrt_sweep(q), lo);

@@ -51,6 +51,12 @@ __device__ __forceinline__ float f4get(const float4& v, int z) { return z == 0 ?
 // 2-axis one when C^2 > (s1-s0)^2, else s0 + C.  The 1- and 2-axis cases share one form with
 // d = min(s1 - s0, C) (as godunov2_fast); the 3-axis case is selected.  A NaN from inf - inf
 // fails every comparison / sorts above +inf in the unsigned min, so +inf inputs give +inf.
+// EIK_G3_ONE_SQRT (default on): the case is selected BEFORE the square root, so each layer-update
+// takes one v_sqrt_f32 (a quarter-rate transcendental) instead of two -- the layered sweep is VALU-bound
+// at its one wave per SIMD (~100 VALU per 3-layer step).
+#ifndef EIK_G3_ONE_SQRT
+#define EIK_G3_ONE_SQRT 1
+#endif
 __device__ __forceinline__ float godunov3_fast(float a, float b, float c, float C) {
     const float lo = umin(a, b), hi = umax(a, b);
     const float mid = umin(hi, c), s2 = umax(hi, c);
@@ -58,10 +64,21 @@ __device__ __forceinline__ float godunov3_fast(float a, float b, float c, float 
     const float C2 = C * C;
     const float bp = s1 - s0, cp = s2 - s0, cb = s2 - s1;
     const float d = umin(bp, C);
+#if EIK_G3_ONE_SQRT
+    const float cc = cp * cp;
+    const bool three = C2 > __builtin_fmaf(cb, cb, cc);  // NaN (an +inf axis) -> false
+    // 2 axes: 2C^2 - d^2; 3 axes: 3C^2 - 2(bp^2 + cp^2 - bp cp), bp^2 - bp cp + cp^2 = bp (bp - cp) + cp^2
+    const float q12 = __builtin_fmaf(-d, d, C2) + C2;
+    const float q3 = __builtin_fmaf(-2.f, __builtin_fmaf(bp, bp - cp, cc), 3.f * C2);
+    const float num = three ? bp + cp : d;
+    const float k = three ? 1.f / 3.f : 0.5f;
+    return __builtin_fmaf(num + __builtin_amdgcn_sqrtf(three ? q3 : q12), k, s0);
+#else
     const float t12 = __builtin_fmaf(0.5f, d + __builtin_amdgcn_sqrtf(__builtin_fmaf(-d, d, C2) + C2), s0);
     const float q3 = 3.f * C2 - 2.f * (bp * bp + cp * cp - bp * cp);
     const float t3 = __builtin_fmaf(bp + cp + __builtin_amdgcn_sqrtf(q3), 1.f / 3.f, s0);
     return C2 > cp * cp + cb * cb ? t3 : t12;
+#endif
 }
 
 // One quadrant sweep over all NL layers (cf. sweep_quadrant in fim2d.hip; same skew, clamp and
