@@ -108,6 +108,12 @@ hipError_t max_finite(const void* cost, int64_t n, bool f64, void* d_max, hipStr
 hipError_t fim3d_init(const Fim3dArgs& a, bool f64, const int64_t* d_goals, int B, hipStream_t st);
 hipError_t fim3d_sweep(const Fim3dArgs& a, bool f64, int grid, hipStream_t st);
 void fim3d_tile_shape(int64_t L, int* tx, int* ty, int* tz);
+// persistent driver of the 3D solver (one launch per solve): q carries the tile FIFO of
+// fim_engine.hpp (qhead .. qstate, qtimeout, qbudget, visits[2]) sized for a.capacity tiles
+hipError_t fim3d_persist_init(const Fim3dArgs& a, const Fim2dArgs& q, bool f64, const int64_t* d_goals, int B,
+                              hipStream_t st);
+hipError_t fim3d_persist(const Fim3dArgs& a, const Fim2dArgs& q, bool f64, int grid, hipStream_t st);
+int fim3d_persist_resident(bool f64, int cus);
 // FastMarching3D.computeTmap's early exit at `start` (:141) from a converged field Tf into Te
 // (a separate buffer); ts_off = start's linear index, or -1 for no early exit (fim3d.hip).
 hipError_t fim3d_early(const void* cost, const void* Tf, void* Te, int64_t H, int64_t W, int64_t L, int64_t ts_off,

@@ -57,19 +57,38 @@ __device__ __forceinline__ float f4get(const float4& v, int z) { return z == 0 ?
 #ifndef EIK_G3_ONE_SQRT
 #define EIK_G3_ONE_SQRT 1
 #endif
+// Sorted triple of non-negative floats / +inf / NaN on their bit patterns: one v_min3_u32, one
+// v_med3_u32, one v_max3_u32 (the compiler's min/max network took ~9 instructions).
+__device__ __forceinline__ void sort3u(float a, float b, float c, float& s0, float& s1, float& s2) {
+    unsigned r0, r1, r2;
+    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r0) : "v"(__float_as_uint(a)), "v"(__float_as_uint(b)), "v"(__float_as_uint(c)));
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r1) : "v"(__float_as_uint(a)), "v"(__float_as_uint(b)), "v"(__float_as_uint(c)));
+    asm("v_max3_u32 %0, %1, %2, %3" : "=v"(r2) : "v"(__float_as_uint(a)), "v"(__float_as_uint(b)), "v"(__float_as_uint(c)));
+    s0 = __uint_as_float(r0);
+    s1 = __uint_as_float(r1);
+    s2 = __uint_as_float(r2);
+}
+#ifndef EIK_G3_SORT3
+#define EIK_G3_SORT3 1
+#endif
 __device__ __forceinline__ float godunov3_fast(float a, float b, float c, float C) {
+#if EIK_G3_SORT3
+    float s0, s1, s2;
+    sort3u(a, b, c, s0, s1, s2);
+#else
     const float lo = umin(a, b), hi = umax(a, b);
     const float mid = umin(hi, c), s2 = umax(hi, c);
     const float s0 = umin(lo, mid), s1 = umax(lo, mid);
+#endif
     const float C2 = C * C;
     const float bp = s1 - s0, cp = s2 - s0, cb = s2 - s1;
     const float d = umin(bp, C);
 #if EIK_G3_ONE_SQRT
-    const float cc = cp * cp;
-    const bool three = C2 > __builtin_fmaf(cb, cb, cc);  // NaN (an +inf axis) -> false
-    // 2 axes: 2C^2 - d^2; 3 axes: 3C^2 - 2(bp^2 + cp^2 - bp cp), bp^2 - bp cp + cp^2 = bp (bp - cp) + cp^2
+    const float cb2 = cb * cb;
+    const bool three = C2 > __builtin_fmaf(cp, cp, cb2);  // NaN (an +inf axis) -> false
+    // 2 axes: 2C^2 - d^2; 3 axes: 3C^2 - 2(bp^2 + cp^2 - bp cp), and bp^2 - bp cp + cp^2 = cb^2 + bp cp
     const float q12 = __builtin_fmaf(-d, d, C2) + C2;
-    const float q3 = __builtin_fmaf(-2.f, __builtin_fmaf(bp, bp - cp, cc), 3.f * C2);
+    const float q3 = __builtin_fmaf(-2.f, __builtin_fmaf(bp, cp, cb2), 3.f * C2);
     const float num = three ? bp + cp : d;
     const float k = three ? 1.f / 3.f : 0.5f;
     return __builtin_fmaf(num + __builtin_amdgcn_sqrtf(three ? q3 : q12), k, s0);

@@ -39,14 +39,21 @@ goal = fin[len(fin) // 2][[1, 0, 2]]
 print("volume", cost.shape, "goal", goal, flush=True)
 # the whole volume -> FM3D (early exit) -> path call, and its solve's share
 a = cap["args"]
-for _ in range(3):
-    t0 = time.perf_counter()
-    orig_arm_path(*a)
-    el = (time.perf_counter() - t0) * 1e3
-    s = ctx.stats()
-    print(f"arm_path wall {el:.3f} ms; its FM3D solve: device {s['solve_ms']:.3f} ms, launches {s['iterations']}, "
-          f"visits {s['tile_visits']}", flush=True)
-for se, grid in ((32, 0), (32, 64), (32, 256), (32, 512)):
+ref = None
+for mode in (L.MODE_PERSISTENT, L.MODE_LIST, L.MODE_PERSISTENT, L.MODE_LIST):
+    ctx.set_option(L.OPT_MODE, mode)
+    for _ in range(3):
+        t0 = time.perf_counter()
+        path, st = orig_arm_path(*a)
+        el = (time.perf_counter() - t0) * 1e3
+        s = ctx.stats()
+        same = ref is None or (path.shape == ref.shape and np.abs(path - ref).max() <= 1e-9)
+        ref = path if ref is None else ref
+        print(f"mode {mode}: arm_path wall {el:.3f} ms; its FM3D solve: device {s['solve_ms']:.3f} ms, launches "
+              f"{s['iterations']}, visits {s['tile_visits']}; path {len(path)} points, same as the first: {same}",
+              flush=True)
+ctx.set_option(L.OPT_MODE, L.MODE_LIST)
+for se, grid in ((32, 0), (32, 256)):
     ctx.set_option(L.OPT_SYNC_EVERY, se)
     ctx.set_option(L.OPT_GRID, grid)
     ctx.tmap3d(cost, goal)
@@ -57,3 +64,32 @@ for se, grid in ((32, 0), (32, 64), (32, 256), (32, 512)):
     s = ctx.stats()
     print(f"sync_every={se} grid={grid or 'default'}: wall {el:.3f} ms, device {s['solve_ms']:.3f} ms, launches {s['iterations']}, "
           f"visits {s['tile_visits']}", flush=True)
+Tl = ctx.tmap3d(cost, goal)
+ctx.set_option(L.OPT_MODE, L.MODE_PERSISTENT)
+ctx.set_option(L.OPT_GRID, 0)
+for _ in range(2):
+    t0 = time.perf_counter()
+    for _ in range(10):
+        Tp = ctx.tmap3d(cost, goal)
+    el = (time.perf_counter() - t0) / 10 * 1e3
+    s = ctx.stats()
+    print(f"persistent: wall {el:.3f} ms, device {s['solve_ms']:.3f} ms, visits {s['tile_visits']}", flush=True)
+fin = np.isfinite(Tl)
+print("persistent vs list field: masks equal", np.array_equal(fin, np.isfinite(Tp)), "max abs",
+      float(np.abs(Tl[fin] - Tp[fin]).max()), flush=True)
+# in-tile relaxation passes per visit (EIK_OPT_PASSES), persistent driver
+for passes in (24, 48, 24, 48):
+    ctx.set_option(L.OPT_PASSES, passes)
+    ctx.set_option(L.OPT_MODE, L.MODE_PERSISTENT)
+    ctx.tmap3d(cost, goal)
+    t0 = time.perf_counter()
+    for _ in range(10):
+        ctx.tmap3d(cost, goal)
+    el = (time.perf_counter() - t0) / 10 * 1e3
+    s = ctx.stats()
+    t1 = time.perf_counter()
+    orig_arm_path(*a)
+    el2 = (time.perf_counter() - t1) * 1e3
+    s2 = ctx.stats()
+    print(f"passes {passes}: full field wall {el:.3f} ms, device {s['solve_ms']:.3f} ms, visits {s['tile_visits']} passes {s['inplace_passes']}; "
+          f"arm_path wall {el2:.3f} ms, early-exit solve {s2['solve_ms']:.3f} ms, visits {s2['tile_visits']}", flush=True)
