@@ -18,6 +18,17 @@ def ctx():
     c.close()
 
 
+@pytest.fixture(scope="module")
+def ctx_list():
+    """The 3D solver's list driver (one launch per outer iteration); the default is persistent."""
+    import eikonal
+    from eikonal import _lib as L
+
+    c = eikonal.Context(0, options={"MODE": L.MODE_LIST})
+    yield c
+    c.close()
+
+
 def check(T, R, f64):
     fin = np.isfinite(R)
     assert np.array_equal(np.isfinite(T), fin)
@@ -60,8 +71,10 @@ def test_path3d(ctx, golden, i):
     assert path2.shape == ref.shape and np.abs(path2 - ref).max() <= 1e-9
 
 
+@pytest.mark.parametrize("driver", ["persistent", "list"])
 @pytest.mark.parametrize("shape,seed", [((200, 230, 5), 1), ((40, 44, 36), 2), ((64, 64, 3), 3), ((33, 70, 9), 4)])
-def test_vs_oracle(ctx, shape, seed):
+def test_vs_oracle(ctx, ctx_list, shape, seed, driver):
+    ctx = ctx if driver == "persistent" else ctx_list
     rng = np.random.default_rng(seed)
     c = rng.uniform(1, 4, shape)
     c[rng.random(shape) < 0.08] = np.inf
