@@ -926,8 +926,8 @@ static int fim3d_solve_persist(eik_ctx* c, Fim3dArgs a, int64_t B, int dtype, co
     HIPCHK(c, c->q3ctl.ensure(kQueueCtlBytes));
     HIPCHK(c, c->q3slot.ensure(sizeof(unsigned) * nq));
     HIPCHK(c, c->q3state.ensure(sizeof(unsigned) * tiles));
-    HIPCHK(c, c->q3vis.ensure(2 * sizeof(unsigned long long)));
-    if (!c->h_q3) HIPCHK(c, hipHostMalloc((void**)&c->h_q3, kQueueCtlBytes + 2 * sizeof(unsigned long long)));
+    HIPCHK(c, c->q3vis.ensure(3 * sizeof(unsigned long long)));  // visits, (unused) in-place, relaxation passes
+    if (!c->h_q3) HIPCHK(c, hipHostMalloc((void**)&c->h_q3, kQueueCtlBytes + 3 * sizeof(unsigned long long)));
     for (hipEvent_t& e : c->e3)
         if (!e) HIPCHK(c, hipEventCreate(&e));
     Fim2dArgs q{};
@@ -944,14 +944,14 @@ static int fim3d_solve_persist(eik_ctx* c, Fim3dArgs a, int64_t B, int dtype, co
     q.qbudget = c->max_visits ? c->max_visits : 1024ull * (unsigned long long)tiles + (1ull << 20);
     q.fresh_first = 0;
     q.qhold = nullptr;
-    a.visits = nullptr;
+    a.visits = (unsigned long long*)c->q3vis.p + 2;
     const bool f64 = dtype == EIK_F64;
     int& res = c->resident3[f64 ? 1 : 0];
     if (res == 0) res = fim3d_persist_resident(f64, c->cu_count);
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(std::min(c->grid > 0 ? c->grid : res, res), tiles));
     hipEvent_t e0 = c->e3[0], e1 = c->e3[1];
     HIPCHK(c, hipEventRecord(e0, st));
-    HIPCHK(c, hipMemsetAsync(c->q3vis.p, 0, 2 * sizeof(unsigned long long), st));
+    HIPCHK(c, hipMemsetAsync(c->q3vis.p, 0, 3 * sizeof(unsigned long long), st));
     HIPCHK(c, c->goals.ensure(sizeof(int64_t) * 3 * B));
     HIPCHK(c, hipMemcpyAsync(c->goals.p, goals, sizeof(int64_t) * 3 * B, hipMemcpyHostToDevice, st));
     HIPCHK(c, fim3d_persist_init(a, q, f64, (const int64_t*)c->goals.p, (int)B, st));
@@ -960,7 +960,7 @@ static int fim3d_solve_persist(eik_ctx* c, Fim3dArgs a, int64_t B, int dtype, co
     unsigned* hq = c->h_q3;
     unsigned long long* hv = (unsigned long long*)((char*)hq + kQueueCtlBytes);
     HIPCHK(c, hipMemcpyAsync(hq, c->q3ctl.p, kQueueCtlBytes, hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipMemcpyAsync(hv, c->q3vis.p, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(hv, c->q3vis.p, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));
     const unsigned err = hq[192 / 4];
     if (err & 1u)
@@ -974,7 +974,7 @@ static int fim3d_solve_persist(eik_ctx* c, Fim3dArgs a, int64_t B, int dtype, co
     c->last.iterations = 1;
     c->last.host_syncs = 1;
     c->last.tile_visits = (int64_t)hv[0];
-    c->last.inplace_passes = (int64_t)hv[1];  // 3D: relaxation passes summed over the visits
+    c->last.inplace_passes = (int64_t)hv[2];  // 3D: relaxation passes summed over the visits
     c->last.solve_ms = ms;
     c->last.bytes_alg = (double)hv[0] * (f64 ? 8 : 4) * 3.0 * a.tx * a.ty * a.tz;
     return EIK_OK;

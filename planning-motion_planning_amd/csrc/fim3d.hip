@@ -282,7 +282,8 @@ __global__ __launch_bounds__(256) void fim3d_sweep_kernel(Fim3dArgs a) {
 }
 
 // PERSISTENT driver (cf. fim2dl_persist_kernel): one launch per solve; workgroups take tiles from
-// the device FIFO of fim_engine.hpp (q carries its queue words; q.visits[0] counts visits) and a
+// the device FIFO of fim_engine.hpp (q carries its queue words; q.visits[0] counts visits, a.visits
+// the relaxation passes) and a
 // visit's face activations queue the neighbours into the running launch.  A tile whose last pass
 // still changed it (pass cap) re-queues itself through its state word, as a busy tile activated by
 // a neighbour does; the solve ends when no tile is pending or busy.
@@ -300,7 +301,8 @@ __global__ __launch_bounds__(256) void fim3d_persist_kernel(Fim3dArgs a, Fim2dAr
                     if (((f >> threadIdx.x) & 1u) && nb >= 0) qpush(q, nb, kSelf);
                 }
                 if (threadIdx.x == 6 && (f & 128u)) atomicOr(&q.qstate[tile], kPending | kSelf);
-                if (threadIdx.x == 7) atomicAdd(q.visits + 1, (unsigned long long)L.passes);
+                // relaxation passes (stats) in the 3D args' counter: q.visits[1] is part of the budget
+                if (threadIdx.x == 7 && a.visits) atomicAdd(a.visits, (unsigned long long)L.passes);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __builtin_amdgcn_wave_barrier();
                 if (threadIdx.x == 0) {
