@@ -287,7 +287,7 @@ def main():
         xs = {
             f"C2_{other}": lambda: bench_c2(ctx, dev, stream, cost, goal_g, args.extra_steps, other),
             "C3": lambda: bench_batch(ctx, dev, stream, args.extra_steps, tdt, edt),
-            "C5": lambda: bench_layers(ctx, dev, stream, cost.float(), goal_g, args.extra_steps),
+            "C5": lambda: bench_layers(ctx, dev, stream, cost.to(tdt), goal_g, args.extra_steps),
             "costmap": lambda: bench_costmap(ctx, dev, stream, args.extra_steps, goal_g),
             "C4_1gpu": lambda: bench_c4(ctx, dev, stream, max(2, args.extra_steps // 2), tdt, edt),
             "arm": lambda: bench_arm(ctx, args.extra_steps),
@@ -295,8 +295,10 @@ def main():
         if f64:
             xs["C4_1gpu_f32"] = lambda: bench_c4(ctx, dev, stream, max(2, args.extra_steps // 2), torch.float32,
                                                  L.EIK_F32)
+            xs["C5_f32"] = lambda: bench_layers(ctx, dev, stream, cost.float(), goal_g, args.extra_steps)
         out["extra_configs"] = {k: fn() for k, fn in xs.items()
-                                if want is None or k in want or (k.startswith("C2_") and "C2_other" in want)}
+                                if want is None or k in want or (k.startswith("C2_") and "C2_other" in want)
+                                or (k == "C5_f32" and "C5" in want)}
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cost, goal_g)
@@ -502,9 +504,11 @@ def bench_layers(ctx, dev, stream, cost2d, goal, steps, Lz=3):
     T = torch.empty_like(cost)
     Lm = Lz + 2
     g3 = np.array([goal[0], goal[1], 1], np.int64)
+    f64 = cost.dtype == torch.float64
+    edt = L.EIK_F64 if f64 else L.EIK_F32
 
     def solve():
-        ctx._chk(L.lib().eik_fim3d_solve(ctx._h, cost.data_ptr(), T.data_ptr(), H, W, Lm, L.EIK_F32, g3,
+        ctx._chk(L.lib().eik_fim3d_solve(ctx._h, cost.data_ptr(), T.data_ptr(), H, W, Lm, edt, g3,
                                          stream.cuda_stream))
 
     sec = timed_loop(solve, steps)
@@ -520,7 +524,7 @@ def bench_layers(ctx, dev, stream, cost2d, goal, steps, Lz=3):
     st_d = torch.zeros(1, dtype=torch.int32, device=dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
-    ctx._chk(L.lib().eik_path3d_dev(ctx._h, T.data_ptr(), L.EIK_F32, H, W, Lm, np.array([256.0, 256.0, 1.0]),
+    ctx._chk(L.lib().eik_path3d_dev(ctx._h, T.data_ptr(), edt, H, W, Lm, np.array([256.0, 256.0, 1.0]),
                                     np.array([float(goal[0]), float(goal[1]), 1.0]), 0.5, out_d.data_ptr(), cap,
                                     n_d.data_ptr(), st_d.data_ptr(), stream.cuda_stream))
     e1.record(stream)
@@ -528,23 +532,24 @@ def bench_layers(ctx, dev, stream, cost2d, goal, steps, Lz=3):
     res = {"workload": f"configs[4]: coupled {H}x{W}x{Lz} layered costmap (x, y, locomotion mode), FM3D semantics, "
                        f"z padded with +inf layers ({Lm} in memory)",
            "reached_fraction": round(float(torch.isfinite(T[:, :, 1:1 + Lz]).float().mean()), 4),
-           "dtype": "f32", "solve_ms_device": round(st.get("solve_ms", 0.0), 4),
+           "dtype": "f64" if f64 else "f32", "solve_ms_device": round(st.get("solve_ms", 0.0), 4),
            "value": round(H * W * Lz / sec / 1e9, 4), "unit": "Gcells/s", "ms_per_step": round(sec * 1e3, 4),
            "steps": steps, "launches_per_solve": st.get("iterations"), "tile_visits_per_solve": st.get("tile_visits"),
            "path_ms_device": round(e0.elapsed_time(e1), 3), "path_points": int(n_d.item()),
            "path_status": int(st_d.item())}
-    # roofline of fim2dl_persist_kernel<3> (algorithmic bytes: 4 B x 3 layers per cell of cost read,
-    # T read and T write per full visit + halo, T write + halo per in-place pass)
+    # roofline of fim2dl_persist_kernel<R, 3> (algorithmic bytes: sizeof(R) x 3 layers per cell of cost
+    # read, T read and T write per full visit + halo, T write + halo per in-place pass)
     ms_k = float(np.mean(ms_l))
     ach = st["bytes_alg"] / (ms_k * 1e-3) / 1e9 if ms_k > 0 else None
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic_c5.json")
+    pmc = os.path.join(ROOT, "profiles", f"pmc_traffic_c5{'_f64' if f64 else ''}.json")
     if os.path.exists(pmc):
         try:
             traffic = json.load(open(pmc)).get("bytes_per_launch")
         except Exception:
             traffic = None
-    res["roofline"] = {"bound": "hbm", "kernel": f"fim2dl_persist_kernel<{Lz}>", "achieved": round(ach, 2) if ach else None,
+    res["roofline"] = {"bound": "hbm", "kernel": f"fim2dl_persist_kernel<{'double' if f64 else 'float'}, {Lz}>",
+                       "achieved": round(ach, 2) if ach else None,
                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None,
                        "traffic": traffic, "alg_bytes_per_launch": round(st["bytes_alg"]),
                        "avg_launch_us": round(ms_k * 1e3, 2), "inplace_passes_per_solve": st.get("inplace_passes")}

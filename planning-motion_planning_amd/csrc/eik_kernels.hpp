@@ -74,12 +74,15 @@ int fim2d_persist_resident(bool f64, int cus, bool wide = false);
 hipError_t fim2d_merge_ghost(const Fim2dArgs& a, bool f64, int side, const void* recv, int64_t len, hipStream_t st);
 hipError_t fim2d_pack_edges(const Fim2dArgs& a, bool f64, void* n, void* s, void* w, void* e, hipStream_t st);
 
-// Layered solver (fim2dl.hip): a [H][W][ls] fp32 volume, layers z0 .. z0+nl-1 (nl <= 4), on the
-// 2D tile engine (persistent mode only; a.ls / a.z0 set, no ghosts, no ordering window).
-hipError_t fim2dl_init(const Fim2dArgs& a, int64_t gx, int64_t gy, int64_t gz, hipStream_t st);
-hipError_t fim2dl_persist(const Fim2dArgs& a, int nl, int grid, hipStream_t st);
-int fim2dl_persist_resident(int nl, int cus);
-hipError_t layer_finite(const float* cost, int64_t hw, int64_t L, int64_t z, int* d_flag, hipStream_t st);
+// Layered solver (fim2dl.hip): a [H][W][ls] volume, layers z0 .. z0+nl-1 (fp32: nl <= 4, tiles of
+// 64 x 64; fp64: nl <= 3, tiles of fim2dl_rows(true) = 40 rows x 64 columns), on the 2D tile engine
+// (persistent mode only; a.ls / a.z0 set, no ghosts, no ordering window; a.nty counts tiles of
+// fim2dl_rows(f64) rows).
+int fim2dl_rows(bool f64);
+hipError_t fim2dl_init(const Fim2dArgs& a, bool f64, int64_t gx, int64_t gy, int64_t gz, hipStream_t st);
+hipError_t fim2dl_persist(const Fim2dArgs& a, int nl, bool f64, int grid, hipStream_t st);
+int fim2dl_persist_resident(int nl, bool f64, int cus);
+hipError_t layer_finite(const void* cost, bool f64, int64_t hw, int64_t L, int64_t z, int* d_flag, hipStream_t st);
 
 // 3D FIM over one H x W x L volume ([y][x][z], FastMarching3D.py layout).
 struct Fim3dArgs {

@@ -72,11 +72,12 @@ struct eik_ctx {
     int grid = 0;
     eik_stats last{};
     eik_fim2d* cached = nullptr;  // solver reused by the host-buffer entry points
-    eik_fim2d* cached_l = nullptr;  // queue state of the layered 3D solver (fim2dl.hip)
+    eik_fim2d* cached_l = nullptr;  // queue state of the layered 3D solver (fim2dl.hip), fp32 tiles
+    eik_fim2d* cached_l64 = nullptr;  // the same for the fp64 layered solver's 40-row tiles
     eik_fim2d* cached_fill = nullptr;  // reachability solver of the cost builder's hole filling
     DevBuf cm_u8, cm_i32, cm_f32, cm_f64;  // cost-builder scratch
     DevBuf arm;                            // end-effector volume scratch (arm.hip)
-    int resident_l[5] = {0, 0, 0, 0, 0};  // co-resident workgroups of fim2dl_persist_kernel<nl>
+    int resident_l[2][5] = {};  // co-resident workgroups of fim2dl_persist_kernel<R, nl> (f32, f64)
     DevBuf cost, T, T2, goals, work, misc;
     DevBuf l3, c3, m3, v3;             // 3D solver scratch (lists, counts, marks, visits)
     int max_passes3 = 24;
@@ -168,6 +169,7 @@ void eik_destroy(eik_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->cached) eik_fim2d_destroy(c->cached);
     if (c->cached_l) eik_fim2d_destroy(c->cached_l);
+    if (c->cached_l64) eik_fim2d_destroy(c->cached_l64);
     if (c->cached_fill) eik_fim2d_destroy(c->cached_fill);
     if (c->h3) (void)hipHostFree(c->h3);
     if (c->h_q3) (void)hipHostFree(c->h_q3);
@@ -210,12 +212,13 @@ int eik_get_stats(const eik_ctx* c, eik_stats* out) {
 }
 
 // ------------------------------------------------------------------------------ fim2d
-int eik_fim2d_create(eik_ctx* c, int64_t B, int64_t H, int64_t W, int dtype, eik_fim2d** out) {
+// th: tile rows (64; the fp64 layered solver's tiles have fim2dl_rows(true) = 40)
+static int fim2d_create_rows(eik_ctx* c, int64_t B, int64_t H, int64_t W, int dtype, int th, eik_fim2d** out) {
     if (!c || !out) return EIK_ERR_ARG;
     *out = nullptr;
     if (B < 1 || H < 1 || W < 1) return set_err(c, EIK_ERR_ARG, "bad shape B=%ld H=%ld W=%ld", (long)B, (long)H, (long)W);
     if (dtype != EIK_F32 && dtype != EIK_F64) return set_err(c, EIK_ERR_ARG, "bad dtype %d", dtype);
-    const int64_t ntx = (W + kTile - 1) / kTile, nty = (H + kTile - 1) / kTile;
+    const int64_t ntx = (W + kTile - 1) / kTile, nty = (H + th - 1) / th;
     const int64_t tiles = B * ntx * nty;
     if (tiles >= (1ll << 31) - 8) return set_err(c, EIK_ERR_ARG, "too many tiles");
     HIPCHK(c, hipSetDevice(c->device));
@@ -274,6 +277,10 @@ int eik_fim2d_create(eik_ctx* c, int64_t B, int64_t H, int64_t W, int dtype, eik
     f->max_iters = 64 * (ntx + nty) + 8 * tiles / B + 4096;
     *out = f;
     return EIK_OK;
+}
+
+int eik_fim2d_create(eik_ctx* c, int64_t B, int64_t H, int64_t W, int dtype, eik_fim2d** out) {
+    return fim2d_create_rows(c, B, H, W, dtype, kTile, out);
 }
 
 void eik_fim2d_destroy(eik_fim2d* f) {
@@ -833,14 +840,17 @@ int eik_path2d_f64(eik_ctx* c, const double* T, int64_t H, int64_t W, const doub
 // Few-layer fp32 volumes (the rover's (x, y, mode) costmaps) on the layered 2D-tile solver:
 // layers z0 .. z0+nl-1 of a [H][W][L] volume, one persistent launch.
 static int solve_layered(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, int64_t W, int64_t L, int z0, int nl,
-                         const int64_t goal[3], hipStream_t st) {
-    eik_fim2d* f = c->cached_l;
+                         const int64_t goal[3], int dtype, hipStream_t st) {
+    const bool f64 = dtype == EIK_F64;
+    const int th = fim2dl_rows(f64);
+    eik_fim2d*& slot = f64 ? c->cached_l64 : c->cached_l;
+    eik_fim2d* f = slot;
     if (!f || f->H != H || f->W != W) {
         if (f) eik_fim2d_destroy(f);
-        c->cached_l = nullptr;
-        int rc = eik_fim2d_create(c, 1, H, W, EIK_F32, &f);
+        slot = nullptr;
+        int rc = fim2d_create_rows(c, 1, H, W, dtype, th, &f);
         if (rc) return rc;
-        c->cached_l = f;
+        slot = f;
     }
     Fim2dArgs a = f->a;
     a.cost = d_cost;
@@ -857,13 +867,14 @@ static int solve_layered(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, i
     // C5 A/B (profiles/r02a_c5_passes.log): 8 / 16 / 24 passes 15.5-16.3 / 13.9 / 12.9 ms
     a.max_passes = c->passes > 0 ? c->passes : 24;
     a.qbudget = c->max_visits ? c->max_visits : 1024ull * (unsigned long long)a.tiles_per_map + (1ull << 20);
-    if (c->resident_l[nl] == 0) c->resident_l[nl] = fim2dl_persist_resident(nl, c->cu_count);
-    const int grid = std::min(c->grid > 0 ? c->grid : 4 * c->cu_count, c->resident_l[nl]);
+    int& res = c->resident_l[f64 ? 1 : 0][nl];
+    if (res == 0) res = fim2dl_persist_resident(nl, f64, c->cu_count);
+    const int grid = std::min(c->grid > 0 ? c->grid : 4 * c->cu_count, res);
     a.fresh_first = c->fresh_first;
     HIPCHK(c, hipEventRecord(f->ev_start, st));
     HIPCHK(c, hipMemsetAsync(f->visits.p, 0, 2 * sizeof(unsigned long long), st));
-    HIPCHK(c, fim2dl_init(a, goal[0], goal[1], goal[2], st));
-    HIPCHK(c, fim2dl_persist(a, nl, grid, st));
+    HIPCHK(c, fim2dl_init(a, f64, goal[0], goal[1], goal[2], st));
+    HIPCHK(c, fim2dl_persist(a, nl, f64, grid, st));
     HIPCHK(c, hipEventRecord(f->ev_stop, st));
     HIPCHK(c, hipMemcpyAsync(f->h_q, f->qctl.p, kQueueCtlBytes, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipMemcpyAsync(f->h_visits, f->visits.p, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
@@ -882,30 +893,35 @@ static int solve_layered(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, i
     c->last.inplace_passes = (int64_t)f->h_visits[1];
     c->last.host_syncs = 1;
     c->last.solve_ms = ms;
-    c->last.bytes_alg = 4.0 * nl *
-                        ((double)c->last.tile_visits * (3 * kTile * kTile + 4 * kTile) +
-                         (double)c->last.inplace_passes * (kTile * kTile + 4 * kTile)) +
-                        4.0 * H * W * L;
+    // per visit: cost + T read and T write of the tile's nl layers plus the halo ring; per in-place
+    // pass: T write + halo
+    const double esz = f64 ? 8.0 : 4.0;
+    c->last.bytes_alg = esz * nl *
+                        ((double)c->last.tile_visits * (3.0 * kTile * th + 2.0 * (kTile + th)) +
+                         (double)c->last.inplace_passes * (1.0 * kTile * th + 2.0 * (kTile + th))) +
+                        esz * H * W * L;
     return EIK_OK;
 }
 
-// Layers [z0, z0 + nl) of an fp32 volume the layered solver can take, or nl = 0: L <= 4 layers,
-// or L <= 6 whose first and last layers are entirely +inf (the reference's z padding).
-static int layered_plan(eik_ctx* c, const void* d_cost, int64_t H, int64_t W, int64_t L, hipStream_t st, int* z0,
-                        int* nl) {
+// Layers [z0, z0 + nl) of a volume the layered solver can take, or nl = 0: L <= kmax layers (fp32 4,
+// fp64 3), or L <= kmax + 2 whose first and last layers are entirely +inf (the reference's z padding).
+static int layered_plan(eik_ctx* c, const void* d_cost, int64_t H, int64_t W, int64_t L, int dtype, hipStream_t st,
+                        int* z0, int* nl) {
+    const bool f64 = dtype == EIK_F64;
+    const int kmax = f64 ? 3 : 4;
     *z0 = 0;
     *nl = 0;
-    if (L <= 4) {
+    if (L <= kmax) {
         *nl = (int)L;
         return EIK_OK;
     }
-    if (L > 6) return EIK_OK;
+    if (L > kmax + 2) return EIK_OK;
     HIPCHK(c, c->misc.ensure(64));
     int* d_flag = (int*)c->misc.p;
     int h_flag = 0;
     HIPCHK(c, hipMemsetAsync(d_flag, 0, sizeof(int), st));
-    HIPCHK(c, layer_finite((const float*)d_cost, H * W, L, 0, d_flag, st));
-    HIPCHK(c, layer_finite((const float*)d_cost, H * W, L, L - 1, d_flag, st));
+    HIPCHK(c, layer_finite(d_cost, f64, H * W, L, 0, d_flag, st));
+    HIPCHK(c, layer_finite(d_cost, f64, H * W, L, L - 1, d_flag, st));
     HIPCHK(c, hipMemcpyAsync(&h_flag, d_flag, sizeof(int), hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));
     if (h_flag == 0) {
@@ -1081,12 +1097,17 @@ static int fim3d_solve_one(eik_ctx* c, const void* d_cost, void* d_T, int64_t H,
         return set_err(c, EIK_ERR_ARG, "goal (%ld,%ld,%ld) outside %ldx%ldx%ld", (long)goal[0], (long)goal[1],
                        (long)goal[2], (long)H, (long)W, (long)L);
     HIPCHK(c, hipSetDevice(c->device));
-    if (dtype == EIK_F32 && c->mode == kModePersistent && c->max_rounds == 1 && H * W * L * 4 < (int64_t)UINT32_MAX) {
+    // few-layer volumes (the rover's (x, y, mode) costmaps, C5): the layered solver, fp32 and fp64
+    const int64_t esz = dtype == EIK_F64 ? 8 : 4;
+    // (an fp64 early-exit solve stays on fim3d.hip: its solve3_ref keeps the reference's exact ties,
+    // which decide FM3D's closed set)
+    if (c->mode == kModePersistent && c->max_rounds == 1 && H * W * L * esz < (int64_t)UINT32_MAX &&
+        !(stop_off >= 0 && dtype == EIK_F64)) {
         int z0 = 0, nl = 0;
-        int rc = layered_plan(c, d_cost, H, W, L, st, &z0, &nl);
+        int rc = layered_plan(c, d_cost, H, W, L, dtype, st, &z0, &nl);
         if (rc) return rc;
         if (nl > 0 && goal[2] >= z0 && goal[2] < z0 + nl) {
-            return solve_layered(c, d_cost, d_T, H, W, L, z0, nl, goal, st);
+            return solve_layered(c, d_cost, d_T, H, W, L, z0, nl, goal, dtype, st);
         }
     }
     return fim3d_solve_batch(c, d_cost, d_T, 1, H, W, L, dtype, goal, st, stop_off);

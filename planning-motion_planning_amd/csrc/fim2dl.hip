@@ -26,25 +26,51 @@
 
 namespace eik {
 
-constexpr int kMaxLayers = 4;  // float4 per cell in LDS
+constexpr int kMaxLayers = 4;  // float4 per cell in LDS (fp32); 3 doubles per cell (fp64)
 
+// A cell's layers in LDS: fp32 one float4 (one ds_read_b128 fetches every layer; unused slots
+// +inf), fp64 three doubles (NL <= 3: the 155 KB tile of 40 rows below fits the 160 KB LDS).
+template <typename R> struct LCell;
+template <> struct LCell<float> {
+    float4 v;
+    __device__ __forceinline__ float get(int z) const { return z == 0 ? v.x : z == 1 ? v.y : z == 2 ? v.z : v.w; }
+    static __device__ __forceinline__ LCell make(const float (&x)[4]) { return LCell{make_float4(x[0], x[1], x[2], x[3])}; }
+};
+template <> struct LCell<double> {
+    double v[3];
+    __device__ __forceinline__ double get(int z) const { return v[z]; }
+    static __device__ __forceinline__ LCell make(const double (&x)[4]) { return LCell{{x[0], x[1], x[2]}}; }
+};
+template <typename R> constexpr int kLayersOf = sizeof(R) == 4 ? 4 : 3;
+// tile rows: 64 (fp32, 156 KB of LDS) or EIK_L64_ROWS (fp64; 40 rows: (40 + 2 + 8 guard) x 66 cells x
+// 48 B = 155 KB, the most that fits 160 KB with a step count divisible by the read-ahead depth);
+// always 64 columns (one lane each)
+#ifndef EIK_L64_ROWS
+#define EIK_L64_ROWS 40
+#endif
+template <typename R> constexpr int kRowsOf = sizeof(R) == 4 ? kTile : EIK_L64_ROWS;
+
+template <typename R, int TH>
 struct TileLdsL {
-    float4 Tbuf[(kLds + 2 * kGuard) * kLds];  // tile + halo ring (66 x 66 at offset kGuard * kLds), guard rows
-                                              // above and below (fim2d.hip's sweep_quadrant)
-    float4 Cbuf[(kLds + 2 * kGuard) * kLds];  // costs in the same layout; halo ring and guard rows = +inf
+    LCell<R> Tbuf[(TH + 2 + 2 * kGuard) * kLds];  // tile + halo ring ((TH+2) x 66 at offset kGuard * kLds), guard
+                                                  // rows above and below (fim2d.hip's sweep_quadrant)
+    LCell<R> Cbuf[(TH + 2 + 2 * kGuard) * kLds];  // costs in the same layout; halo ring and guard rows = +inf
     unsigned flags;
     unsigned key[5];
     int tile;
     unsigned dirs;
 };
-// A sweep's 4-step group spans rows [-(kAhead - 1), kLds - 1 + kAhead - 1]: every row it reads (T
+// A sweep's 4-step group spans rows [-(kAhead - 1), TH + 1 + kAhead - 1]: every row it reads (T
 // and cost alike) is inside the guard rows of both arrays, and a guard row's +inf cost keeps its T
 // at +inf (the Godunov update of an infinite cost never lowers a cell).
 static_assert(kGuard >= kAhead - 1, "guard rows must cover a group's overshoot");
-static_assert(offsetof(TileLdsL, Cbuf) == sizeof(float4) * (kLds + 2 * kGuard) * kLds, "Cbuf must follow Tbuf");
-static_assert(sizeof(TileLdsL) <= 160 * 1024, "one layered tile per CU (160 KB LDS)");
-
-__device__ __forceinline__ float f4get(const float4& v, int z) { return z == 0 ? v.x : z == 1 ? v.y : z == 2 ? v.z : v.w; }
+using TileLdsL32 = TileLdsL<float, kTile>;
+using TileLdsL64 = TileLdsL<double, EIK_L64_ROWS>;
+static_assert(offsetof(TileLdsL32, Cbuf) == sizeof(float4) * (kTile + 2 + 2 * kGuard) * kLds, "Cbuf must follow Tbuf");
+static_assert(offsetof(TileLdsL64, Cbuf) == 24 * (EIK_L64_ROWS + 2 + 2 * kGuard) * kLds, "Cbuf must follow Tbuf");
+static_assert(EIK_L64_ROWS % 4 == 0 && EIK_L64_ROWS <= kTile, "fp64 tile rows: whole rows per thread, <= 64");
+static_assert(sizeof(TileLdsL<float, kTile>) <= 160 * 1024, "one layered fp32 tile per CU (160 KB LDS)");
+static_assert(sizeof(TileLdsL64) <= 160 * 1024, "one layered fp64 tile per CU (160 KB LDS)");
 
 // n-D Godunov of FastMarching3D.py:59-75 on the axis minima a, b, c (non-negative or +inf, never
 // NaN): sorted s0 <= s1 <= s2, the 3-axis solution when C^2 > (s2-s0)^2 + (s2-s1)^2, else the
@@ -99,36 +125,75 @@ __device__ __forceinline__ float godunov3_fast(float a, float b, float c, float 
     return C2 > cp * cp + cb * cb ? t3 : t12;
 #endif
 }
+// fp64 (the reference's precision): the same select-before-one-square-root form.  The minima are
+// IEEE minNum / maxNum (v_min_f64 / v_max_f64: a NaN operand yields the other; the inputs are
+// never NaN), the square root is the range-free two-Newton sequence of the 2D fp64 step
+// (eik_common.hpp godunov2_chain, EIK_CHAIN 3): q >= C^2 in both cases (3 axes: C^2 > cp^2 + cb^2
+// gives q3 > C^2) and the staged costs are >= 2^-500, so q >= 2^-1000; C = +inf gives NaN (no update).
+__device__ __forceinline__ double fmax_nn(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double godunov3_fast(double a, double b, double c, double C) {
+    const double lo = fmin_nn(a, b), hi = fmax_nn(a, b);
+    const double s0 = fmin_nn(lo, c), s2 = fmax_nn(hi, c), s1 = fmin_nn(hi, fmax_nn(lo, c));
+    const double C2 = C * C;
+    const double bp = s1 - s0, cp = s2 - s0, cb = s2 - s1;
+    const double d = fmin_nn(bp, C);  // NaN bp (all +inf) -> C
+    const double cb2 = cb * cb;
+    const bool three = C2 > __builtin_fma(cp, cp, cb2);
+    const double q12 = __builtin_fma(-d, d, C2) + C2;
+    const double q3 = __builtin_fma(-2.0, __builtin_fma(bp, cp, cb2), 3.0 * C2);
+    const double num = three ? bp + cp : d;
+    const double k = three ? 1.0 / 3.0 : 0.5;
+    const double q = three ? q3 : q12;
+    const double y = __builtin_amdgcn_rsq(q);
+    const double g = q * y, h = 0.5 * y;
+    const double s1n = __builtin_fma(__builtin_fma(-g, g, q), h, g);
+    const double r = __builtin_fma(__builtin_fma(-s1n, s1n, q), h, s1n);
+    return __builtin_fma(num + r, k, s0);
+}
+
+// Lane l-1's fresh value for lanes 1.. (DPP wave shift), lane 0's from LDS (the halo column).
+// fp32: the prefetched LDS value of the same cell is a valid, possibly lower, bound too -- one
+// v_min_u32_dpp takes both; fp64: the DPP value alone (as fim2d.hip's fp64 sweep).
+__device__ __forceinline__ float upstream_x(float cur, float lds) { return umin(wave_shr1_umin_id(cur), lds); }
+__device__ __forceinline__ double upstream_x(double cur, double lds) { return wave_shr1(cur, lds); }
+__device__ __forceinline__ float min_nn(float a, float b) { return umin(a, b); }
+__device__ __forceinline__ double min_nn(double a, double b) { return fmin_nn(a, b); }
 
 // One quadrant sweep over all NL layers (cf. sweep_quadrant in fim2d.hip; same skew, clamp and
-// read-ahead, float4 cells, and the same upstream-only x/y neighbours: the four concurrent sweeps
-// cover every x/y neighbour pair and the n-D update is monotone, so the fixed point is the one of
-// reading both neighbours per axis -- 3 float4 LDS reads per step instead of 5).
-template <int NL, int DX, int DY>
-__device__ __forceinline__ void sweep_layered(float4* __restrict__ Ts, int lane) {
-    constexpr float INF = __builtin_inff();
-    constexpr int S = (int)sizeof(float4);
+// read-ahead, one LDS cell per neighbour, and the same upstream-only x/y neighbours: the four
+// concurrent sweeps cover every x/y neighbour pair and the n-D update is monotone, so the fixed
+// point is the one of reading both neighbours per axis -- 3 cell reads per step instead of 5).
+// TH tile rows: TH + 64 skewed steps.
+template <typename R, int TH, int NL, int DX, int DY>
+__device__ __forceinline__ void sweep_layered(LCell<R>* __restrict__ Ts, int lane) {
+    constexpr R INF = Real<R>::inf();
+    constexpr int S = (int)sizeof(LCell<R>);
     constexpr int kRow = kLds * S;
-    constexpr int kCsB = (kLds + 2 * kGuard) * kLds * S;  // Cs - Ts in bytes (Cbuf - Tbuf)
+    constexpr int kCsB = (TH + 2 + 2 * kGuard) * kLds * S;  // Cs - Ts in bytes (Cbuf - Tbuf)
     constexpr int D = kAhead;
+    static_assert((TH + kTile) % D == 0, "pipeline depth must divide the step count");
     char* const base = reinterpret_cast<char*>(Ts);
-    auto ld = [&](int off) { return *reinterpret_cast<const float4*>(base + off); };
+    auto ld = [&](int off) { return *reinterpret_cast<const LCell<R>*>(base + off); };
     const int col = (DX > 0 ? lane : kTile - 1 - lane) + 1;
-    // the LDS row is clamped once per group of D steps (its lowest row into [-(D - 1), 65]) and the
-    // group's steps are immediate offsets from it, as in fim2d.hip's sweep_quadrant
-    const int lo_b = -(D - 1) * kRow + col * S, hi_b = (kLds - 1) * kRow + col * S;
-    int raw = DY > 0 ? (1 - lane) * kRow + col * S : (kTile - (D - 1) + lane) * kRow + col * S;
+    // the LDS row is clamped once per group of D steps (its lowest row into [-(D - 1), TH + 1]) and
+    // the group's steps are immediate offsets from it, as in fim2d.hip's sweep_quadrant
+    const int lo_b = -(D - 1) * kRow + col * S, hi_b = (TH + 1) * kRow + col * S;
+    int raw = DY > 0 ? (1 - lane) * kRow + col * S : (TH - (D - 1) + lane) * kRow + col * S;
     auto off = [](int u) { return (DY > 0 ? u : D - 1 - u) * kRow; };
     auto clampb = [&](int x) {
         int r;
         asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo_b), "v"(hi_b));
         return r;
     };
-    const float4 h = ld((DY > 0 ? 0 : kLds - 1) * kRow + col * S);
-    float cur[NL];
+    const LCell<R> h = ld((DY > 0 ? 0 : TH + 1) * kRow + col * S);
+    R cur[NL];
 #pragma unroll
-    for (int z = 0; z < NL; ++z) cur[z] = f4get(h, z);
-    float4 q_old[D], q_upx[D], q_c[D];
+    for (int z = 0; z < NL; ++z) cur[z] = h.get(z);
+    LCell<R> q_old[D], q_upx[D], q_c[D];
     int gb = clampb(raw);  // lowest row of the group being fetched
     raw += DY * D * kRow;
     auto fetch = [&](int u) {
@@ -139,22 +204,21 @@ __device__ __forceinline__ void sweep_layered(float4* __restrict__ Ts, int lane)
     };
 #pragma unroll
     for (int u = 0; u < D; ++u) fetch(u);
-    for (int s = 0; s < 2 * kTile; s += D) {
+    for (int s = 0; s < TH + kTile; s += D) {
         const int gcur = gb;
         gb = clampb(raw);
         raw += DY * D * kRow;
 #pragma unroll
         for (int u = 0; u < D; ++u) {
-            float* const cell = reinterpret_cast<float*>(base + gcur + off(u));
+            R* const cell = reinterpret_cast<R*>(base + gcur + off(u));
 #pragma unroll
             for (int z = 0; z < NL; ++z) {
-                const float old = f4get(q_old[u], z);
-                // lanes 1..: lane l-1's fresh value, or the (possibly lower) LDS one; lane 0: halo column
-                const float ux = umin(wave_shr1_umin_id(cur[z]), f4get(q_upx[u], z));
-                const float tz = umin(z > 0 ? f4get(q_old[u], z - 1) : INF, z + 1 < NL ? f4get(q_old[u], z + 1) : INF);
-                const float w = godunov3_fast(ux, cur[z], tz, f4get(q_c[u], z));
+                const R old = q_old[u].get(z);
+                const R ux = upstream_x(cur[z], q_upx[u].get(z));
+                const R tz = min_nn(z > 0 ? q_old[u].get(z - 1) : INF, z + 1 < NL ? q_old[u].get(z + 1) : INF);
+                const R w = godunov3_fast(ux, cur[z], tz, q_c[u].get(z));
                 lds_min(cell + z, w);
-                cur[z] = umin(w, old);
+                cur[z] = min_nn(w, old);  // NaN w (no update) keeps old
             }
             fetch(u);
             __builtin_amdgcn_sched_barrier(0);
@@ -163,128 +227,141 @@ __device__ __forceinline__ void sweep_layered(float4* __restrict__ Ts, int lane)
 }
 
 // Stage, sweep and write back one layered tile (cf. process_tile in fim2d.hip).  Thread t owns
-// cells t + 256 j (j < 16): row (t >> 6) + 4 j, column t & 63 -- a wave reads whole tile rows,
-// i.e. 64 * ls contiguous floats per layer load.  Leaves L.flags (bits 0..3: neighbour N/S/W/E
+// cells t + 256 j (j < TH / 4): row (t >> 6) + 4 j, column t & 63 -- a wave reads whole tile rows,
+// i.e. 64 * ls contiguous values per layer load.  Leaves L.flags (bits 0..3: neighbour N/S/W/E
 // can improve; 128: some cell decreased by more than the tolerance).
-template <int NL, bool COH>
-__device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int tile, TileLdsL& L, float keep) {
-    constexpr float INF = __builtin_inff();
-    const float4 INF4 = make_float4(INF, INF, INF, INF);
-    float4* const Ts = L.Tbuf + kGuard * kLds;
-    float4* const Cs = L.Cbuf + kGuard * kLds;
+template <typename R, int NL, bool COH>
+__device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int tile, TileLdsL<R, kRowsOf<R>>& L,
+                                                     float keep) {
+    constexpr int TH = kRowsOf<R>;
+    constexpr int NJ = TH / 4;  // cells per thread
+    constexpr int NZ = kLayersOf<R>;
+    constexpr R INF = Real<R>::inf();
+    const R INFS[4] = {INF, INF, INF, INF};
+    const LCell<R> INFC = LCell<R>::make(INFS);
+    LCell<R>* const Ts = L.Tbuf + kGuard * kLds;
+    LCell<R>* const Cs = L.Cbuf + kGuard * kLds;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int map = tile / a.tiles_per_map;
     const int rem = tile - map * a.tiles_per_map;
     const int ty = rem / a.ntx, tx = rem - (rem / a.ntx) * a.ntx;
     const int64_t ls = a.ls, plane = a.H * a.W * ls;
-    const float* __restrict__ cost = static_cast<const float*>(a.cost) + map * plane;
-    const TMem<float, COH> T(static_cast<float*>(a.T) + map * plane, plane);
-    const int64_t y0 = (int64_t)ty * kTile, x0 = (int64_t)tx * kTile;
+    const R* __restrict__ cost = static_cast<const R*>(a.cost) + map * plane;
+    const TMem<R, COH> T(static_cast<R*>(a.T) + map * plane, plane);
+    const int64_t y0 = (int64_t)ty * TH, x0 = (int64_t)tx * kTile;
 
     if (tid == 0) L.flags = 0;
     if (tid < 5) L.key[tid] = 0x7f800000u;
-    // halo ring: wave 0 north row, 1 south row, 2 west column, 3 east column (out of range: +inf)
+    // halo ring: wave 0 north row, 1 south row, 2 west column, 3 east column (out of range: +inf;
+    // lanes >= TH of the column waves have none)
     int h;
     int64_t hy, hx;
     if (wave == 0)      { h = 0 * kLds + lane + 1;          hy = y0 - 1;      hx = x0 + lane; }
-    else if (wave == 1) { h = (kLds - 1) * kLds + lane + 1; hy = y0 + kTile;  hx = x0 + lane; }
+    else if (wave == 1) { h = (TH + 1) * kLds + lane + 1;   hy = y0 + TH;     hx = x0 + lane; }
     else if (wave == 2) { h = (lane + 1) * kLds + 0;        hy = y0 + lane;   hx = x0 - 1; }
     else                { h = (lane + 1) * kLds + kLds - 1; hy = y0 + lane;   hx = x0 + kTile; }
-    const bool hin = hy >= 0 && hy < a.H && hx >= 0 && hx < a.W;
+    const bool hcell = wave < 2 || lane < TH;
+    const bool hin = hcell && hy >= 0 && hy < a.H && hx >= 0 && hx < a.W;
     const int64_t hgi = hin ? (hy * a.W + hx) * ls + a.z0 : 0;
     auto load_halo = [&]() {  // unconditional loads (an in-range index), then the +inf select
-        float v[4] = {INF, INF, INF, INF};
+        R v[4] = {INF, INF, INF, INF};
 #pragma unroll
         for (int z = 0; z < NL; ++z) v[z] = T.ld(hgi + z);
 #pragma unroll
         for (int z = 0; z < NL; ++z) v[z] = hin ? v[z] : INF;
-        return make_float4(v[0], v[1], v[2], v[3]);
+        return LCell<R>::make(v);
     };
     // ---- stage: every global load of the visit (T, cost, halo) is issued before the first LDS
     // store and each path stores its own values (as fim2d.hip's process_tile; interleaved, the
     // staging took one memory round trip per row, 16 in all)
-    float told[16][NL];
-    auto store_tile = [&](const float (&cc)[16][NL], float4 hv) {
+    R told[NJ][NL];
+    auto store_tile = [&](const R (&cc)[NJ][NL], LCell<R> hv) {
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
+        for (int j = 0; j < NJ; ++j) {
             const int ry = wave + 4 * j;
-            float t4[4] = {INF, INF, INF, INF}, c4[4] = {INF, INF, INF, INF};
+            R t4[4] = {INF, INF, INF, INF}, c4[4] = {INF, INF, INF, INF};
 #pragma unroll
             for (int z = 0; z < NL; ++z) {
                 t4[z] = told[j][z];
                 c4[z] = cc[j][z];
             }
-            Ts[(ry + 1) * kLds + lane + 1] = make_float4(t4[0], t4[1], t4[2], t4[3]);
-            Cs[(ry + 1) * kLds + lane + 1] = make_float4(c4[0], c4[1], c4[2], c4[3]);
+            Ts[(ry + 1) * kLds + lane + 1] = LCell<R>::make(t4);
+            Cs[(ry + 1) * kLds + lane + 1] = LCell<R>::make(c4);
         }
-        Ts[h] = hv;
+        if (hcell) Ts[h] = hv;
     };
-    if (y0 + kTile <= a.H && x0 + kTile <= a.W) {  // full tile: no per-cell range test
-        float cc[16][NL];
+    // fp64: costs as the sweep keeps them (>= 2^-500: the range-free square root, fim2d.hip stage_cost)
+    auto scost = [](R c) -> R {
+        if constexpr (sizeof(R) == 8) return __builtin_fmax(c, 0x1p-500);
+        else return c;
+    };
+    if (y0 + TH <= a.H && x0 + kTile <= a.W) {  // full tile: no per-cell range test
+        R cc[NJ][NL];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
+        for (int j = 0; j < NJ; ++j) {
             const int64_t gi = ((y0 + wave + 4 * j) * a.W + x0 + lane) * ls + a.z0;
 #pragma unroll
             for (int z = 0; z < NL; ++z) {
                 told[j][z] = T.ld(gi + z);
-                cc[j][z] = cost[gi + z];
+                cc[j][z] = scost(cost[gi + z]);
             }
         }
         store_tile(cc, load_halo());
     } else {
-        float cc[16][NL];
+        R cc[NJ][NL];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
+        for (int j = 0; j < NJ; ++j) {
             const int64_t gy = y0 + wave + 4 * j, gx = x0 + lane;
             const bool in = gy < a.H && gx < a.W;
             const int64_t gi = in ? (gy * a.W + gx) * ls + a.z0 : 0;
 #pragma unroll
             for (int z = 0; z < NL; ++z) {
-                const float t = T.ld(gi + z), c = cost[gi + z];
+                const R t = T.ld(gi + z), c = cost[gi + z];
                 told[j][z] = in ? t : INF;
-                cc[j][z] = in ? c : INF;
+                cc[j][z] = in ? scost(c) : INF;
             }
         }
         store_tile(cc, load_halo());
     }
-    Cs[h] = INF4;
+    if (hcell) Cs[h] = INFC;
     if (lane < 4) {
-        const int corner = (lane >> 1) * (kLds - 1) * kLds + (lane & 1) * (kLds - 1);
-        Cs[corner] = INF4;
-        Ts[corner] = INF4;
+        const int corner = (lane >> 1) * (TH + 1) * kLds + (lane & 1) * (kLds - 1);
+        Cs[corner] = INFC;
+        Ts[corner] = INFC;
     }
     __syncthreads();
+    (void)NZ;
 
     const int kPasses = COH ? a.max_passes : 1;
     unsigned dirs = L.dirs;  // this pass's sweeps (register: see fim2d.hip process_tile)
     for (int pass = 0;; ++pass) {
         if ((dirs >> wave) & 1u) {
-            if (wave == 0)      sweep_layered<NL, +1, +1>(Ts, lane);
-            else if (wave == 1) sweep_layered<NL, -1, +1>(Ts, lane);
-            else if (wave == 2) sweep_layered<NL, +1, -1>(Ts, lane);
-            else                sweep_layered<NL, -1, -1>(Ts, lane);
+            if (wave == 0)      sweep_layered<R, TH, NL, +1, +1>(Ts, lane);
+            else if (wave == 1) sweep_layered<R, TH, NL, -1, +1>(Ts, lane);
+            else if (wave == 2) sweep_layered<R, TH, NL, +1, -1>(Ts, lane);
+            else                sweep_layered<R, TH, NL, -1, -1>(Ts, lane);
         }
         __syncthreads();
         // ---- write back changed cells, collect side flags
         unsigned fl = 0;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
+        for (int j = 0; j < NJ; ++j) {
             const int ry = wave + 4 * j;
             const int64_t gy = y0 + ry, gx = x0 + lane;
             const bool in = gy < a.H && gx < a.W;
             const int64_t gi = (gy * a.W + gx) * ls + a.z0;
-            const float4 nv4 = Ts[(ry + 1) * kLds + lane + 1];
+            const LCell<R> nv4 = Ts[(ry + 1) * kLds + lane + 1];
 #pragma unroll
             for (int z = 0; z < NL; ++z) {
-                const float nv = f4get(nv4, z);
+                const R nv = nv4.get(z);
                 if (in && nv < told[j][z]) T.st(gi + z, nv);
-                if (nv < told[j][z] * keep) {
+                if (nv < told[j][z] * R(keep)) {
                     fl |= 128u;
                     // a neighbour can improve only if this edge value undercuts its adjacent cell
-                    if (ry == 0 && nv < f4get(Ts[lane + 1], z)) fl |= 1u;
-                    if (ry == kTile - 1 && nv < f4get(Ts[(kLds - 1) * kLds + lane + 1], z)) fl |= 2u;
-                    if (lane == 0 && nv < f4get(Ts[(ry + 1) * kLds], z)) fl |= 4u;
-                    if (lane == kTile - 1 && nv < f4get(Ts[(ry + 1) * kLds + kLds - 1], z)) fl |= 8u;
+                    if (ry == 0 && nv < Ts[lane + 1].get(z)) fl |= 1u;
+                    if (ry == TH - 1 && nv < Ts[(TH + 1) * kLds + lane + 1].get(z)) fl |= 2u;
+                    if (lane == 0 && nv < Ts[(ry + 1) * kLds].get(z)) fl |= 4u;
+                    if (lane == kTile - 1 && nv < Ts[(ry + 1) * kLds + kLds - 1].get(z)) fl |= 8u;
                 }
                 told[j][z] = nv;  // what memory holds now
             }
@@ -296,26 +373,28 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
         if (!(f & 128u) || pass + 1 >= kPasses) break;
         // the halo reload is issued first and the budget charge goes to wave 1, so wave 0's
         // activation atomics are the only round trips the next pass waits for
-        const float4 hv = load_halo();
+        const LCell<R> hv = load_halo();
         if (tid == 64) charge_inplace_pass(a);  // in-place passes: stats and the visit budget
         activate_neighbours(a, tile, f, L.key, 0, 0u);  // lanes 0..4 (T already drained)
         dirs = 0xFu;  // a self revisit: every direction
-        Ts[h] = hv;
+        if (hcell) Ts[h] = hv;
         __syncthreads();  // every wave has read L.flags and its halo side is in
         if (tid == 0) L.flags = 0;
     }
 }
 
 // Persistent driver (cf. fim2d_persist_kernel): one launch per solve, device FIFO of tiles.
-template <int NL>
+template <typename R, int NL>
 __global__ __launch_bounds__(kThreads) void fim2dl_persist_kernel(Fim2dArgs a) {
-    __shared__ TileLdsL L;
-    constexpr float INF = __builtin_inff();
+    constexpr int TH = kRowsOf<R>;
+    __shared__ TileLdsL<R, TH> L;
+    constexpr R INF = Real<R>::inf();
+    const R INFS[4] = {INF, INF, INF, INF};
     for (int i = threadIdx.x; i < kGuard * kLds; i += kThreads) {  // guard rows: read by sweeps, never lowered
-        L.Tbuf[i] = make_float4(INF, INF, INF, INF);
-        L.Tbuf[(kLds + kGuard) * kLds + i] = make_float4(INF, INF, INF, INF);
-        L.Cbuf[i] = make_float4(INF, INF, INF, INF);
-        L.Cbuf[(kLds + kGuard) * kLds + i] = make_float4(INF, INF, INF, INF);
+        L.Tbuf[i] = LCell<R>::make(INFS);
+        L.Tbuf[(TH + 2 + kGuard) * kLds + i] = LCell<R>::make(INFS);
+        L.Cbuf[i] = LCell<R>::make(INFS);
+        L.Cbuf[(TH + 2 + kGuard) * kLds + i] = LCell<R>::make(INFS);
     }
     const float keep = a.keep;
     int tile = -1;
@@ -344,82 +423,115 @@ __global__ __launch_bounds__(kThreads) void fim2dl_persist_kernel(Fim2dArgs a) {
         __syncthreads();
         tile = __builtin_amdgcn_readfirstlane(L.tile);
         if (tile < 0) break;
-        process_tile_layered<NL, true>(a, tile, L, keep);
+        process_tile_layered<R, NL, true>(a, tile, L, keep);
     }
     if (threadIdx.x == 0 && nvis) atomicAdd(a.visits, (unsigned long long)nvis);
 }
 
-__global__ void fim2dl_init_kernel(float* __restrict__ T, int64_t n, unsigned* __restrict__ qstate, int64_t ntiles,
+template <typename R>
+__global__ void fim2dl_init_kernel(R* __restrict__ T, int64_t n, unsigned* __restrict__ qstate, int64_t ntiles,
                                    unsigned* __restrict__ qslot, int64_t nslots) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) T[i] = __builtin_inff();
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) T[i] = Real<R>::inf();
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ntiles; i += stride) qstate[i] = 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += stride) qslot[i] = 0;
 }
 
-// T[goal] = 0 (gz: absolute layer index) and the goal's tile queued
-__global__ void fim2dl_seed_kernel(Fim2dArgs a, int64_t gx, int64_t gy, int64_t gz) {
-    static_cast<float*>(a.T)[(gy * a.W + gx) * a.ls + gz] = 0.f;
-    qpush(a, (int)(gy / kTile) * a.ntx + (int)(gx / kTile), kSelf);
+// T[goal] = 0 (gz: absolute layer index) and the goal's tile (th rows) queued
+template <typename R>
+__global__ void fim2dl_seed_kernel(Fim2dArgs a, int64_t gx, int64_t gy, int64_t gz, int th) {
+    static_cast<R*>(a.T)[(gy * a.W + gx) * a.ls + gz] = R(0);
+    __threadfence();
+    qpush(a, (int)(gy / th) * a.ntx + (int)(gx / kTile), kSelf);
 }
 
 __global__ void fim2dl_rewind_kernel(Fim2dArgs a) { *a.qhead = *a.qtail; }
 
 // flag |= 1 if layer z of the [HW][L] volume holds a finite cost
-__global__ void layer_finite_kernel(const float* __restrict__ cost, int64_t hw, int64_t L, int64_t z, int* flag) {
+template <typename R>
+__global__ void layer_finite_kernel(const R* __restrict__ cost, int64_t hw, int64_t L, int64_t z, int* flag) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     bool any = false;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < hw; i += stride)
-        any |= cost[i * L + z] != __builtin_inff();
+        any |= cost[i * L + z] != Real<R>::inf();
     if (__any(any) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
 }
 
 // ------------------------------------------------------------------------- host launchers
-hipError_t fim2dl_init(const Fim2dArgs& a, int64_t gx, int64_t gy, int64_t gz, hipStream_t st) {
+int fim2dl_rows(bool f64) { return f64 ? kRowsOf<double> : kRowsOf<float>; }
+
+hipError_t fim2dl_init(const Fim2dArgs& a, bool f64, int64_t gx, int64_t gy, int64_t gz, hipStream_t st) {
     const int64_t n = a.H * a.W * a.ls;
     const int64_t nslots = (int64_t)a.qmask + 1;
-    const int grid = (int)std::min<int64_t>(4096, (n + 255) / 256);
+    const int grid = (int)std::min<int64_t>(4096, (std::max(n, nslots) + 255) / 256);
     hipError_t e = hipMemsetAsync(a.qhead, 0, kQueueCtlBytes, st);  // head tail active error
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(fim2dl_init_kernel, dim3(grid), dim3(256), 0, st, static_cast<float*>(a.T), n, a.qstate,
-                       (int64_t)a.tiles_per_map, a.qslot, nslots);
-    hipLaunchKernelGGL(fim2dl_seed_kernel, dim3(1), dim3(1), 0, st, a, gx, gy, gz);
+    if (f64) {
+        hipLaunchKernelGGL(fim2dl_init_kernel<double>, dim3(grid), dim3(256), 0, st, static_cast<double*>(a.T), n,
+                           a.qstate, (int64_t)a.tiles_per_map, a.qslot, nslots);
+        hipLaunchKernelGGL(fim2dl_seed_kernel<double>, dim3(1), dim3(1), 0, st, a, gx, gy, gz, kRowsOf<double>);
+    } else {
+        hipLaunchKernelGGL(fim2dl_init_kernel<float>, dim3(grid), dim3(256), 0, st, static_cast<float*>(a.T), n,
+                           a.qstate, (int64_t)a.tiles_per_map, a.qslot, nslots);
+        hipLaunchKernelGGL(fim2dl_seed_kernel<float>, dim3(1), dim3(1), 0, st, a, gx, gy, gz, kRowsOf<float>);
+    }
     return hipGetLastError();
 }
 
-template <int NL>
+template <typename R, int NL>
 static int resident_of(int cus) {
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fim2dl_persist_kernel<NL>, kThreads, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fim2dl_persist_kernel<R, NL>, kThreads, 0) != hipSuccess ||
         per_cu < 1)
         per_cu = 1;
     return per_cu * cus;
 }
 
-int fim2dl_persist_resident(int nl, int cus) {
+int fim2dl_persist_resident(int nl, bool f64, int cus) {
+    if (f64) {
+        switch (nl) {
+            case 1: return resident_of<double, 1>(cus);
+            case 2: return resident_of<double, 2>(cus);
+            default: return resident_of<double, 3>(cus);
+        }
+    }
     switch (nl) {
-        case 1: return resident_of<1>(cus);
-        case 2: return resident_of<2>(cus);
-        case 3: return resident_of<3>(cus);
-        default: return resident_of<4>(cus);
+        case 1: return resident_of<float, 1>(cus);
+        case 2: return resident_of<float, 2>(cus);
+        case 3: return resident_of<float, 3>(cus);
+        default: return resident_of<float, 4>(cus);
     }
 }
 
-hipError_t fim2dl_persist(const Fim2dArgs& a, int nl, int grid, hipStream_t st) {
-    switch (nl) {
-        case 1: hipLaunchKernelGGL(fim2dl_persist_kernel<1>, dim3(grid), dim3(kThreads), 0, st, a); break;
-        case 2: hipLaunchKernelGGL(fim2dl_persist_kernel<2>, dim3(grid), dim3(kThreads), 0, st, a); break;
-        case 3: hipLaunchKernelGGL(fim2dl_persist_kernel<3>, dim3(grid), dim3(kThreads), 0, st, a); break;
-        case 4: hipLaunchKernelGGL(fim2dl_persist_kernel<4>, dim3(grid), dim3(kThreads), 0, st, a); break;
-        default: return hipErrorInvalidValue;
+hipError_t fim2dl_persist(const Fim2dArgs& a, int nl, bool f64, int grid, hipStream_t st) {
+    if (f64) {
+        switch (nl) {
+            case 1: hipLaunchKernelGGL((fim2dl_persist_kernel<double, 1>), dim3(grid), dim3(kThreads), 0, st, a); break;
+            case 2: hipLaunchKernelGGL((fim2dl_persist_kernel<double, 2>), dim3(grid), dim3(kThreads), 0, st, a); break;
+            case 3: hipLaunchKernelGGL((fim2dl_persist_kernel<double, 3>), dim3(grid), dim3(kThreads), 0, st, a); break;
+            default: return hipErrorInvalidValue;
+        }
+    } else {
+        switch (nl) {
+            case 1: hipLaunchKernelGGL((fim2dl_persist_kernel<float, 1>), dim3(grid), dim3(kThreads), 0, st, a); break;
+            case 2: hipLaunchKernelGGL((fim2dl_persist_kernel<float, 2>), dim3(grid), dim3(kThreads), 0, st, a); break;
+            case 3: hipLaunchKernelGGL((fim2dl_persist_kernel<float, 3>), dim3(grid), dim3(kThreads), 0, st, a); break;
+            case 4: hipLaunchKernelGGL((fim2dl_persist_kernel<float, 4>), dim3(grid), dim3(kThreads), 0, st, a); break;
+            default: return hipErrorInvalidValue;
+        }
     }
     hipLaunchKernelGGL(fim2dl_rewind_kernel, dim3(1), dim3(1), 0, st, a);
     return hipGetLastError();
 }
 
-hipError_t layer_finite(const float* cost, int64_t hw, int64_t L, int64_t z, int* d_flag, hipStream_t st) {
+hipError_t layer_finite(const void* cost, bool f64, int64_t hw, int64_t L, int64_t z, int* d_flag, hipStream_t st) {
     const int grid = (int)std::min<int64_t>(2048, (hw + 255) / 256);
-    hipLaunchKernelGGL(layer_finite_kernel, dim3(grid), dim3(256), 0, st, cost, hw, L, z, d_flag);
+    if (f64)
+        hipLaunchKernelGGL(layer_finite_kernel<double>, dim3(grid), dim3(256), 0, st, static_cast<const double*>(cost), hw,
+                           L, z, d_flag);
+    else
+        hipLaunchKernelGGL(layer_finite_kernel<float>, dim3(grid), dim3(256), 0, st, static_cast<const float*>(cost), hw,
+                           L, z, d_flag);
     return hipGetLastError();
 }
 

@@ -111,30 +111,33 @@ def _layered_case(shape, seed, pad=False, switch=False):
                                                      ((64, 64, 4), 13, False, True), ((90, 140, 3), 14, True, True),
                                                      ((300, 257, 3), 15, False, True), ((70, 65, 1), 16, False, False)])
 def test_layered_vs_oracle(ctx, shape, seed, pad, switch):
+    """fp32 (<= 4 layers, 64-row tiles) and fp64 (<= 3 layers, 40-row tiles; 4 layers go to fim3d)."""
     c, goal = _layered_case(shape, seed, pad, switch)
     O.set_strict(False)
     try:
         R = O.fmm3d(c, goal, None)
     finally:
         O.set_strict(True)
-    T = ctx.tmap3d(c, goal, dtype=np.float32)
-    check(T, R, False)
-    if pad:
-        assert np.all(np.isinf(T[:, :, 0])) and np.all(np.isinf(T[:, :, -1]))
+    for f64 in (False, True):
+        T = ctx.tmap3d(c, goal, dtype=np.float64 if f64 else np.float32)
+        check(T, R, f64)
+        if pad:
+            assert np.all(np.isinf(T[:, :, 0])) and np.all(np.isinf(T[:, :, -1]))
 
 
-def test_layered_device_entry(ctx):
+@pytest.mark.parametrize("f64", [False, True])
+def test_layered_device_entry(ctx, f64):
     """eik_fim3d_solve on device buffers (the bench's C5 route) equals the host entry point."""
     import torch
     from eikonal import _lib as L
 
     c, goal = _layered_case((257, 300, 3), 21, pad=True, switch=True)
     dev = torch.device("cuda", 0)
-    cd = torch.from_numpy(c.astype(np.float32)).to(dev)
+    cd = torch.from_numpy(c.astype(np.float64 if f64 else np.float32)).to(dev)
     Td = torch.empty_like(cd)
     H, W, Lz = c.shape
     st = torch.cuda.current_stream(dev)
-    ctx._chk(L.lib().eik_fim3d_solve(ctx._h, cd.data_ptr(), Td.data_ptr(), H, W, Lz, L.EIK_F32,
+    ctx._chk(L.lib().eik_fim3d_solve(ctx._h, cd.data_ptr(), Td.data_ptr(), H, W, Lz, L.EIK_F64 if f64 else L.EIK_F32,
                                      np.ascontiguousarray(goal, np.int64), st.cuda_stream))
     torch.cuda.synchronize()
     s = ctx.stats()
@@ -145,7 +148,7 @@ def test_layered_device_entry(ctx):
         R = O.fmm3d(c, goal, None)
     finally:
         O.set_strict(True)
-    check(T, R, False)
+    check(T, R, f64)
 
 
 @pytest.mark.parametrize("passes", [1, 8])

@@ -22,5 +22,9 @@ python tools/pmc_traffic.py /tmp/pmc_fetch_$R /tmp/pmc_write_$R "$K" $D > $O/pmc
 C5="python bench.py --dtype $D --steps 1 --warmup 0 --no-cpu-baseline --no-path --no-timing --extras C5 --extra-steps 2"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d /tmp/pmc_fetch_c5_$R -o f -- $C5 > $O/pmc_fetch_c5.out 2>&1 || { echo "pmc fetch c5 rc=$?"; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d /tmp/pmc_write_c5_$R -o w -- $C5 > $O/pmc_write_c5.out 2>&1 || { echo "pmc write c5 rc=$?"; exit 1; }
-python tools/pmc_traffic.py /tmp/pmc_fetch_c5_$R /tmp/pmc_write_c5_$R "fim2dl_persist_kernel" f32 > $O/pmc_traffic_${R}_c5.json 2>> $O/pmc_traffic.err
+# (a --dtype f64 run holds both C5 kernels: the fp64 one (C5) and the fp32 one (C5_f32))
+python tools/pmc_traffic.py /tmp/pmc_fetch_c5_$R /tmp/pmc_write_c5_$R "fim2dl_persist_kernel<float" f32 > $O/pmc_traffic_${R}_c5.json 2>> $O/pmc_traffic.err
+if [ "$D" = f64 ]; then
+python tools/pmc_traffic.py /tmp/pmc_fetch_c5_$R /tmp/pmc_write_c5_$R "fim2dl_persist_kernel<double" f64 > $O/pmc_traffic_${R}_c5_f64.json 2>> $O/pmc_traffic.err
+fi
 echo ALLOK
