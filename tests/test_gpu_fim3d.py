@@ -125,6 +125,31 @@ def test_layered_vs_oracle(ctx, shape, seed, pad, switch):
             assert np.all(np.isinf(T[:, :, 0])) and np.all(np.isinf(T[:, :, -1]))
 
 
+@pytest.mark.parametrize("shape,seed", [((1, 1, 1), 41), ((5, 3, 2), 42), ((39, 65, 3), 43), ((41, 64, 1), 44),
+                                        ((80, 129, 2), 45)])
+def test_layered_edge_shapes(ctx, shape, seed):
+    """Layered solver at the tile edges: volumes smaller than one tile, one row / column past a
+    tile (fp64 tiles are 40 rows, fp32 64), a single cell; +inf islands and cheap cells (0.5; a zero
+    cost has no reference result -- FastMarching3D.py:62-73 empties its list and raises -- and at
+    costs << 1 the reference's 3-axis form (S + sqrt(nC^2 + S^2 - nQ))/n cancels: at C = 1e-3 and
+    T ~ 100 its own error is ~1e-8, above the 1e-9 tolerance; the layered solver solves relative to
+    the smallest neighbour, fim3d.hip's fp64 path in the reference's arithmetic)."""
+    rng = np.random.default_rng(seed)
+    c = rng.uniform(1, 4, shape)
+    c[rng.random(shape) < 0.05] = 0.5
+    c[rng.random(shape) < 0.08] = np.inf
+    H, W, L = shape
+    goal = np.array([W // 2, H // 2, L // 2])
+    c[goal[1], goal[0], goal[2]] = 1.0
+    O.set_strict(False)
+    try:
+        R = O.fmm3d(c, goal, None)
+    finally:
+        O.set_strict(True)
+    for f64 in (False, True):
+        check(ctx.tmap3d(c, goal, dtype=np.float64 if f64 else np.float32), R, f64)
+
+
 @pytest.mark.parametrize("f64", [False, True])
 def test_layered_device_entry(ctx, f64):
     """eik_fim3d_solve on device buffers (the bench's C5 route) equals the host entry point."""
