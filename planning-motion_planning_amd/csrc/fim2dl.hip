@@ -8,8 +8,9 @@
 // 2D solver (fim_engine.hpp, persistent FIFO driver, in-place revisits, activation-direction
 // sweeps -- fim2d.hip):
 //
-//  * a 64 x 64 tile keeps, per cell, its NL layers in one float4 LDS slot (T and cost; unused
-//    slots +inf), so one ds_read_b128 fetches every layer of a neighbour;
+//  * a 64 x 64 tile (fp32; fp64: 40 rows x 64 columns, see kRowsOf) keeps, per cell, its NL layers
+//    in one LDS slot (T and cost arrays; fp32 a float4, unused slots +inf, so one ds_read_b128
+//    fetches every layer of a neighbour; fp64 three doubles);
 //  * each of the four waves runs one quadrant sweep (skewed anti-diagonals, DPP upstream-x, as
 //    in fim2d.hip); at each step a lane updates its cell in ALL layers -- NL independent
 //    Godunov chains that hide each other's latency.  The z neighbours of a layer are the
@@ -41,7 +42,6 @@ template <> struct LCell<double> {
     __device__ __forceinline__ double get(int z) const { return v[z]; }
     static __device__ __forceinline__ LCell make(const double (&x)[4]) { return LCell{{x[0], x[1], x[2]}}; }
 };
-template <typename R> constexpr int kLayersOf = sizeof(R) == 4 ? 4 : 3;
 // tile rows: 64 (fp32, 156 KB of LDS) or EIK_L64_ROWS (fp64; 40 rows: (40 + 2 + 8 guard) x 66 cells x
 // 48 B = 155 KB, the most that fits 160 KB with a step count divisible by the read-ahead depth);
 // always 64 columns (one lane each)
@@ -235,7 +235,6 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
                                                      float keep) {
     constexpr int TH = kRowsOf<R>;
     constexpr int NJ = TH / 4;  // cells per thread
-    constexpr int NZ = kLayersOf<R>;
     constexpr R INF = Real<R>::inf();
     const R INFS[4] = {INF, INF, INF, INF};
     const LCell<R> INFC = LCell<R>::make(INFS);
@@ -330,7 +329,6 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
         Ts[corner] = INFC;
     }
     __syncthreads();
-    (void)NZ;
 
     const int kPasses = COH ? a.max_passes : 1;
     unsigned dirs = L.dirs;  // this pass's sweeps (register: see fim2d.hip process_tile)
