@@ -85,6 +85,8 @@ struct eik_ctx {
     DevBuf q3ctl, q3slot, q3state, q3vis;  // 3D persistent driver: tile FIFO (fim_engine.hpp)
     unsigned* h_q3 = nullptr;          // pinned copy of q3ctl + the two visit counters
     int resident3[2] = {0, 0};         // co-resident workgroups of fim3d_persist_kernel (f32, f64)
+    hipStream_t stream2 = nullptr;     // second stream: the rover path's two walks run side by side
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     hipEvent_t e3[2] = {nullptr, nullptr};
 };
 
@@ -175,6 +177,9 @@ void eik_destroy(eik_ctx* c) {
     if (c->h_q3) (void)hipHostFree(c->h_q3);
     for (hipEvent_t e : c->e3)
         if (e) (void)hipEventDestroy(e);
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -328,7 +333,9 @@ int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
     // C4 at one GPU 16.4-16.6 vs 16.3-16.4 at 16 (within noise); 8 is clearly slower on both.
     // A single map large enough for the 4-waves-per-SIMD kernel (>= kWideTiles tiles, 16384^2) is
     // throughput-bound: 16 passes, 17.1-17.3 -> 18.3-18.9 Gcells/s (profiles/r02w_passes_wide.log).
-    f->a.max_passes = c->passes > 0 ? c->passes : f->B > 1 ? 2 : (!f->f64 && f->a.tiles_per_map >= kWideTiles) ? 16 : 24;
+    // A few large maps (biComputeTmap's two fronts: B = 2 of 4096^2) are latency-bound like one map.
+    const bool batch = f->B > 4 || (f->B > 1 && f->a.tiles_per_map < 1024);
+    f->a.max_passes = c->passes > 0 ? c->passes : batch ? 2 : (!f->f64 && f->a.tiles_per_map >= kWideTiles) ? 16 : 24;
     f->a.qbudget = c->max_visits ? c->max_visits : 1024ull * (unsigned long long)(f->B * f->a.tiles_per_map) + (1ull << 20);
     f->iterations = 0;
     f->host_syncs = 0;
@@ -744,13 +751,26 @@ int eik_tmap2d_bidir_f64(eik_ctx* c, const double* cost, int64_t H, int64_t W, i
     if (!c || !cost || !TG || !TS || !join) return c ? set_err(c, EIK_ERR_ARG, "NULL argument") : EIK_ERR_ARG;
     const int64_t n = H * W;
     if (n >= (1ll << 29)) return set_err(c, EIK_ERR_ARG, "bidirectional join supports < 2^29 cells");
-    // both fronts as one 2-map batch: map 0 from the goal, map 1 from the start
-    std::vector<double> cost2((size_t)(2 * n));
-    std::memcpy(cost2.data(), cost, sizeof(double) * n);
-    std::memcpy(cost2.data() + n, cost, sizeof(double) * n);
+    // both fronts as one 2-map batch: map 0 from the goal, map 1 from the start.  The raster goes up
+    // once and is duplicated on the device; the fields come back straight into TG / TS (no host
+    // staging copies: the drop-in's biComputeTmap spent ~200 ms in them for a 4096^2 raster)
     const int64_t goals[4] = {gx, gy, sx, sy};
-    std::vector<double> T2((size_t)(2 * n));
-    int rc = tmap_host<double>(c, cost2.data(), 2, H, W, goals, T2.data());
+    for (int b = 0; b < 2; ++b)
+        if (goals[2 * b] < 0 || goals[2 * b + 1] < 0 || goals[2 * b] >= W || goals[2 * b + 1] >= H)
+            return set_err(c, EIK_ERR_ARG, "node (%ld, %ld) outside %ldx%ld", (long)goals[2 * b], (long)goals[2 * b + 1],
+                           (long)H, (long)W);
+    int rc = check_cost(c, cost, n);
+    if (rc) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    eik_fim2d* f = nullptr;
+    rc = get_solver(c, 2, H, W, EIK_F64, &f);
+    if (rc) return rc;
+    HIPCHK(c, c->cost.ensure(sizeof(double) * 2 * n));
+    HIPCHK(c, c->T.ensure(sizeof(double) * 2 * n));
+    double* dcost = (double*)c->cost.p;
+    HIPCHK(c, hipMemcpyAsync(dcost, cost, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(dcost + n, dcost, sizeof(double) * n, hipMemcpyDeviceToDevice, c->stream));
+    rc = eik_fim2d_solve(f, dcost, c->T.p, goals, c->stream);
     if (rc) return rc;
     // join from the device-resident fields (c->T holds both maps back to back)
     const size_t wb = bidir_join_work_bytes(n);
@@ -1430,10 +1450,19 @@ int eik_rover_path_f64(eik_ctx* c, const double* Z, int64_t H, int64_t W, const 
     int64_t* dn = (int64_t*)(dP + 2 * 2 * pcap);
     int* dst = (int*)(dn + 2);
     const double eg[2] = {(double)g[0], (double)g[1]}, es[2] = {(double)g[2], (double)g[3]};
+    // the two walks are independent one-workgroup kernels: pathS runs on a second stream beside
+    // pathG (each walk is one dependent chain of steps, ~0.4 us each)
+    if (!c->stream2) HIPCHK(c, hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+    if (!c->ev_fork) HIPCHK(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+    if (!c->ev_join) HIPCHK(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+    HIPCHK(c, hipEventRecord(c->ev_fork, st));
+    HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
     rc = eik_path2d_dev(c, dT, EIK_F64, H, W, jn, eg, q->tau, dP, pcap, dn, dst, st);
     if (rc) return rc;
-    rc = eik_path2d_dev(c, dT + n, EIK_F64, H, W, jn, es, q->tau, dP + 2 * pcap, pcap, dn + 1, dst + 1, st);
+    rc = eik_path2d_dev(c, dT + n, EIK_F64, H, W, jn, es, q->tau, dP + 2 * pcap, pcap, dn + 1, dst + 1, c->stream2);
     if (rc) return rc;
+    HIPCHK(c, hipEventRecord(c->ev_join, c->stream2));
+    HIPCHK(c, hipStreamWaitEvent(st, c->ev_join, 0));
     int64_t hn[2];
     int hs[2];
     HIPCHK(c, hipMemcpyAsync(hn, dn, sizeof hn, hipMemcpyDeviceToHost, st));
