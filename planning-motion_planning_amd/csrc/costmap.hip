@@ -366,10 +366,14 @@ hipError_t cm_morph(const unsigned char* A, int64_t H, int64_t W, int r, bool er
 
 // ---- image_filling (:82-94) around a reachability solve ---------------------------------
 // cost for the flood fill: 1 on pixels equal to the seed value m[0], +inf elsewhere
+// Reachability by the block-FIM solver: cost 0 on the seed's value (+inf elsewhere), so a reached
+// cell is 0 at once and never revisited for a refinement -- only connectivity is asked.  (The solve
+// still takes ~2.3 ms at 4096^2, as with cost 1: a flood from the corner pixel is a chain of ~128
+// tile hops across the raster, tools/rover_probe.py under rocprofv3.)
 __global__ void cm_fill_cost_kernel(const unsigned char* __restrict__ m, int64_t n, float* __restrict__ c) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    c[i] = m[i] == m[0] ? 1.f : __builtin_inff();
+    c[i] = m[i] == m[0] ? 0.f : __builtin_inff();
 }
 // filled = seed pixel's component set to 1; out = m | (~filled - 254) (uint8): seed 0 -> holes
 // (zeros not reached) become 1; seed 1 -> every pixel 1 (the reference's arithmetic)
