@@ -395,6 +395,128 @@ hipError_t cm_fill_apply(unsigned char* m, const float* T, int64_t n, hipStream_
     return hipGetLastError();
 }
 
+// ---- image_filling (:82-94) as connected components: the 4-connected component of pixel (0, 0)
+// among the pixels equal to m[0], by lock-free union-find (links always from the larger to the
+// smaller index, so the component of pixel 0 has root 0).  The block-FIM flood (cm_fill_cost /
+// cm_fill_apply above) is a chain of ~128 tile hops from the corner across a 4096^2 raster
+// (2.3 ms); here no information travels tile by tile:
+//  1. per 32 x 32 tile, union-find in LDS over the tile's pixels, each pixel's local root written
+//     as a global index (lroot; -1: not the seed value);
+//  2. one thread per pixel pair across a tile border: union of their local roots in `parent`;
+//  3. every local root resolved to its final root, then the fill applied from parent[lroot[i]].
+constexpr int kCcl = 32;
+__device__ __forceinline__ int ccl_ld(const int* p, int x, int scope) {
+    return scope == 0 ? __hip_atomic_load(p + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+                      : __hip_atomic_load(p + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ccl_find(const int* p, int x, int scope) {
+    for (int y = ccl_ld(p, x, scope); y != x; y = ccl_ld(p, x, scope)) x = y;
+    return x;
+}
+__device__ __forceinline__ void ccl_union(int* p, int a, int b, int scope) {
+    for (;;) {
+        a = ccl_find(p, a, scope);
+        b = ccl_find(p, b, scope);
+        if (a == b) return;
+        if (a > b) { const int t = a; a = b; b = t; }
+        const int old = atomicCAS(p + b, b, a);  // link root b under a, unless b stopped being a root
+        if (old == b) return;
+        b = old;
+    }
+}
+
+__global__ __launch_bounds__(256) void cm_ccl_local_kernel(const unsigned char* __restrict__ m, int64_t H, int64_t W,
+                                                           int* __restrict__ lroot, int* __restrict__ parent) {
+    __shared__ int lp[kCcl * kCcl];
+    const unsigned char v = m[0];
+    const int64_t y0 = (int64_t)blockIdx.y * kCcl, x0 = (int64_t)blockIdx.x * kCcl;
+    bool s[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int q = threadIdx.x + 256 * k;
+        const int64_t gy = y0 + q / kCcl, gx = x0 + q % kCcl;
+        s[k] = gy < H && gx < W && m[gy * W + gx] == v;
+        lp[q] = s[k] ? q : -1;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int q = threadIdx.x + 256 * k;
+        if (!s[k]) continue;
+        const int lx = q % kCcl, ly = q / kCcl;
+        if (lx + 1 < kCcl && ccl_ld(lp, q + 1, 0) >= 0) ccl_union(lp, q, q + 1, 0);  // -1 never changes
+        if (ly + 1 < kCcl && ccl_ld(lp, q + kCcl, 0) >= 0) ccl_union(lp, q, q + kCcl, 0);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int q = threadIdx.x + 256 * k;
+        const int64_t gy = y0 + q / kCcl, gx = x0 + q % kCcl;
+        if (gy >= H || gx >= W) continue;
+        const int64_t g = gy * W + gx;
+        int r = -1;
+        if (s[k]) {
+            const int lr = ccl_find(lp, q, 0);
+            r = (int)((y0 + lr / kCcl) * W + x0 + lr % kCcl);
+        }
+        lroot[g] = r;
+        parent[g] = (int)g;
+    }
+}
+
+// pairs across tile borders: n_v = H * (ntx - 1) vertical-border pairs, then W * (nty - 1) horizontal
+__global__ void cm_ccl_border_kernel(int64_t H, int64_t W, const int* __restrict__ lroot, int* parent, int64_t nv,
+                                     int64_t total) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= total) return;
+    int64_t a, b;
+    if (t < nv) {
+        const int64_t y = t % H, k = t / H + 1;  // border between columns k*32 - 1 and k*32
+        a = y * W + k * kCcl - 1;
+        b = a + 1;
+    } else {
+        const int64_t u = t - nv, x = u % W, k = u / W + 1;
+        a = (k * kCcl - 1) * W + x;
+        b = a + W;
+    }
+    const int ra = lroot[a], rb = lroot[b];
+    if (ra >= 0 && rb >= 0 && ra != rb) ccl_union(parent, ra, rb, 1);
+}
+
+__global__ void cm_ccl_resolve_kernel(int64_t n, const int* __restrict__ lroot, int* parent) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || lroot[i] != (int)i) return;  // local roots only
+    parent[i] = ccl_find(parent, (int)i, 1);
+}
+
+// the fill of cm_fill_apply_kernel with "reached" = in pixel 0's component
+__global__ void cm_ccl_apply_kernel(unsigned char* __restrict__ m, const int* __restrict__ lroot,
+                                    const int* __restrict__ parent, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const unsigned char seed = m[0];  // read before any write: m[0] is never changed by this kernel
+    const int r = lroot[i];
+    const bool reached = r >= 0 && parent[r] == 0;
+    const unsigned char filled = (m[i] == seed && reached) ? 1 : m[i];
+    const unsigned char inv = (unsigned char)((unsigned char)~filled - 254);
+    m[i] = m[i] | inv;
+}
+
+hipError_t cm_fill_ccl(unsigned char* m, int64_t H, int64_t W, int* lroot, int* parent, hipStream_t st) {
+    const int64_t n = H * W;
+    if (n >= (1ll << 31)) return hipErrorInvalidValue;
+    const int64_t ntx = (W + kCcl - 1) / kCcl, nty = (H + kCcl - 1) / kCcl;
+    hipLaunchKernelGGL(cm_ccl_local_kernel, dim3((unsigned)ntx, (unsigned)nty), dim3(256), 0, st, m, H, W, lroot, parent);
+    const int64_t nv = H * (ntx - 1), total = nv + W * (nty - 1);
+    if (total > 0)
+        hipLaunchKernelGGL(cm_ccl_border_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, H, W, lroot,
+                           parent, nv, total);
+    const unsigned grid = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(cm_ccl_resolve_kernel, dim3(grid), dim3(256), 0, st, n, lroot, parent);
+    hipLaunchKernelGGL(cm_ccl_apply_kernel, dim3(grid), dim3(256), 0, st, m, lroot, parent, n);
+    return hipGetLastError();
+}
+
 __global__ void cm_border_kernel(unsigned char* __restrict__ m, int64_t H, int64_t W, unsigned char v) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < W) {

@@ -1272,9 +1272,14 @@ int eik_gradient2d_f64(eik_ctx* c, const double* T, int64_t H, int64_t W, double
 }  // extern "C"
 
 // ------------------------------------------------------------------ cost-raster builder
-// image_filling (:82-94) of the device mask m in place: reachability of the pixels equal to
-// m[0] from (0, 0) (the 4-connected flood fill) by the block-FIM solver on cost 1 / +inf.
+// image_filling (:82-94) of the device mask m in place: the pixels equal to m[0] that the
+// 4-connected flood fill from (0, 0) reaches.  Default: connected components (cm_fill_ccl,
+// union-find); EIK_FILL_FIM=1 in the build: reachability by the block-FIM solver on cost 0 / +inf.
+#ifndef EIK_FILL_FIM
+#define EIK_FILL_FIM 0
+#endif
 static int cm_fill(eik_ctx* c, unsigned char* m, int64_t H, int64_t W, float* fcost, float* fT, hipStream_t st) {
+#if EIK_FILL_FIM
     eik_fim2d* f = c->cached_fill;
     if (!f || f->H != H || f->W != W) {
         if (f) eik_fim2d_destroy(f);
@@ -1290,6 +1295,10 @@ static int cm_fill(eik_ctx* c, unsigned char* m, int64_t H, int64_t W, float* fc
     c->last = keep;
     if (rc) return rc;
     HIPCHK(c, cm_fill_apply(m, fT, H * W, st));
+#else
+    // the two f32 scratch planes serve as the int32 lroot / parent arrays
+    HIPCHK(c, cm_fill_ccl(m, H, W, reinterpret_cast<int*>(fcost), reinterpret_cast<int*>(fT), st));
+#endif
     return EIK_OK;
 }
 

@@ -40,6 +40,31 @@ def test_image_filling(ctx, shape, seed, p):
         assert np.array_equal(ctx.image_fill(im), CO.image_filling(im))
 
 
+def _spiral(n, w=2):
+    """A one-corridor spiral of free pixels from (0, 0) inwards: one component that winds through
+    every 32 x 32 tile of the union-find many times, plus closed pockets (holes) beside it."""
+    im = np.ones((n, n), np.uint8)
+    y0, x0, y1, x1 = 0, 0, n - 1, n - 1
+    while y1 - y0 > 2 * w and x1 - x0 > 2 * w:
+        im[y0:y0 + w, x0:x1 + 1] = 0
+        im[y0:y1 + 1, x1 - w + 1:x1 + 1] = 0
+        im[y1 - w + 1:y1 + 1, x0 + w + 1:x1 + 1] = 0
+        im[y0 + 2 * w:y1 + 1, x0 + w + 1:x0 + 2 * w + 1] = 0
+        y0, x0, y1, x1 = y0 + 2 * w, x0 + 2 * w + 1, y1 - 2 * w, x1 - 2 * w
+    return im
+
+
+@pytest.mark.parametrize("n", [97, 300, 1025])
+def test_image_filling_spiral(ctx, n):
+    """image_filling (:82-94) on a maze: a corridor spiralling through many union-find tiles, and
+    pockets of free pixels it does not reach (the holes filled), against the oracle's flood fill."""
+    im = _spiral(n)
+    rng = np.random.default_rng(n)
+    pockets = (rng.random(im.shape) < 0.002) & (im == 1)
+    im[pockets] = 0  # isolated free pixels inside the walls: holes to fill
+    assert np.array_equal(ctx.image_fill(im), CO.image_filling(im))
+
+
 @pytest.mark.parametrize("n,seed,rms", [(120, 5, 0.25), (200, 6, 0.2), (257, 7, 0.3)])
 def test_costmap_vs_oracle(ctx, n, seed, rms):
     Z = terrain_np.dem(n, n, seed=seed, rms_slope=rms) + 3.0
