@@ -24,6 +24,7 @@ static int N, NT, policy;
 static float delta = 0.f;  /* policy 2: bucket width */
 static long seq = 0;
 static int oneside = 0;  /* 1: each quadrant sweep reads only its upstream neighbours */
+static int skipdir = 0;  /* 1: an in-place pass skips the one direction that alone changed the tile last pass */
 static float *cost, *T, *key_of;
 static unsigned char *pend, *held;
 
@@ -80,13 +81,15 @@ static int take(void) {
     return -1;
 }
 
-typedef struct { int t, p; float kmin; float L[TS + 2][TS + 2], C[TS + 2][TS + 2]; } Work;
+typedef struct { int t, p, last; float kmin; float L[TS + 2][TS + 2], C[TS + 2][TS + 2]; } Work;
 
 int main(int argc, char** argv) {
     const char* cf = argv[1]; N = atoi(argv[2]); policy = atoi(argv[3]);
     const int maxp = atoi(argv[4]), K = atoi(argv[5]);
     if (argc > 6) delta = atof(argv[6]);
     if (getenv("ONESIDE")) oneside = 1;
+    if (getenv("SKIPDIR")) skipdir = 1;
+    long dsweeps = 0;  /* quadrant sweeps run */
     NT = N / TS;
     const int nt = NT * NT;
     cost = malloc(sizeof(float) * N * N); T = malloc(sizeof(float) * N * N);
@@ -111,7 +114,7 @@ int main(int argc, char** argv) {
                 int t = take();
                 if (t < 0) continue;
                 held[t] = 1; pend[t] = 0; key_of[t] = INFINITY; ++visits; visited[t] = 1;
-                W[k].t = t; W[k].p = 0;
+                W[k].t = t; W[k].p = 0; W[k].last = -1;
                 int ty = t / NT, tx = t % NT, y0 = ty * TS, x0 = tx * TS;
                 for (int y = -1; y <= TS; ++y)
                     for (int x = -1; x <= TS; ++x) {
@@ -122,6 +125,7 @@ int main(int argc, char** argv) {
             } else {
                 /* in place: refresh the halo from T as of this round's start */
                 int t = W[k].t, y0 = (t / NT) * TS, x0 = (t % NT) * TS;
+                if (pend[t]) W[k].last = -1;  /* activated meanwhile: every direction */
                 pend[t] = 0; key_of[t] = INFINITY;
                 for (int x = -1; x <= TS; ++x) { W[k].L[0][x + 1] = at(y0 - 1, x0 + x); W[k].L[TS + 1][x + 1] = at(y0 + TS, x0 + x); }
                 for (int y = 0; y < TS; ++y) { W[k].L[y + 1][0] = at(y0 + y, x0 - 1); W[k].L[y + 1][TS + 1] = at(y0 + y, x0 + TS); }
@@ -136,8 +140,10 @@ int main(int argc, char** argv) {
             if (W[k].t < 0) continue;
             ++npass; ++W[k].p;
             float (*L)[TS + 2] = W[k].L, (*C)[TS + 2] = W[k].C;
-            int ch = 0;
+            int ch = 0, chd[4] = {0, 0, 0, 0};
             for (int d = 0; d < 4; ++d) {
+                if (skipdir && W[k].last == d) continue;
+                ++dsweeps;
                 int sx = (d & 1) ? -1 : 1, sy = (d & 2) ? -1 : 1;
                 for (int yy = 0; yy < TS; ++yy) {
                     int y = (sy > 0 ? yy : TS - 1 - yy) + 1;
@@ -145,11 +151,12 @@ int main(int argc, char** argv) {
                         int x = (sx > 0 ? xx : TS - 1 - xx) + 1;
                         float a = oneside ? L[y][x - sx] : fminf(L[y][x - 1], L[y][x + 1]), b = oneside ? L[y - sy][x] : fminf(L[y - 1][x], L[y + 1][x]);
                         float w = god(a, b, C[y][x]);
-                        if (w < L[y][x]) { L[y][x] = w; ch = 1; }
+                        if (w < L[y][x]) { L[y][x] = w; ch = 1; chd[d] = 1; }
                     }
                 }
             }
             changed[k] = ch;
+            W[k].last = (chd[0] + chd[1] + chd[2] + chd[3] == 1) ? (chd[1] ? 1 : chd[2] ? 2 : chd[3] ? 3 : 0) : -1;
         }
         /* round end: write back, activate, release */
         for (int k = 0; k < K; ++k) {
@@ -185,7 +192,7 @@ int main(int argc, char** argv) {
     }
     double s = 0; long fin = 0;
     for (size_t i = 0; i < (size_t)N * N; ++i) if (isfinite(T[i])) { s += T[i]; ++fin; }
-    printf("policy %d passes %d K %d: rounds %ld visits %ld passes %ld (%.2f/tile) avg busy %.0f checksum %.6e finite %ld\n", policy,
-           maxp, K, rounds, visits, npass, (double)npass / nt, (double)busy_sum / rounds, s, fin);
+    printf("policy %d passes %d K %d: rounds %ld visits %ld passes %ld (%.2f/tile) sweeps %ld avg busy %.0f checksum %.6e finite %ld\n", policy,
+           maxp, K, rounds, visits, npass, (double)npass / nt, dsweeps, (double)busy_sum / rounds, s, fin);
     return 0;
 }
