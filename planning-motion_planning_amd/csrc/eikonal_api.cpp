@@ -335,12 +335,12 @@ int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
     // throughput-bound: 16 passes, 17.1-17.3 -> 18.3-18.9 Gcells/s (profiles/r02w_passes_wide.log).
     // A few large maps (biComputeTmap's two fronts: B = 2 of 4096^2) are latency-bound like one map.
     const bool batch = f->B > 4 || (f->B > 1 && f->a.tiles_per_map < 1024);
-    // One fp64 map: 40 (profiles/r03v_passes_f64_c2_ab.log: C2 fp64 2.467 ms at 24, 2.40-2.44 at 32-64).
+    // One map (round 3, profiles/r03v_passes_f64_c2_ab.log): 40 -- C2 fp64 2.461-2.468 ms at 24,
+    // 2.394-2.420 at 40; fp32 1.733-1.748 at 24, 1.723-1.726 at 40.
     f->a.max_passes = c->passes > 0 ? c->passes
                       : batch                                             ? 2
                       : (!f->f64 && f->a.tiles_per_map >= kWideTiles)     ? 16
-                      : f->f64                                            ? 40
-                                                                          : 24;
+                                                                          : 40;
     f->a.qbudget = c->max_visits ? c->max_visits : 1024ull * (unsigned long long)(f->B * f->a.tiles_per_map) + (1ull << 20);
     f->iterations = 0;
     f->host_syncs = 0;
