@@ -10,8 +10,11 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/eikonal.h"
@@ -50,6 +53,71 @@ struct DevBuf {
     }
 };
 
+// Host memcpy split over a few worker threads and the caller (the pinned-staging copies below).
+class CopyPool {
+  public:
+    explicit CopyPool(int workers) {
+        for (int i = 0; i < workers; ++i) th_.emplace_back([this] { loop(); });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            quit_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    void copy(void* dst, const void* src, size_t len) {
+        const int parts = (int)th_.size() + 1;
+        {
+            std::lock_guard<std::mutex> g(m_);
+            dst_ = static_cast<char*>(dst);
+            src_ = static_cast<const char*>(src);
+            len_ = len;
+            parts_ = parts;
+            next_ = 1;  // part 0 is the caller's
+            left_ = parts - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        part(0, parts);
+        std::unique_lock<std::mutex> lk(m_);
+        done_.wait(lk, [&] { return left_ == 0; });
+    }
+
+  private:
+    void part(int k, int parts) {
+        const size_t a = len_ * k / parts, e = len_ * (k + 1) / parts;
+        std::memcpy(dst_ + a, src_ + a, e - a);
+    }
+    void loop() {
+        for (;;) {
+            int k, parts;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return quit_ || next_ < parts_; });
+                if (quit_) return;
+                k = next_++;
+                parts = parts_;
+            }
+            part(k, parts);
+            {
+                std::lock_guard<std::mutex> g(m_);
+                if (--left_ == 0) done_.notify_one();
+            }
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    char* dst_ = nullptr;
+    const char* src_ = nullptr;
+    size_t len_ = 0;
+    int parts_ = 0, next_ = 0, left_ = 0;
+    unsigned long long gen_ = 0;
+    bool quit_ = false;
+};
+
 }  // namespace
 
 struct eik_ctx {
@@ -86,6 +154,10 @@ struct eik_ctx {
     unsigned* h_q3 = nullptr;          // pinned copy of q3ctl + the two visit counters
     int resident3[2] = {0, 0};         // co-resident workgroups of fim3d_persist_kernel (f32, f64)
     hipStream_t stream2 = nullptr;     // second stream: the rover path's two walks run side by side
+    // pinned staging of large host <-> device copies (host_to_dev / dev_to_host)
+    char* stage[2] = {nullptr, nullptr};
+    hipEvent_t stage_ev[2] = {nullptr, nullptr};
+    CopyPool* pool = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     hipEvent_t e3[2] = {nullptr, nullptr};
 };
@@ -139,6 +211,69 @@ static int bytes_per_visit(bool f64) { return (f64 ? 8 : 4) * (3 * kTile * kTile
 // in-place pass of a busy tile (persistent mode): T write-back + halo ring re-read
 static int bytes_per_pass(bool f64) { return (f64 ? 8 : 4) * (kTile * kTile + 4 * kTile); }
 
+// Large host <-> device copies through a pinned ring of two 8 MiB chunks, host memcpy by a few
+// threads overlapped with the DMA of the other chunk.  A pageable hipMemcpyAsync of a FRESH host
+// buffer (every numpy array the drop-in receives or returns) ran at ~8 GB/s: 16 ms per 128 MiB,
+// 3 ms only once the runtime had seen the buffer; staged: ~4 ms either way (tools/h2d_probe.cpp).
+// host_to_dev returns once the source has been read (the DMA of the last chunk may still run on
+// st); dev_to_host returns with the data in dst (it waits for st's earlier work).
+constexpr size_t kStageChunk = 8ull << 20;
+static hipError_t stage_init(eik_ctx* c) {
+    for (int b = 0; b < 2; ++b) {
+        if (!c->stage[b]) {
+            hipError_t e = hipHostMalloc((void**)&c->stage[b], kStageChunk);
+            if (e != hipSuccess) return e;
+        }
+        if (!c->stage_ev[b]) {
+            hipError_t e = hipEventCreateWithFlags(&c->stage_ev[b], hipEventDisableTiming);
+            if (e != hipSuccess) return e;
+        }
+    }
+    if (!c->pool) c->pool = new CopyPool((int)std::max(1u, std::min(3u, std::thread::hardware_concurrency() / 2)));
+    return hipSuccess;
+}
+static hipError_t host_to_dev(eik_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st) {
+    if (bytes < 2 * kStageChunk) return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
+    hipError_t e = stage_init(c);
+    if (e != hipSuccess) return e;
+    int k = 0;
+    for (size_t off = 0; off < bytes; off += kStageChunk, ++k) {
+        const int b = k & 1;
+        const size_t len = std::min(kStageChunk, bytes - off);
+        if ((e = hipEventSynchronize(c->stage_ev[b])) != hipSuccess) return e;  // its last DMA is done
+        c->pool->copy(c->stage[b], static_cast<const char*>(src) + off, len);
+        if ((e = hipMemcpyAsync(static_cast<char*>(dst) + off, c->stage[b], len, hipMemcpyHostToDevice, st)) != hipSuccess)
+            return e;
+        if ((e = hipEventRecord(c->stage_ev[b], st)) != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+static hipError_t dev_to_host(eik_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st) {
+    if (bytes < 2 * kStageChunk) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st);
+    hipError_t e = stage_init(c);
+    if (e != hipSuccess) return e;
+    const size_t nch = (bytes + kStageChunk - 1) / kStageChunk;
+    // a host_to_dev on another stream may still be reading the staging buffers
+    for (int b = 0; b < 2; ++b)
+        if ((e = hipStreamWaitEvent(st, c->stage_ev[b], 0)) != hipSuccess) return e;
+    auto issue = [&](size_t k) -> hipError_t {
+        const int b = (int)(k & 1);
+        const size_t off = k * kStageChunk, len = std::min(kStageChunk, bytes - off);
+        hipError_t r = hipMemcpyAsync(c->stage[b], static_cast<const char*>(src) + off, len, hipMemcpyDeviceToHost, st);
+        return r == hipSuccess ? hipEventRecord(c->stage_ev[b], st) : r;
+    };
+    if ((e = issue(0)) != hipSuccess) return e;
+    for (size_t k = 0; k < nch; ++k) {
+        // the next chunk's DMA lands in the buffer chunk k - 1 used, already copied out
+        if (k + 1 < nch && (e = issue(k + 1)) != hipSuccess) return e;
+        const int b = (int)(k & 1);
+        if ((e = hipEventSynchronize(c->stage_ev[b])) != hipSuccess) return e;
+        const size_t off = k * kStageChunk;
+        c->pool->copy(static_cast<char*>(dst) + off, c->stage[b], std::min(kStageChunk, bytes - off));
+    }
+    return hipSuccess;
+}
+
 extern "C" {
 
 const char* eik_version(void) { return "eikonal-mi355x 0.1 (gfx950 block-FIM, 64x64 tiles)"; }
@@ -178,6 +313,11 @@ void eik_destroy(eik_ctx* c) {
     for (hipEvent_t e : c->e3)
         if (e) (void)hipEventDestroy(e);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
+    for (int b = 0; b < 2; ++b) {
+        if (c->stage[b]) (void)hipHostFree(c->stage[b]);
+        if (c->stage_ev[b]) (void)hipEventDestroy(c->stage_ev[b]);
+    }
+    delete c->pool;
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -726,10 +866,10 @@ static int tmap_host(eik_ctx* c, const R* cost, int64_t B, int64_t H, int64_t W,
     if (rc) return rc;
     HIPCHK(c, c->cost.ensure(sizeof(R) * n));
     HIPCHK(c, c->T.ensure(sizeof(R) * n));
-    HIPCHK(c, hipMemcpyAsync(c->cost.p, cost, sizeof(R) * n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, host_to_dev(c, c->cost.p, cost, sizeof(R) * n, c->stream));
     rc = eik_fim2d_solve(f, c->cost.p, c->T.p, goals, c->stream);
     if (rc) return rc;
-    HIPCHK(c, hipMemcpyAsync(T, c->T.p, sizeof(R) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, dev_to_host(c, T, c->T.p, sizeof(R) * n, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return EIK_OK;
 }
@@ -773,7 +913,7 @@ int eik_tmap2d_bidir_f64(eik_ctx* c, const double* cost, int64_t H, int64_t W, i
     HIPCHK(c, c->cost.ensure(sizeof(double) * 2 * n));
     HIPCHK(c, c->T.ensure(sizeof(double) * 2 * n));
     double* dcost = (double*)c->cost.p;
-    HIPCHK(c, hipMemcpyAsync(dcost, cost, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, host_to_dev(c, dcost, cost, sizeof(double) * n, c->stream));
     HIPCHK(c, hipMemcpyAsync(dcost + n, dcost, sizeof(double) * n, hipMemcpyDeviceToDevice, c->stream));
     rc = eik_fim2d_solve(f, dcost, c->T.p, goals, c->stream);
     if (rc) return rc;
@@ -788,8 +928,8 @@ int eik_tmap2d_bidir_f64(eik_ctx* c, const double* cost, int64_t H, int64_t W, i
                             (const unsigned long long*)c->misc.p, c->stream));
     unsigned long long best = 0;
     HIPCHK(c, hipMemcpyAsync(&best, c->misc.p, sizeof best, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(TG, c->T.p, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(TS, (double*)c->T.p + n, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, dev_to_host(c, TG, c->T.p, sizeof(double) * n, c->stream));
+    HIPCHK(c, dev_to_host(c, TS, (double*)c->T.p + n, sizeof(double) * n, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (best == ~0ull) return set_err(c, EIK_ERR_UNREACHABLE, "goal and start are not connected");
     const int64_t node = (int64_t)(best & ((1ull << 29) - 1));
@@ -843,7 +983,7 @@ int eik_path2d_f64(eik_ctx* c, const double* T, int64_t H, int64_t W, const doub
     const int64_t n = H * W;
     HIPCHK(c, c->T2.ensure(sizeof(double) * n));
     HIPCHK(c, c->work.ensure(sizeof(double) * 2 * cap + 64));
-    HIPCHK(c, hipMemcpyAsync(c->T2.p, T, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, host_to_dev(c, c->T2.p, T, sizeof(double) * n, c->stream));
     double* d_out = (double*)c->work.p;
     int64_t* d_n = (int64_t*)(d_out + 2 * cap);
     int* d_st = (int*)(d_n + 1);
@@ -1160,7 +1300,7 @@ static int tmap3d_host(eik_ctx* c, const R* cost, int64_t H, int64_t W, int64_t 
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, c->cost.ensure(sizeof(R) * n));
     HIPCHK(c, c->T.ensure(sizeof(R) * n));
-    HIPCHK(c, hipMemcpyAsync(c->cost.p, cost, sizeof(R) * n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, host_to_dev(c, c->cost.p, cost, sizeof(R) * n, c->stream));
     const int dt = sizeof(R) == 8 ? EIK_F64 : EIK_F32;
     rc = fim3d_solve_one(c, c->cost.p, c->T.p, H, W, L, dt, goal, c->stream, early_offset(goal, start, H, W, L));
     if (rc) return rc;
@@ -1171,7 +1311,7 @@ static int tmap3d_host(eik_ctx* c, const R* cost, int64_t H, int64_t W, int64_t 
         if (rc) return rc;
         src = c->T2.p;
     }
-    HIPCHK(c, hipMemcpyAsync(T, src, sizeof(R) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, dev_to_host(c, T, src, sizeof(R) * n, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return EIK_OK;
 }
@@ -1241,7 +1381,7 @@ int eik_path3d_f64(eik_ctx* c, const double* T, int64_t H, int64_t W, int64_t L,
     const int64_t n = H * W * L;
     HIPCHK(c, c->T2.ensure(sizeof(double) * n));
     HIPCHK(c, c->work.ensure(sizeof(double) * 3 * cap + 64));
-    HIPCHK(c, hipMemcpyAsync(c->T2.p, T, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, host_to_dev(c, c->T2.p, T, sizeof(double) * n, c->stream));
     double* d_out = (double*)c->work.p;
     int64_t* d_n = (int64_t*)(d_out + 3 * cap);
     int* d_st = (int*)(d_n + 1);
@@ -1265,11 +1405,11 @@ int eik_gradient2d_f64(eik_ctx* c, const double* T, int64_t H, int64_t W, double
     const int64_t n = H * W;
     HIPCHK(c, c->T2.ensure(sizeof(double) * n));
     HIPCHK(c, c->work.ensure(sizeof(double) * 2 * n));
-    HIPCHK(c, hipMemcpyAsync(c->T2.p, T, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, host_to_dev(c, c->T2.p, T, sizeof(double) * n, c->stream));
     double* gx = (double*)c->work.p;
     HIPCHK(c, gradient2d((const double*)c->T2.p, H, W, gx, gx + n, c->stream));
-    HIPCHK(c, hipMemcpyAsync(gnx, gx, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(gny, gx + n, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, dev_to_host(c, gnx, gx, sizeof(double) * n, c->stream));
+    HIPCHK(c, dev_to_host(c, gny, gx + n, sizeof(double) * n, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return EIK_OK;
 }
@@ -1362,11 +1502,11 @@ int eik_costmap_f64(eik_ctx* c, const double* Z, int64_t H, int64_t W, double re
     double* dZ = (double*)c->T2.p;
     double* dC = dZ + n;
     uint8_t* dO = (uint8_t*)(dC + n);
-    HIPCHK(c, hipMemcpyAsync(dZ, Z, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, host_to_dev(c, dZ, Z, sizeof(double) * n, c->stream));
     int rc = eik_costmap_dev(c, dZ, H, W, res, size, params, dC, dO, c->stream);
     if (rc) return rc;
-    HIPCHK(c, hipMemcpyAsync(cost_out, dC, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
-    if (obst_out) HIPCHK(c, hipMemcpyAsync(obst_out, dO, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, dev_to_host(c, cost_out, dC, sizeof(double) * n, c->stream));
+    if (obst_out) HIPCHK(c, dev_to_host(c, obst_out, dO, n, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return EIK_OK;
 }
@@ -1380,11 +1520,11 @@ int eik_surface_normal_f64(eik_ctx* c, const double* Z, int64_t H, int64_t W, do
     HIPCHK(c, c->T2.ensure(sizeof(double) * 4 * n + 64));
     double* dZ = (double*)c->T2.p;
     unsigned long long* red = (unsigned long long*)(dZ + 4 * n);
-    HIPCHK(c, hipMemcpyAsync(dZ, Z, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, host_to_dev(c, dZ, Z, sizeof(double) * n, c->stream));
     HIPCHK(c, cm_normals(dZ, H, W, size, red, 0.0, nullptr, dZ + n, dZ + 2 * n, dZ + 3 * n, c->stream));
-    HIPCHK(c, hipMemcpyAsync(Nx, dZ + n, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(Ny, dZ + 2 * n, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(Nz, dZ + 3 * n, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, dev_to_host(c, Nx, dZ + n, sizeof(double) * n, c->stream));
+    HIPCHK(c, dev_to_host(c, Ny, dZ + 2 * n, sizeof(double) * n, c->stream));
+    HIPCHK(c, dev_to_host(c, Nz, dZ + 3 * n, sizeof(double) * n, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return EIK_OK;
 }
@@ -1396,11 +1536,11 @@ int eik_image_fill_u8(eik_ctx* c, const uint8_t* im, int64_t H, int64_t W, uint8
     HIPCHK(c, c->cm_u8.ensure(3 * n + 64));
     HIPCHK(c, c->cm_f32.ensure(sizeof(float) * 2 * n));
     unsigned char* m = (unsigned char*)c->cm_u8.p;
-    HIPCHK(c, hipMemcpyAsync(m, im, n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, host_to_dev(c, m, im, n, c->stream));
     float* fcost = (float*)c->cm_f32.p;
     int rc = cm_fill(c, m, H, W, fcost, fcost + n, c->stream);
     if (rc) return rc;
-    HIPCHK(c, hipMemcpyAsync(out, m, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, dev_to_host(c, out, m, n, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return EIK_OK;
 }
@@ -1433,12 +1573,12 @@ int eik_rover_path_f64(eik_ctx* c, const double* Z, int64_t H, int64_t W, const 
     double* dZ = (double*)c->T2.p;
     double* dcost = (double*)c->cost.p;
     double* dT = (double*)c->T.p;
-    HIPCHK(c, hipMemcpyAsync(dZ, Z, sizeof(double) * n, hipMemcpyHostToDevice, st));
+    HIPCHK(c, host_to_dev(c, dZ, Z, sizeof(double) * n, st));
     int rc = eik_costmap_dev(c, dZ, H, W, res, q->size, params, dcost, nullptr, st);  // :1101-1216
     if (rc) return rc;
     // biComputeTmap(cMap.T, goal = sample node, start = rover node)   :1222; both fronts, one batch
     HIPCHK(c, hipMemcpyAsync(dcost + n, dcost, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
-    if (cost_out) HIPCHK(c, hipMemcpyAsync(cost_out, dcost, sizeof(double) * n, hipMemcpyDeviceToHost, st));
+    if (cost_out) HIPCHK(c, dev_to_host(c, cost_out, dcost, sizeof(double) * n, st));
     eik_fim2d* f = nullptr;
     rc = get_solver(c, 2, H, W, EIK_F64, &f);
     if (rc) return rc;
@@ -1688,15 +1828,15 @@ int eik_arm_obst_map_f64(eik_ctx* c, const double* Z, const double* obst, int64_
     double* dF = dO + nz;
     double* dOm = omap ? dF + nc : nullptr;
     double* dGm = gmap ? dF + 2 * nc : nullptr;
-    HIPCHK(c, hipMemcpyAsync(dZ, Z, sizeof(double) * nz, hipMemcpyHostToDevice, st));
-    HIPCHK(c, hipMemcpyAsync(dO, obst, sizeof(double) * nz, hipMemcpyHostToDevice, st));
+    HIPCHK(c, host_to_dev(c, dZ, Z, sizeof(double) * nz, st));
+    HIPCHK(c, host_to_dev(c, dO, obst, sizeof(double) * nz, st));
     rc = arm_volume_dev(c, dZ, dO, m, n, nullptr, nullptr, 0, v, dF, dOm, dGm, nullptr, nullptr, st);
     if (rc) return rc;
     unsigned bad = 0;
     HIPCHK(c, hipMemcpyAsync(&bad, c->misc.p, sizeof bad, hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipMemcpyAsync(fmap, dF, sizeof(double) * nc, hipMemcpyDeviceToHost, st));
-    if (omap) HIPCHK(c, hipMemcpyAsync(omap, dOm, sizeof(double) * nc, hipMemcpyDeviceToHost, st));
-    if (gmap) HIPCHK(c, hipMemcpyAsync(gmap, dGm, sizeof(double) * nc, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, dev_to_host(c, fmap, dF, sizeof(double) * nc, st));
+    if (omap) HIPCHK(c, dev_to_host(c, omap, dOm, sizeof(double) * nc, st));
+    if (gmap) HIPCHK(c, dev_to_host(c, gmap, dGm, sizeof(double) * nc, st));
     HIPCHK(c, hipStreamSynchronize(st));
     if (bad) return set_err(c, EIK_ERR_ARG, "GetObstMap: a surface index below -sZ (the reference raises IndexError)");
     return EIK_OK;
@@ -1714,7 +1854,7 @@ int eik_arm_tunnel_cost_f64(eik_ctx* c, const double* gamma2D, const double* hea
     rc = arm_volume_dev(c, nullptr, nullptr, 0, 0, gamma2D, heading, npts, v, nullptr, nullptr, nullptr, dT, nullptr,
                         c->stream);
     if (rc) return rc;
-    HIPCHK(c, hipMemcpyAsync(Cmap, dT, sizeof(double) * nc, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, dev_to_host(c, Cmap, dT, sizeof(double) * nc, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return EIK_OK;
 }
@@ -1750,8 +1890,8 @@ int eik_arm_path_f64(eik_ctx* c, const double* Z, const double* obst, int64_t m,
     double* dP = dT + nc;
     int64_t* dn = (int64_t*)(dP + 3 * pcap);
     int* dst = (int*)(dn + 1);
-    HIPCHK(c, hipMemcpyAsync(dZ, Z, sizeof(double) * nz, hipMemcpyHostToDevice, st));
-    HIPCHK(c, hipMemcpyAsync(dO, obst, sizeof(double) * nz, hipMemcpyHostToDevice, st));
+    HIPCHK(c, host_to_dev(c, dZ, Z, sizeof(double) * nz, st));
+    HIPCHK(c, host_to_dev(c, dO, obst, sizeof(double) * nz, st));
     rc = arm_volume_dev(c, dZ, dO, m, n, gamma2D, heading, npts, v, dF, nullptr, nullptr, dTun, dC, st);
     if (rc) return rc;
     // FM3D.computeTmap(Cmap, finalWayPointArm, initialWayPointArm) :1585; H = sY rows, W = sX columns
@@ -1774,8 +1914,8 @@ int eik_arm_path_f64(eik_ctx* c, const double* Z, const double* obst, int64_t m,
     HIPCHK(c, hipStreamSynchronize(st));
     *n_out = hn;
     HIPCHK(c, hipMemcpyAsync(path, dP, sizeof(double) * 3 * hn, hipMemcpyDeviceToHost, st));
-    if (cost_out) HIPCHK(c, hipMemcpyAsync(cost_out, dC, sizeof(double) * nc, hipMemcpyDeviceToHost, st));
-    if (T_out) HIPCHK(c, hipMemcpyAsync(T_out, dT, sizeof(double) * nc, hipMemcpyDeviceToHost, st));
+    if (cost_out) HIPCHK(c, dev_to_host(c, cost_out, dC, sizeof(double) * nc, st));
+    if (T_out) HIPCHK(c, dev_to_host(c, T_out, dT, sizeof(double) * nc, st));
     HIPCHK(c, hipStreamSynchronize(st));
     return EIK_OK;
 }
@@ -1794,10 +1934,10 @@ int eik_tmap3d_batch_f64(eik_ctx* c, const double* cost, int64_t B, int64_t H, i
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, c->cost.ensure(sizeof(double) * n));
     HIPCHK(c, c->T.ensure(sizeof(double) * n));
-    HIPCHK(c, hipMemcpyAsync(c->cost.p, cost, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, host_to_dev(c, c->cost.p, cost, sizeof(double) * n, c->stream));
     rc = fim3d_solve_batch(c, c->cost.p, c->T.p, B, H, W, L, EIK_F64, goals, c->stream);
     if (rc) return rc;
-    HIPCHK(c, hipMemcpyAsync(T, c->T.p, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, dev_to_host(c, T, c->T.p, sizeof(double) * n, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return EIK_OK;
 }

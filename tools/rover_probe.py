@@ -18,8 +18,9 @@ for opts in os.environ.get("OPTS_LIST", ",PASSES=8,PASSES=24,,PASSES=8,PASSES=24
     ctx.rover_path(Zh, q)
     ts = []
     for _ in range(3):
+        Zc = Zh.copy() if os.environ.get("FRESH") else Zh  # a fresh host array per plan, as the planner reads one
         t0 = time.perf_counter()
-        r = ctx.rover_path(Zh, q)
+        r = ctx.rover_path(Zc, q)
         ts.append((time.perf_counter() - t0) * 1e3)
     print(f"{opts or 'default'}: {np.median(ts):.2f} ms, waypoints {len(r[0])}, join {list(r[2])}", flush=True)
     ctx.close()
@@ -31,9 +32,10 @@ cost = np.ascontiguousarray(cMap.T)
 gx, gy = 2048, 2048
 sx, sy = 256, 256
 ctx = eikonal.Context(0)
-for rep in range(2):
+for rep in range(3):
+    cc = cost.copy() if os.environ.get("FRESH") else cost
     t0 = time.perf_counter()
-    ctx.tmap2d_bidir(cost, (gx, gy), (sx, sy))
+    ctx.tmap2d_bidir(cc, (gx, gy), (sx, sy))
     s = ctx.stats()
     print(f"bidir batch: wall {(time.perf_counter() - t0) * 1e3:.2f} ms, solve {s['solve_ms']:.2f} ms, visits "
           f"{s['tile_visits']}, in-place {s['inplace_passes']}", flush=True)
