@@ -164,6 +164,8 @@ hipError_t cm_fill_cost(const unsigned char* m, int64_t n, float* c, hipStream_t
 hipError_t cm_fill_apply(unsigned char* m, const float* T, int64_t n, hipStream_t st);
 // the same fill by connected components (union-find; lroot, parent: n ints of scratch)
 hipError_t cm_fill_ccl(unsigned char* m, int64_t H, int64_t W, int* lroot, int* parent, hipStream_t st);
+// first index with cost < 0 or NaN into *first (~0: none); costmap.hip
+hipError_t cost_check(const void* cost, int64_t n, bool f64, unsigned long long* first, hipStream_t st);
 hipError_t cm_border(unsigned char* m, int64_t H, int64_t W, unsigned char v, hipStream_t st);
 hipError_t cm_cost(const unsigned char* obst, const unsigned char* dil, const int* Dobst, int64_t H, int64_t W,
                    double res, double high, double gradient, double* work, double* tmp, double* cost,

@@ -136,6 +136,9 @@ enum { kGdmDone = 0, kGdmFallback = 1, kGdmError = 2 };
 #define EIK_P3DECL ((void)0)
 #define EIK_P3FLUSH ((void)0)
 #endif
+#ifndef EIK_P3RUN
+#define EIK_P3RUN 1  // the 3D walker's integer-descent run loop (gdm3d_kernel)
+#endif
 #ifndef EIK_P2PROBE
 #define EIK_P2PROBE(k) ((void)0)  // 2D walker phase timing hooks (tools/path2_prof.hip)
 #define EIK_P2DECL ((void)0)
@@ -735,6 +738,15 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
+// v from lane - SH of the same 16-lane row (DPP row_shr); lanes with no source keep their own
+template <int SH>
+__device__ __forceinline__ double row_shr_f64(double v) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp((int)(unsigned)b, (int)(unsigned)b, 0x110 + SH, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(unsigned)(b >> 32), (int)(unsigned)(b >> 32), 0x110 + SH, 0xf, 0xf, false);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
 // window origin along one axis: the needed span [lo, hi] (clipped to the volume) centred in a
 // window of n cells that stays inside [0, len)
 __device__ __forceinline__ int64_t win_origin(int64_t lo, int64_t hi, int n, int64_t len) {
@@ -853,8 +865,108 @@ __global__ __launch_bounds__(kP3Threads) void gdm3d_kernel(Gdm3dArgs a) {
         for (int c = 0; c < 3; ++c) mstep[q][c] = nrm < 0.01 ? tau * (ustep[q][c] / nrm) : tau * ustep[q][c];
     }
     double p2x = 0.0, p2y = 0.0, p2z = 0.0;  // path point n - 2 (point n - 1 is (gx, gy, gz))
+    // the descent's moves are exact unit steps (tau * (-off / tau) == -off, e.g. tau = 0.5): after
+    // an integer-node step the walk stays on nodes, and the run loop below takes the next ones
+    bool int_moves = EIK_P3RUN != 0;
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+        for (int c = 0; c < 3; ++c) int_moves &= mstep[q][c] == (double)(-off[q][c]);
+    bool run = false;  // the previous step was an integer-node step and int_moves holds
     EIK_P3DECL;
     for (long k = 0; k < a.steps; ++k) {
+        // Integer-descent run (the C5 regime).  After an integer-node step from node M to its
+        // neighbour N the step at N, as the general body below takes it, is: the point test of
+        // :238-240 pops N itself (distance 0) but not M (distance exactly 1), puts N back where
+        // it was (the same value in the same slot), and -- when the fallback is taken (a T sample
+        // of the gradient not finite, T[N] finite, every neighbour in range: an interior node) and
+        // some neighbour is lower -- appends N + off[best] (the tail's N - mstep[best], exact).
+        // The run loop does exactly that on scalar node coordinates; any other case (window
+        // bookkeeping due, a face node, no lower neighbour, the point budget) leaves it for the
+        // general body of the same step.
+        if (run) {
+            // every value the loop branches on is wave-uniform and held in scalar registers (the
+            // window bounds come from the general body's VALU conversions: read them once)
+            auto rfl = [](int q) { return __builtin_amdgcn_readfirstlane(q); };
+            auto rfl64 = [](int64_t q) {
+                return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)((uint64_t)q >> 32)) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readfirstlane((int)q));
+            };
+            int x = rfl((int)gx), y = rfl((int)gy), z = rfl((int)gz);
+            const int wy0 = rfl((int)v.y0), wx0 = rfl((int)v.x0), wz0 = rfl((int)v.z0);
+            // the fast window bounds and the interior test in one range per axis
+            const int ylo = rfl(bj_lo > 1 ? bj_lo : 1), yhi = rfl(bj_hi < (int)H - 2 ? bj_hi : (int)H - 2);
+            const int xlo = rfl(bi_lo > 1 ? bi_lo : 1), xhi = rfl(bi_hi < (int)W - 2 ? bi_hi : (int)W - 2);
+            const int zlo = rfl(bk_lo > 1 ? bk_lo : 1), zhi = rfl(bk_hi < (int)L - 2 ? bk_hi : (int)L - 2);
+            const int len = g_ax == 0 ? (int)H : g_ax == 1 ? (int)W : (int)L;  // lanes 0..23: the sample axis
+            const int lane_xyz = g_ax;  // which coordinate a gradient lane's corner runs along
+            const bool node_lane = lane >= 24 && lane < 31;
+            const R* w = v.w;
+            int64_t nn = rfl64(n), ll = rfl64(lo), kq = rfl64((int64_t)k);
+            const int64_t cap = a.cap, steps = a.steps;
+            bool fin = false, moved = false;
+            int xp = 0, yp = 0, zp = 0;
+            for (;;) {
+                if (y < ylo || y > yhi || x < xlo || x > xhi || z < zlo || z > zhi) break;
+                const int base = ((y - wy0) * v.WX + (x - wx0)) * v.WZ + (z - wz0);
+                const int pc = (lane_xyz == 0 ? y : lane_xyz == 1 ? x : z) + g_c;  // >= 1: never the first
+                const int idx = base + g_off;
+                const R r_hi = w[idx + (pc == len - 1 ? 0 : g_str)];
+                const R r_lo = w[idx - g_str];
+                const double t_hi = (double)r_hi;
+                const unsigned long long nonfin =
+                    __ballot(lane < 24 && !(__builtin_isfinite(r_hi) && __builtin_isfinite(r_lo)));
+                const double tnode = readlane_f64(t_hi, 24);
+                // T[N] +inf (the general body's fallback test) or NaN (its ordered scan below never
+                // moves; the minimum below would skip the NaN): the general body
+                if (nonfin == 0ull || !(tnode < __builtin_inf())) break;
+                // The reference's ordered scan (curT = T[N]; `if T[nb] < curT` over the six
+                // neighbours) picks the FIRST neighbour attaining the minimum, if that minimum is
+                // below T[N].  As a lane minimum over lanes 24..30 (the node first: a tie with it
+                // keeps the node) and the lowest lane holding it; NaN neighbours are never taken by
+                // either (v_min_f64 returns the other operand, NaN == m is false).
+                double mv = node_lane ? t_hi : __builtin_inf();
+                mv = __builtin_fmin(mv, row_shr_f64<1>(mv));
+                mv = __builtin_fmin(mv, row_shr_f64<2>(mv));
+                mv = __builtin_fmin(mv, row_shr_f64<4>(mv));
+                const double m = readlane_f64(mv, 30);  // row_shr 1, 2, 4: lanes 23..30, lane 23 +inf
+                const unsigned long long eq = __ballot(node_lane && t_hi == m);
+                const int best = rfl(__builtin_ctzll(eq) - 25);  // -1: the node itself
+                if (best < 0 || nn >= cap) break;
+                const int nx = x + (best == 2 ? -1 : best == 3 ? 1 : 0);
+                const int ny = y + (best == 0 ? -1 : best == 1 ? 1 : 0);
+                const int nz = z + (best == 4 ? -1 : best == 5 ? 1 : 0);
+                put(nn, (double)nx, (double)ny, (double)nz);
+                ++nn;
+                if (nn - ll > kRing) ll = nn - kRing;
+                moved = true;
+                xp = x;
+                yp = y;
+                zp = z;
+                x = nx;
+                y = ny;
+                z = nz;
+                if (sq3((double)nx - a.end[0], (double)ny - a.end[1], (double)nz - a.end[2]) < 2.25) {
+                    fin = true;  // :266-267
+                    break;
+                }
+                if (++kq >= steps) {
+                    fin = true;
+                    break;
+                }
+            }
+            n = nn;
+            lo = ll;
+            k = (long)kq;
+            if (moved) {  // the last two points: the current node and the node before it
+                p2x = (double)xp;
+                p2y = (double)yp;
+                p2z = (double)zp;
+                gx = (double)x;
+                gy = (double)y;
+                gz = (double)z;
+            }
+            if (fin) break;
+        }
         EIK_P3PROBE(3);
         const uint32_t i = cvt_u32(gx), j = cvt_u32(gy), kk = cvt_u32(gz);
         if (i + 1 >= (uint64_t)W || j + 1 >= (uint64_t)H || kk + 1 >= (uint64_t)L) { status = kGdmError; break; }
@@ -1109,6 +1221,7 @@ __global__ __launch_bounds__(kP3Threads) void gdm3d_kernel(Gdm3dArgs a) {
         gz = az;
         if (__builtin_isnan(ax) || __builtin_isnan(ay) || __builtin_isnan(az)) { status = kGdmError; break; }
         if (sq3(ax - a.end[0], ay - a.end[1], az - a.end[2]) < 2.25) break;  // :266-267
+        run = int_moves && intstep;
     }
     if (pending) wait_built();  // no build may still be writing when the builders are told to quit
     __hip_atomic_store(&sl.req_seq, -1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);

@@ -156,6 +156,35 @@ def test_bad_inputs_raise(ctx):
         ctx.tmap2d(c, [1, 1])
 
 
+def test_bad_cost_reports_first_index(ctx):
+    """The cost check runs on the device copy (one kernel, an 8-byte read-back) in every host
+    entry that takes a cost array: EIK_ERR_ARG naming the FIRST bad index and its value, and the
+    context stays usable afterwards."""
+    import eikonal
+    from eikonal import _lib as L
+
+    rng = np.random.default_rng(3)
+    c = rng.uniform(1, 2, (300, 500))
+    c[250, 7] = -2.0
+    c[41, 333] = np.nan  # first in row-major order: 41 * 500 + 333
+    c[200, 100] = -0.5
+    want = f"cost[{41 * 500 + 333}] = nan"
+    calls = [lambda: ctx.tmap2d(c, [1, 1]), lambda: ctx.tmap2d(c.astype(np.float32), [1, 1], dtype=np.float32),
+             lambda: ctx.tmap2d_batch(np.stack([np.ones_like(c), c]), [[1, 1], [2, 2]]),
+             lambda: ctx.tmap2d_bidir(c, [1, 1], [400, 290]),
+             lambda: ctx.tmap3d(c.reshape(300, 50, 10), [1, 1, 1]),
+             lambda: ctx.tmap3d_batch(c.reshape(1, 300, 50, 10), [[1, 1, 1]])]
+    for k, call in enumerate(calls):
+        with pytest.raises(eikonal.EikError) as e:
+            call()
+        assert e.value.code == L.EIK_ERR_ARG
+        w = want if k != 2 else f"cost[{300 * 500 + 41 * 500 + 333}] = nan"
+        assert w in str(e.value), (k, str(e.value))
+    ok = np.ones((40, 60))
+    T = ctx.tmap2d(ok, [0, 0])
+    assert T[0, 0] == 0 and np.isfinite(T).all()
+
+
 def test_batch_matches_single(ctx):
     rng = np.random.default_rng(5)
     B, H, W = 6, 190, 260
