@@ -63,13 +63,18 @@ struct LiveBox {
     const void* recv[2][4];  // host: this block's receive strips by parity and side
 };
 constexpr int kModeList = 0, kModePersistent = 1;
-constexpr size_t kQueueCtlBytes = 256;
+// queue words: head @0, tail @64, active @128, error @192; the 2D solver's two visit counters
+// @kVisitsOff, on a 128-B line of their own (sharing the error word's line -- polled by every
+// grab -- with the in-place passes' atomics cost C2 ~20 %)
+constexpr size_t kQueueCtlBytes = 384;
+constexpr size_t kVisitsOff = 256;
 
-hipError_t fim2d_init(const Fim2dArgs& a, bool f64, int nmaps, const int64_t* d_goals, hipStream_t st);
+// T = inf, queue / list / visit / edge words cleared, goals seeded
+hipError_t fim2d_init(const Fim2dArgs& a, bool f64, int nmaps, const int64_t* d_goals, unsigned* edge, hipStream_t st);
 hipError_t fim2d_sweep(const Fim2dArgs& a, bool f64, int grid, hipStream_t st);
 // wide: the 4-waves-per-SIMD form of the fp32 kernel, for maps of >= kWideTiles tiles
 constexpr int64_t kWideTiles = 16384;
-hipError_t fim2d_persist(const Fim2dArgs& a, bool f64, int grid, hipStream_t st, bool wide = false);
+hipError_t fim2d_persist(const Fim2dArgs& a, bool f64, int grid, hipStream_t st, bool wide = false, bool rewind = true);
 int fim2d_persist_resident(bool f64, int cus, bool wide = false);
 hipError_t fim2d_merge_ghost(const Fim2dArgs& a, bool f64, int side, const void* recv, int64_t len, hipStream_t st);
 hipError_t fim2d_pack_edges(const Fim2dArgs& a, bool f64, void* n, void* s, void* w, void* e, hipStream_t st);

@@ -168,17 +168,19 @@ struct eik_fim2d {
     bool f64 = false;
     Fim2dArgs a{};
     hipStream_t stream = nullptr;
-    DevBuf lists, counts, mark, visits, edge, goals, key;
+    DevBuf lists, counts, mark, edge, goals, key;
     DevBuf qctl, qslot, qstate;          // persistent-mode FIFO
     int* h_counts = nullptr;             // pinned
     unsigned* h_q = nullptr;             // pinned copy of qctl
     unsigned long long* h_visits = nullptr;
+    int64_t* h_goals = nullptr;          // pinned: the goals' upload does not stall the host
     int64_t iterations = 0, host_syncs = 0, max_iters = 0;
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     std::vector<hipEvent_t> ev_pool;     // per-launch timing pairs (timing option)
     size_t ev_used = 0;
     double sweep_ms = 0.0, solve_ms = 0.0;
     bool started = false;
+    bool defer_sync = false;             // eik_fim2d_solve: the launch's read-back syncs with the finish
     int persist_grid = 0;                // co-resident workgroups of the persistent kernel
     // live domain decomposition: hold word on the device, mailbox of the halo agent on the host
     DevBuf hold;
@@ -395,10 +397,10 @@ static int fim2d_create_rows(eik_ctx* c, int64_t B, int64_t H, int64_t W, int dt
         (e = hipHostMalloc((void**)&f->h_q, kQueueCtlBytes)) != hipSuccess ||
         (e = f->counts.ensure(sizeof(int) * 64)) != hipSuccess || (e = f->mark.ensure(sizeof(unsigned) * tiles)) != hipSuccess ||
         (e = f->key.ensure(sizeof(unsigned) * tiles)) != hipSuccess ||
-        (e = f->visits.ensure(2 * sizeof(unsigned long long))) != hipSuccess ||
         (e = f->edge.ensure(sizeof(unsigned) * 4)) != hipSuccess || (e = f->goals.ensure(sizeof(int64_t) * 2 * B)) != hipSuccess ||
         (e = hipHostMalloc((void**)&f->h_counts, sizeof(int) * 64)) != hipSuccess ||
         (e = hipHostMalloc((void**)&f->h_visits, 2 * sizeof(unsigned long long))) != hipSuccess ||
+        (e = hipHostMalloc((void**)&f->h_goals, sizeof(int64_t) * 2 * B)) != hipSuccess ||
         (e = hipEventCreate(&f->ev_start)) != hipSuccess || (e = hipEventCreate(&f->ev_stop)) != hipSuccess) {
         eik_fim2d_destroy(f);
         return set_err(c, EIK_ERR_NOMEM, "fim2d allocation: %s", hipGetErrorString(e));
@@ -408,7 +410,9 @@ static int fim2d_create_rows(eik_ctx* c, int64_t B, int64_t H, int64_t W, int dt
     a.mark = (unsigned*)f->mark.p;
     a.key = (unsigned*)f->key.p;
     a.minkey = (unsigned*)f->counts.p + 16;
-    a.visits = (unsigned long long*)f->visits.p;
+    // the visit counters sit in the queue words' block (own 128-B line): one read-back after a
+    // persistent launch brings both
+    a.visits = (unsigned long long*)((char*)f->qctl.p + kVisitsOff);
     a.edge_dirty = nullptr;
     a.qhead = (unsigned long long*)f->qctl.p;
     a.qtail = (unsigned long long*)((char*)f->qctl.p + 64);
@@ -432,6 +436,7 @@ void eik_fim2d_destroy(eik_fim2d* f) {
     if (!f) return;
     if (f->h_counts) (void)hipHostFree(f->h_counts);
     if (f->h_visits) (void)hipHostFree(f->h_visits);
+    if (f->h_goals) (void)hipHostFree(f->h_goals);
     if (f->h_q) (void)hipHostFree(f->h_q);
     if (f->ev_start) (void)hipEventDestroy(f->ev_start);
     if (f->ev_stop) (void)hipEventDestroy(f->ev_stop);
@@ -488,11 +493,25 @@ int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
     f->solve_ms = 0.0;
     f->ev_used = 0;
     HIPCHK(c, hipEventRecord(f->ev_start, f->stream));
-    HIPCHK(c, hipMemcpyAsync(f->goals.p, goals, sizeof(int64_t) * 2 * f->B, hipMemcpyHostToDevice, f->stream));
-    HIPCHK(c, hipMemsetAsync(f->visits.p, 0, 2 * sizeof(unsigned long long), f->stream));
-    HIPCHK(c, hipMemsetAsync(f->edge.p, 0, sizeof(unsigned) * 4, f->stream));
-    HIPCHK(c, fim2d_init(f->a, f->f64, (int)f->B, (const int64_t*)f->goals.p, f->stream));
+    // (the previous solve on this solver synchronised before returning: h_goals is free)
+    memcpy(f->h_goals, goals, sizeof(int64_t) * 2 * f->B);
+    HIPCHK(c, hipMemcpyAsync(f->goals.p, f->h_goals, sizeof(int64_t) * 2 * f->B, hipMemcpyHostToDevice, f->stream));
+    HIPCHK(c, fim2d_init(f->a, f->f64, (int)f->B, (const int64_t*)f->goals.p, (unsigned*)f->edge.p, f->stream));
     f->started = true;
+    return EIK_OK;
+}
+
+// the persistent launch's queue words (h_q, read back after it): errors and the active count
+static int persist_result(eik_fim2d* f, int64_t* active) {
+    eik_ctx* c = f->ctx;
+    const unsigned err = f->h_q[192 / 4];
+    if (err & 1u)
+        return set_err(c, EIK_ERR_HIP, "persistent solver: a queue wait exceeded %.1f s (EIK_OPT_QTIMEOUT)",
+                       c->qtimeout_s);
+    if (err & 2u)
+        return set_err(c, EIK_ERR_NOCONVERGE, "no convergence within %llu tile visits (negative costs?)",
+                       (unsigned long long)f->a.qbudget);
+    if (active) *active = f->h_q[128 / 4];
     return EIK_OK;
 }
 
@@ -531,22 +550,16 @@ int eik_fim2d_iterate(eik_fim2d* f, int64_t max_iters, int64_t* active) {
         const int g = std::min(grid, f->persist_grid);
         f->a.fresh_first = c->fresh_first;
         f->a.sched = c->sched;
-        HIPCHK(c, fim2d_persist(f->a, f->f64, g, f->stream, wide));
+        // (eik_fim2d_solve: the next solve's init clears the queue, no rewind needed)
+        HIPCHK(c, fim2d_persist(f->a, f->f64, g, f->stream, wide, !f->defer_sync));
         if (c->timing) HIPCHK(c, hipEventRecord(f->ev_pool[f->ev_used++], f->stream));
         ++f->iterations;
         HIPCHK(c, hipMemcpyAsync(f->h_q, f->qctl.p, kQueueCtlBytes, hipMemcpyDeviceToHost, f->stream));
+        if (f->defer_sync) return EIK_OK;  // eik_fim2d_solve: one synchronisation for the whole solve
         HIPCHK(c, hipStreamSynchronize(f->stream));
         ++f->host_syncs;
         if (c->timing) drain_timing(f);
-        const unsigned err = f->h_q[192 / 4];
-        if (err & 1u)
-            return set_err(c, EIK_ERR_HIP, "persistent solver: a queue wait exceeded %.1f s (EIK_OPT_QTIMEOUT)",
-                           c->qtimeout_s);
-        if (err & 2u)
-            return set_err(c, EIK_ERR_NOCONVERGE, "no convergence within %llu tile visits (negative costs?)",
-                           (unsigned long long)f->a.qbudget);
-        if (active) *active = f->h_q[128 / 4];
-        return EIK_OK;
+        return persist_result(f, active);
     }
     while (done < max_iters) {
         const int64_t K = std::min<int64_t>(c->sync_every, max_iters - done);
@@ -593,25 +606,56 @@ int eik_fim2d_active(eik_fim2d* f, int64_t* active) {
     return EIK_OK;
 }
 
-static int finish_solve(eik_fim2d* f) {
+static void fill_stats(const eik_fim2d* f, eik_stats* out);
+
+// Wait for a solve's stream: poll first (a blocking wait's wake-up cost ~20 us per solve on the
+// C2 raster, ~1 % of it), then block for long solves.
+static hipError_t wait_stream(hipStream_t st) {
+    static const int spin_on = [] {
+        const char* v = getenv("EIK_WAIT_SPIN");
+        return v ? atoi(v) : 1;
+    }();
+    if (!spin_on) return hipStreamSynchronize(st);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spin = 0;; ++spin) {
+        const hipError_t e = hipStreamQuery(st);
+        if (e != hipErrorNotReady) return e;
+        if ((spin & 63u) == 63u &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 0.02)
+            return hipStreamSynchronize(st);
+        __builtin_ia32_pause();
+    }
+}
+
+// the stop event and the visit counters after the solve's launches, then ONE synchronisation
+// (the persistent launch's queue words were queued for read-back behind it)
+static int finish_solve(eik_fim2d* f, int64_t* active) {
     eik_ctx* c = f->ctx;
     HIPCHK(c, hipEventRecord(f->ev_stop, f->stream));
-    HIPCHK(c, hipMemcpyAsync(f->h_visits, f->visits.p, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, f->stream));
-    HIPCHK(c, hipStreamSynchronize(f->stream));
+    const bool persist = f->a.mode == kModePersistent;  // h_q (queued after the launch) holds the counters
+    if (!persist)
+        HIPCHK(c, hipMemcpyAsync(f->h_visits, (void*)f->a.visits, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                 f->stream));
+    HIPCHK(c, wait_stream(f->stream));
+    ++f->host_syncs;
+    if (persist) memcpy(f->h_visits, (const char*)f->h_q + kVisitsOff, 2 * sizeof(unsigned long long));
+    if (c->timing) drain_timing(f);
     float ms = 0.f;
     (void)hipEventElapsedTime(&ms, f->ev_start, f->ev_stop);
     f->solve_ms = ms;
-    eik_fim2d_stats(f, &c->last);
-    return EIK_OK;
+    fill_stats(f, &c->last);
+    return f->a.mode == kModePersistent ? persist_result(f, active) : EIK_OK;
 }
 
 int eik_fim2d_solve(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* goals, void* stream) {
     int rc = eik_fim2d_start(f, d_cost, d_T, goals, stream);
     if (rc) return rc;
     int64_t active = 0;
+    f->defer_sync = f->a.mode == kModePersistent;
     rc = eik_fim2d_iterate(f, f->max_iters, &active);
+    f->defer_sync = false;
     if (rc) return rc;
-    rc = finish_solve(f);
+    rc = finish_solve(f, &active);
     if (rc) return rc;
     if (active != 0)
         return set_err(f->ctx, EIK_ERR_NOCONVERGE, "no convergence after %ld iterations (negative costs?)",
@@ -806,10 +850,15 @@ int eik_fim2d_stats(eik_fim2d* f, eik_stats* out) {
     if (!f || !out) return EIK_ERR_ARG;
     if (f->started) {
         eik_ctx* c = f->ctx;
-        HIPCHK(c, hipMemcpyAsync(f->h_visits, f->visits.p, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+        HIPCHK(c, hipMemcpyAsync(f->h_visits, (void*)f->a.visits, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                                  f->stream));
         HIPCHK(c, hipStreamSynchronize(f->stream));
     }
+    fill_stats(f, out);
+    return EIK_OK;
+}
+
+static void fill_stats(const eik_fim2d* f, eik_stats* out) {
     out->iterations = f->iterations;
     out->tile_visits = (int64_t)f->h_visits[0];
     out->inplace_passes = (int64_t)f->h_visits[1];
@@ -819,7 +868,6 @@ int eik_fim2d_stats(eik_fim2d* f, eik_stats* out) {
     out->bytes_alg = (double)out->tile_visits * bytes_per_visit(f->f64) +
                      (double)out->inplace_passes * bytes_per_pass(f->f64) +
                      (double)f->B * f->H * f->W * (f->f64 ? 8 : 4);
-    return EIK_OK;
 }
 
 }  // extern "C"
@@ -1043,12 +1091,12 @@ static int solve_layered(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, i
     const int grid = std::min(c->grid > 0 ? c->grid : 4 * c->cu_count, res);
     a.fresh_first = c->fresh_first;
     HIPCHK(c, hipEventRecord(f->ev_start, st));
-    HIPCHK(c, hipMemsetAsync(f->visits.p, 0, 2 * sizeof(unsigned long long), st));
+    HIPCHK(c, hipMemsetAsync((void*)f->a.visits, 0, 2 * sizeof(unsigned long long), st));
     HIPCHK(c, fim2dl_init(a, f64, goal[0], goal[1], goal[2], st));
     HIPCHK(c, fim2dl_persist(a, nl, f64, grid, st));
     HIPCHK(c, hipEventRecord(f->ev_stop, st));
     HIPCHK(c, hipMemcpyAsync(f->h_q, f->qctl.p, kQueueCtlBytes, hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipMemcpyAsync(f->h_visits, f->visits.p, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(f->h_visits, (void*)f->a.visits, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));
     const unsigned err = f->h_q[192 / 4];
     if (err & 1u)

@@ -699,8 +699,20 @@ __global__ __launch_bounds__(kThreads, WPS) void fim2d_persist_kernel(Fim2dArgs 
 template <typename R>
 __global__ void fim2d_init_kernel(R* __restrict__ T, int64_t n, unsigned* __restrict__ mark, int64_t ntiles,
                                   unsigned* __restrict__ key, unsigned* __restrict__ minkey, unsigned* __restrict__ qstate,
-                                  unsigned* __restrict__ qslot, int64_t nslots) {
+                                  unsigned* __restrict__ qslot, int64_t nslots, unsigned* __restrict__ counts,
+                                  unsigned* __restrict__ qctl, unsigned* __restrict__ visits, unsigned* __restrict__ edge) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    // the solve's control words (list counts, queue head / tail / active / error, visit counters,
+    // DD edge flags) -- here rather than four memset nodes ahead of this kernel
+    if (blockIdx.x == 0 && threadIdx.x < kQueueCtlBytes / 4) {
+        const int t = threadIdx.x;
+        if (qctl) qctl[t] = 0u;
+        if (t < 4) {
+            if (counts) counts[t] = 0u;
+            if (visits) visits[t] = 0u;
+            if (edge) edge[t] = 0u;
+        }
+    }
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) T[i] = Real<R>::inf();
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ntiles; i += stride) {
         mark[i] = 0;
@@ -801,7 +813,7 @@ int fim2d_persist_resident(bool f64, int cus, bool wide) {
     return per_cu * cus;
 }
 
-hipError_t fim2d_persist(const Fim2dArgs& a, bool f64, int grid, hipStream_t st, bool wide) {
+hipError_t fim2d_persist(const Fim2dArgs& a, bool f64, int grid, hipStream_t st, bool wide, bool rewind) {
     if (f64)
         hipLaunchKernelGGL((fim2d_persist_kernel<double, 1>), dim3(grid), dim3(kThreads), 0, st, a);
     else if (wide)
@@ -809,25 +821,26 @@ hipError_t fim2d_persist(const Fim2dArgs& a, bool f64, int grid, hipStream_t st,
     else
         hipLaunchKernelGGL((fim2d_persist_kernel<float, 1>), dim3(grid), dim3(kThreads), 0, st, a);
     // before anything (merge kernel, next launch) appends again
-    hipLaunchKernelGGL(fim2d_qrewind_kernel, dim3(1), dim3(1), 0, st, a);
+    if (rewind) hipLaunchKernelGGL(fim2d_qrewind_kernel, dim3(1), dim3(1), 0, st, a);
     return hipGetLastError();
 }
 
-hipError_t fim2d_init(const Fim2dArgs& a, bool f64, int nmaps, const int64_t* d_goals, hipStream_t st) {
+hipError_t fim2d_init(const Fim2dArgs& a, bool f64, int nmaps, const int64_t* d_goals, unsigned* edge, hipStream_t st) {
+    static_assert(kQueueCtlBytes / 4 <= 256, "the init kernel's block 0 clears the queue words");
     const int64_t n = (int64_t)nmaps * a.H * a.W;
     const int64_t ntiles = (int64_t)nmaps * a.tiles_per_map;
     const int grid = (int)std::min<int64_t>(4096, (n + 255) / 256);
-    hipError_t e0 = hipMemsetAsync(a.counts, 0, sizeof(int) * 4, st);
-    if (e0 == hipSuccess && a.qhead) e0 = hipMemsetAsync(a.qhead, 0, kQueueCtlBytes, st);  // head tail active error
-    if (e0 != hipSuccess) return e0;
     const int64_t nslots = a.qslot ? (int64_t)a.qmask + 1 : 0;
+    unsigned* const counts = reinterpret_cast<unsigned*>(a.counts);
+    unsigned* const qctl = reinterpret_cast<unsigned*>(a.qhead);  // head tail active error
+    unsigned* const visits = reinterpret_cast<unsigned*>(a.visits);
     if (f64) {
         hipLaunchKernelGGL(fim2d_init_kernel<double>, dim3(grid), dim3(256), 0, st, static_cast<double*>(a.T), n,
-                           a.mark, ntiles, a.key, a.minkey, a.qstate, a.qslot, nslots);
+                           a.mark, ntiles, a.key, a.minkey, a.qstate, a.qslot, nslots, counts, qctl, visits, edge);
         hipLaunchKernelGGL(fim2d_seed_kernel<double>, dim3((nmaps + 255) / 256), dim3(256), 0, st, a, d_goals, nmaps);
     } else {
         hipLaunchKernelGGL(fim2d_init_kernel<float>, dim3(grid), dim3(256), 0, st, static_cast<float*>(a.T), n,
-                           a.mark, ntiles, a.key, a.minkey, a.qstate, a.qslot, nslots);
+                           a.mark, ntiles, a.key, a.minkey, a.qstate, a.qslot, nslots, counts, qctl, visits, edge);
         hipLaunchKernelGGL(fim2d_seed_kernel<float>, dim3((nmaps + 255) / 256), dim3(256), 0, st, a, d_goals, nmaps);
     }
     return hipGetLastError();
