@@ -3,7 +3,7 @@
 export TMPDIR=/tmp
 O=gpurun_out
 rocprofv3 -L > $O/pmc_list.txt 2>&1 || true
-B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-path --no-timing --no-extra"
+B=${BENCH:-"python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-path --no-timing --no-extra"}
 i=0
 for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE" \
            "SQ_WAIT_INST_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_VMEM GRBM_COUNT"; do
