@@ -215,7 +215,13 @@ __device__ __forceinline__ void sweep_layered(LCell<R>* __restrict__ Ts, int lan
             for (int z = 0; z < NL; ++z) {
                 const R old = q_old[u].get(z);
                 const R ux = upstream_x(cur[z], q_upx[u].get(z));
-                const R tz = min_nn(z > 0 ? q_old[u].get(z - 1) : INF, z + 1 < NL ? q_old[u].get(z + 1) : INF);
+                // layer neighbours; an end layer has one (the minima are inline asm, which the
+                // compiler cannot fold against the +inf of a missing neighbour)
+                R tz;
+                if constexpr (NL == 1) tz = INF;
+                else if (z == 0) tz = q_old[u].get(1);
+                else if (z + 1 == NL) tz = q_old[u].get(z - 1);
+                else tz = min_nn(q_old[u].get(z - 1), q_old[u].get(z + 1));
                 const R w = godunov3_fast(ux, cur[z], tz, q_c[u].get(z));
                 lds_min(cell + z, w);
                 cur[z] = min_nn(w, old);  // NaN w (no update) keeps old
