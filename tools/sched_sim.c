@@ -25,6 +25,7 @@ static float delta = 0.f;  /* policy 2: bucket width */
 static long seq = 0;
 static int oneside = 0;  /* 1: each quadrant sweep reads only its upstream neighbours */
 static int skipdir = 0;  /* 1: an in-place pass skips the one direction that alone changed the tile last pass */
+static int wrap = 0;     /* 1: the skewed sweep's idle tail steps run its rows again (lane l: rows 0..62-l) */
 static float *cost, *T, *key_of;
 static unsigned char *pend, *held;
 
@@ -89,6 +90,7 @@ int main(int argc, char** argv) {
     if (argc > 6) delta = atof(argv[6]);
     if (getenv("ONESIDE")) oneside = 1;
     if (getenv("SKIPDIR")) skipdir = 1;
+    if (getenv("WRAP")) wrap = 1;
     long dsweeps = 0;  /* quadrant sweeps run */
     NT = N / TS;
     const int nt = NT * NT;
@@ -148,6 +150,21 @@ int main(int argc, char** argv) {
                 for (int yy = 0; yy < TS; ++yy) {
                     int y = (sy > 0 ? yy : TS - 1 - yy) + 1;
                     for (int xx = 0; xx < TS; ++xx) {
+                        int x = (sx > 0 ? xx : TS - 1 - xx) + 1;
+                        float a = oneside ? L[y][x - sx] : fminf(L[y][x - 1], L[y][x + 1]), b = oneside ? L[y - sy][x] : fminf(L[y - 1][x], L[y + 1][x]);
+                        float w = god(a, b, C[y][x]);
+                        if (w < L[y][x]) { L[y][x] = w; ch = 1; chd[d] = 1; }
+                    }
+                }
+            }
+            /* WRAP: the ramp-down steps of the 4 skewed sweeps (lane l idle after step l + 63) run
+             * the first 63 - l rows of their column again: the triangle yy + xx <= 62 of each
+             * direction's frame (modelled after the four full sweeps) */
+            for (int d = 0; wrap && d < 4; ++d) {
+                int sx = (d & 1) ? -1 : 1, sy = (d & 2) ? -1 : 1;
+                for (int yy = 0; yy < TS - 1; ++yy) {
+                    int y = (sy > 0 ? yy : TS - 1 - yy) + 1;
+                    for (int xx = 0; xx + yy <= TS - 2; ++xx) {
                         int x = (sx > 0 ? xx : TS - 1 - xx) + 1;
                         float a = oneside ? L[y][x - sx] : fminf(L[y][x - 1], L[y][x + 1]), b = oneside ? L[y - sy][x] : fminf(L[y - 1][x], L[y + 1][x]);
                         float w = god(a, b, C[y][x]);
