@@ -1,7 +1,7 @@
 """Multi-rank domain decomposition on CPU (gloo): the halo-exchange drivers of eikonal/dd.py
-(dd.solve rounds and the dd.solve_live protocol over P2PHalo), run with 2 and 4 ranks on blocks
-of one raster, must converge to the single-domain solution (the
-oracle FMM field, <= 1e-9 abs: same Godunov fixed point).  The GPU bench plugs the HIP solver
+(dd.solve rounds and the dd.solve_live protocol over P2PHalo), run with 2, 4 and 8 ranks (the
+bench's 2x1 / 2x2 / 4x2 splits) on blocks of one raster, must converge to the single-domain
+solution (the oracle FMM field, <= 1e-9 abs: same Godunov fixed point).  The GPU bench plugs the HIP solver
 into the same driver over RCCL."""
 import os
 import socket
@@ -60,7 +60,7 @@ def _worker(rank, world, port, H, W, goal, seed, q, live=False):
 
 
 @pytest.mark.parametrize("live", [False, True, "node"])
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_dd_matches_single_domain(world, live):
     H, W, seed = 48, 70, 3
     goal = (9, 30)
