@@ -164,7 +164,7 @@ def _ipc_worker(rank, world, port, H, W, goal, seed, q, f64):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,f64", [(2, False), (2, True), (4, False), (4, True)])
+@pytest.mark.parametrize("world,f64", [(2, False), (2, True), (4, False), (4, True), (8, True)])
 def test_live_ipc_processes(world, f64):
     import torch.multiprocessing as mp
 
