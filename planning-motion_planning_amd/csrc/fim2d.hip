@@ -52,6 +52,20 @@ __device__ __forceinline__ R stage_cost(R c) {
 #define EIK_EDGE_FIRST 0
 #endif
 
+// EIK_ACT_SPLIT (persistent in-place passes, default on): the neighbour activations' state-word
+// atomics are issued at the pass boundary and their queueing is finished by wave 0 when its next
+// sweep reaches step kActStep (fim_engine.hpp qpush_issue / qpush_complete), so no wave waits for
+// their round trips at the boundary's barrier: the other three waves start sweeping at once.
+// C2 fp64 2.37-2.42 -> 2.28-2.32 ms, fp32 1.66-1.69 -> 1.56 ms; step 0 (at the sweep's start)
+// ties 4 and beats 8 / 16, which delay the neighbour's queueing (profiles/r03zz_act_split_ab.log).
+#ifndef EIK_ACT_SPLIT
+#define EIK_ACT_SPLIT 1
+#endif
+#ifndef EIK_ACT_STEP
+#define EIK_ACT_STEP 0
+#endif
+constexpr int kActStep = EIK_ACT_STEP;
+
 // ------------------------------------------------------------------------- quadrant sweep
 // A tile cell in LDS: arrival time and cost side by side, so one ds_read_b64 (fp32) fetches both.
 template <typename R>
@@ -117,8 +131,8 @@ __device__ __forceinline__ Cell<R> make_cell(R t, R c, int col) {
 // into [-(kAhead - 1), kTile + 1] -- and addresses the group's steps with immediate offsets, so a
 // group of a lane outside its window may reach kAhead - 1 rows past a halo row.
 
-template <typename R, int DX, int DY, bool TRACK>
-__device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lane, R keep) {
+template <typename R, int DX, int DY, bool TRACK, class Hook>
+__device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lane, R keep, Hook&& hook) {
     constexpr int S = (int)sizeof(Cell<R>);
     constexpr int kRow = kLds * S;
     constexpr int D = kAhead;
@@ -165,6 +179,7 @@ __device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lan
 #pragma unroll
     for (int u = 0; u < D; ++u) fetch(u);
     for (int s = 0; s < 2 * kTile; s += D) {
+        if (s == kActStep) hook();  // (EIK_ACT_SPLIT: the previous pass's queueing, wave 0)
         const int gcur = gb;  // this group's rows (its ds_min targets)
         gb = clampb(raw);     // the next group's (past the last step: guard / halo rows, unused)
         raw += DY * D * kRow;
@@ -197,6 +212,10 @@ __device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lan
         }
     }
     return changed;
+}
+template <typename R, int DX, int DY, bool TRACK>
+__device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lane, R keep) {
+    return sweep_quadrant<R, DX, DY, TRACK>(Ts, lane, keep, [] {});
 }
 
 // LDS of one tile visit
@@ -336,16 +355,25 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
     // quadrant sweeps of this pass (bit w: wave w), in a register: the caller's L.dirs for the
     // first pass, then set by the in-place branch below
     unsigned dirs = L.dirs;
+    // EIK_ACT_SPLIT: this lane's activation issued at the last pass boundary (-1: none)
+    int act_tile = -1;
+    unsigned act_old = 0u;
+    auto act_complete = [&]() {
+        if (act_tile >= 0) qpush_complete(a, act_tile, act_old);
+        act_tile = -1;
+    };
     for (int pass = 0;; ++pass) {
         // ---- sweep rounds (quadrant directions concurrently, one per wave; `dirs` selects them)
         const bool sweep = (dirs >> wave) & 1u;
         bool last_changed = false;
         if (a.max_rounds == 1) {  // single round: "changed" is read off the write-back below
             if (sweep) {
-                if (wave == 0)      sweep_quadrant<R, +1, +1, false>(Ts, lane, keep);
+                if (wave == 0)      sweep_quadrant<R, +1, +1, false>(Ts, lane, keep, act_complete);
                 else if (wave == 1) sweep_quadrant<R, -1, +1, false>(Ts, lane, keep);
                 else if (wave == 2) sweep_quadrant<R, +1, -1, false>(Ts, lane, keep);
                 else                sweep_quadrant<R, -1, -1, false>(Ts, lane, keep);
+            } else if (EIK_ACT_SPLIT && wave == 0) {
+                act_complete();
             }
             __syncthreads();
         } else {
@@ -465,7 +493,10 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
             // a.sched bit 1: after the first pass, neighbour activations wait for the visit's end
             // (one activation with the converged edges instead of one per pass)
             const bool defer = (a.sched & 2) && pass > 0;
-            activate_neighbours(a, tile, defer ? 0u : f, L.key, 0, 0u);  // lanes 0..4 (T already drained)
+            if constexpr (EIK_ACT_SPLIT)
+                act_tile = activate_neighbours_issue(a, tile, defer ? 0u : f, act_old);  // completed in the next sweep
+            else
+                activate_neighbours(a, tile, defer ? 0u : f, L.key, 0, 0u);  // lanes 0..4 (T already drained)
             if (defer && tid == 0) L.flags_acc |= f & 0x6fu;
             dirs = self ? 0xFu : sweep_dirs(pend);  // a self revisit: every direction
             cell_t(Ts, h, hcol) = hv;
@@ -479,6 +510,7 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
             break;
         }
     }
+    act_complete();  // (never pending here: every issue is followed by a pass)
     EIK_PROBE(3);
 }
 

@@ -242,9 +242,17 @@ __device__ __forceinline__ void qslot_put_front(const Fim2dArgs& a, int tile) {
 }
 // Queue the tile unless it is already pending (nothing to do) or busy (its processor re-queues it
 // when it finishes).
-__device__ __forceinline__ void qpush(const Fim2dArgs& a, int tile, unsigned trig) {
+// Split in two halves (EIK_ACT_SPLIT): the state word's atomicOr (qpush_issue) and the queueing
+// its old value decides (qpush_complete), so a busy tile's in-place pass can issue the first at the
+// pass boundary and finish the second inside its next sweep.  Between the two the neighbour is
+// PENDING but not yet queued: other activations of it do nothing (its entry is on the way), and
+// the activating tile is still busy, so the active count stays above zero.
+__device__ __forceinline__ unsigned qpush_issue(const Fim2dArgs& a, int tile, unsigned trig) {
     const unsigned old = atomicOr(&a.qstate[tile], kPending | trig);
     EIK_ACT(tile, old);
+    return old;
+}
+__device__ __forceinline__ void qpush_complete(const Fim2dArgs& a, int tile, unsigned old) {
     if ((old & (kPending | kBusy)) == 0u) {
         atomicAdd(a.qactive, 1);  // before the slot store: a waiter never sees "empty and idle"
         if (!(old & kVisited) && a.fresh_first)
@@ -252,6 +260,9 @@ __device__ __forceinline__ void qpush(const Fim2dArgs& a, int tile, unsigned tri
         else
             qslot_put(a, tile);
     }
+}
+__device__ __forceinline__ void qpush(const Fim2dArgs& a, int tile, unsigned trig) {
+    qpush_complete(a, tile, qpush_issue(a, tile, trig));
 }
 
 __device__ __forceinline__ void activate(const Fim2dArgs& a, int tile, int list, unsigned stamp, float key,
@@ -286,6 +297,35 @@ __device__ __forceinline__ void activate_neighbours(const Fim2dArgs& a, int tile
         if (((f & 8u) || (f & 64u)) && tx + 1 == a.ntx) e |= 8u;
         if (e) atomicOr(a.edge_dirty, e);
     }
+}
+
+// The issue half of a persistent in-place pass's activations (EIK_ACT_SPLIT): thread q in 1..4
+// issues its side's state-word atomicOr and returns the neighbour (-1: none) with `old` to be
+// passed to qpush_complete later; thread 0 flags changed subdomain edges as above.
+__device__ __forceinline__ int activate_neighbours_issue(const Fim2dArgs& a, int tile, unsigned f, unsigned& old) {
+    const int tid = threadIdx.x;
+    old = 0u;
+    if (tid >= 5) return -1;
+    const int map = tile / a.tiles_per_map;
+    const int rem = tile - map * a.tiles_per_map;
+    const int ty = rem / a.ntx, tx = rem - (rem / a.ntx) * a.ntx;
+    const int base = map * a.tiles_per_map;
+    int nb = -1;
+    unsigned trig = 0u;
+    if (tid == 1 && (f & 1u) && ty > 0) { nb = base + rem - a.ntx; trig = kFromS; }
+    if (tid == 2 && (f & 2u) && ty + 1 < a.nty) { nb = base + rem + a.ntx; trig = kFromN; }
+    if (tid == 3 && (f & 4u) && tx > 0) { nb = base + rem - 1; trig = kFromE; }
+    if (tid == 4 && (f & 8u) && tx + 1 < a.ntx) { nb = base + rem + 1; trig = kFromW; }
+    if (nb >= 0) old = qpush_issue(a, nb, trig);
+    if (tid == 0 && a.edge_dirty) {
+        unsigned e = 0;
+        if ((f & 1u) && ty == 0) e |= 1u;
+        if (((f & 2u) || (f & 32u)) && ty + 1 == a.nty) e |= 2u;
+        if ((f & 4u) && tx == 0) e |= 4u;
+        if (((f & 8u) || (f & 64u)) && tx + 1 == a.ntx) e |= 8u;
+        if (e) atomicOr(a.edge_dirty, e);
+    }
+    return nb;
 }
 
 // ------------------------------------------------------------------- PERSISTENT driver
