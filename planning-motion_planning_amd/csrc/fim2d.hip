@@ -58,9 +58,7 @@ __device__ __forceinline__ R stage_cost(R c) {
 // their round trips at the boundary's barrier: the other three waves start sweeping at once.
 // C2 fp64 2.37-2.42 -> 2.28-2.32 ms, fp32 1.66-1.69 -> 1.56 ms; step 0 (at the sweep's start)
 // ties 4 and beats 8 / 16, which delay the neighbour's queueing (profiles/r03zz_act_split_ab.log).
-#ifndef EIK_ACT_SPLIT
-#define EIK_ACT_SPLIT 1
-#endif
+// (EIK_ACT_SPLIT: fim_engine.hpp)
 #ifndef EIK_ACT_STEP
 #define EIK_ACT_STEP 0
 #endif

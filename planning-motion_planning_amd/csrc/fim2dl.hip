@@ -232,6 +232,12 @@ __device__ __forceinline__ void sweep_layered(LCell<R>* __restrict__ Ts, int lan
     }
 }
 
+// EIK_ACT_SPLIT_L: the split activations of fim2d.hip's in-place passes (EIK_ACT_SPLIT) for the
+// layered solver.  Off: built but not yet measured on the GPU (the 2D form was, C2 -3.5 / -6 %).
+#ifndef EIK_ACT_SPLIT_L
+#define EIK_ACT_SPLIT_L 0
+#endif
+
 // Stage, sweep and write back one layered tile (cf. process_tile in fim2d.hip).  Thread t owns
 // cells t + 256 j (j < TH / 4): row (t >> 6) + 4 j, column t & 63 -- a wave reads whole tile rows,
 // i.e. 64 * ls contiguous values per layer load.  Leaves L.flags (bits 0..3: neighbour N/S/W/E
@@ -338,7 +344,13 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
 
     const int kPasses = COH ? a.max_passes : 1;
     unsigned dirs = L.dirs;  // this pass's sweeps (register: see fim2d.hip process_tile)
+    int act_tile = -1;       // EIK_ACT_SPLIT_L: this lane's activation issued at the last pass boundary
+    unsigned act_old = 0u;
     for (int pass = 0;; ++pass) {
+        if (EIK_ACT_SPLIT_L && act_tile >= 0) {  // wave 0 lanes 1..4, as its sweep starts (fim2d.hip)
+            qpush_complete(a, act_tile, act_old);
+            act_tile = -1;
+        }
         if ((dirs >> wave) & 1u) {
             if (wave == 0)      sweep_layered<R, TH, NL, +1, +1>(Ts, lane);
             else if (wave == 1) sweep_layered<R, TH, NL, -1, +1>(Ts, lane);
@@ -379,7 +391,10 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
         // activation atomics are the only round trips the next pass waits for
         const LCell<R> hv = load_halo();
         if (tid == 64) charge_inplace_pass(a);  // in-place passes: stats and the visit budget
-        activate_neighbours(a, tile, f, L.key, 0, 0u);  // lanes 0..4 (T already drained)
+        if constexpr (COH && EIK_ACT_SPLIT_L)
+            act_tile = activate_neighbours_issue(a, tile, f, act_old);  // queued as the next pass starts
+        else
+            activate_neighbours(a, tile, f, L.key, 0, 0u);  // lanes 0..4 (T already drained)
         dirs = 0xFu;  // a self revisit: every direction
         if (hcell) Ts[h] = hv;
         __syncthreads();  // every wave has read L.flags and its halo side is in

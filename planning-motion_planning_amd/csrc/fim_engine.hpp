@@ -242,6 +242,9 @@ __device__ __forceinline__ void qslot_put_front(const Fim2dArgs& a, int tile) {
 }
 // Queue the tile unless it is already pending (nothing to do) or busy (its processor re-queues it
 // when it finishes).
+#ifndef EIK_ACT_SPLIT
+#define EIK_ACT_SPLIT 1  // in-place passes use the split halves below (fim2d.hip, fim2dl.hip)
+#endif
 // Split in two halves (EIK_ACT_SPLIT): the state word's atomicOr (qpush_issue) and the queueing
 // its old value decides (qpush_complete), so a busy tile's in-place pass can issue the first at the
 // pass boundary and finish the second inside its next sweep.  Between the two the neighbour is
