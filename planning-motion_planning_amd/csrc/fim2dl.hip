@@ -233,7 +233,8 @@ __device__ __forceinline__ void sweep_layered(LCell<R>* __restrict__ Ts, int lan
 }
 
 // EIK_ACT_SPLIT_L: the split activations of fim2d.hip's in-place passes (EIK_ACT_SPLIT) for the
-// layered solver.  Off: built but not yet measured on the GPU (the 2D form was, C2 -3.5 / -6 %).
+// layered solver.  Off: no gain on C5 (fp64 2.01-2.07 -> 2.00-2.03, fp32 4.80-4.85 -> 4.69-4.82
+// Gcells/s, profiles/r03zz2_layered_act_split_ab.log), unlike the 2D sweep (C2 -3.5 / -6 %).
 #ifndef EIK_ACT_SPLIT_L
 #define EIK_ACT_SPLIT_L 0
 #endif
