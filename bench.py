@@ -199,6 +199,12 @@ def main():
 
     if world > 1:  # the halo transport delivered every final edge (a wrong field cannot pass)
         dd_ok = dd.halo_consistent(blk, T, ghost, group=ctrl)
+        # and the assembled field is the single-domain one: every rank solves the whole raster on
+        # its own GPU and compares its block (no gather), then -- on RCCL -- one untimed solve of
+        # the relaunch schedule (--dd rounds: batch_isend_irecv + all_reduce over RCCL), checked
+        # the same way, so the north_star transport runs whenever the node has several GPUs
+        dd_check = dd_field_check(args, ctx, dev, stream, blk, cost, T, H, W, seed, goal_g, tdt, edt, ctrl,
+                                  local if (dd_mode == "live" and not shared) else None, send, recv, lgoal)
     value = H * W * args.steps / el / 1e9
     ms_per_step = el / args.steps * 1e3
 
@@ -244,7 +250,8 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "strong" if strong else "weak",
+        # N = 1: one GPU, no scaling; labelled as the N > 1 default (strong: configs[3]'s raster fixed)
+        "scaling": "strong" if (strong or world == 1) else "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": f"synthetic (fractal DEM seed {seed} -> planner cost recipe, eikonal/terrain.py)",
@@ -265,6 +272,7 @@ def main():
         out["config"]["halo_transport"] = ("hipIpc peer stores (xGMI) + node vote" if dd_mode == "live"
                                            else "RCCL batch_isend_irecv + all_reduce")
         out["config"]["dd_halo_consistent"] = dd_ok
+        out["config"].update(dd_check)
         rr = dd_rounds[-args.steps:]
         out["config"]["dd_rounds_per_solve"] = round(sum(rr) / max(len(rr), 1), 1)
         out["config"]["dd_us_per_round"] = round(ms_per_step * 1e3 / max(sum(rr) / max(len(rr), 1), 1), 1)
@@ -291,6 +299,7 @@ def main():
             "costmap": lambda: bench_costmap(ctx, dev, stream, args.extra_steps, goal_g),
             "C4_1gpu": lambda: bench_c4(ctx, dev, stream, max(2, args.extra_steps // 2), tdt, edt),
             "arm": lambda: bench_arm(ctx, args.extra_steps),
+            "C1": lambda: bench_c1(ctx),
         }
         if f64:
             xs["C4_1gpu_f32"] = lambda: bench_c4(ctx, dev, stream, max(2, args.extra_steps // 2), torch.float32,
@@ -301,7 +310,7 @@ def main():
                                 or (k == "C5_f32" and "C5" in want)}
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(cost, goal_g)
+        out["cpu_baseline"] = cpu_baseline(cost, goal_g, dev)
 
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -310,14 +319,34 @@ def main():
 
 
 def ms_to_path(cost, ctx, fim, dev, stream, goal, edt, start=(256, 256), reps=3):
-    """host cost (pageable numpy) -> H2D -> solve -> path kernel -> D2H path."""
+    """Host cost raster -> arrival field -> path, two routes:
+    * ms_to_path (the product's): the drop-in's own calls, FastMarching.computeTmap then
+      getPathGDM, i.e. eik_tmap2d_f64 / eik_path2d_f64 on host numpy arrays (the C ABI copies
+      through its pinned staging ring; the reference's API hands the field back to the host
+      between the two calls, so it crosses PCIe three times: cost in, field out, field in);
+    * ms_to_path_torch: pageable torch .to(dev) -> device solve -> eik_path2d_dev on the resident
+      field -> path back (one host copy of the cost, none of the field).
+    Also the path kernel alone on the resident field (hipEvents on the solver stream) and its
+    time per path step."""
     host_cost = cost.cpu().numpy()
+    f64 = edt == L.EIK_F64
     cap = 30004
     out_d = torch.empty((cap, 2), dtype=torch.float64, device=dev)
     n_d = torch.zeros(1, dtype=torch.int64, device=dev)
     st_d = torch.zeros(1, dtype=torch.int32, device=dev)
     H, W = host_cost.shape
-    tot, devs, lens = [], [], []
+    res = {}
+    if f64:  # the drop-in computes in float64 (FastMarching.py:93-95)
+        tot, lens = [], []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            Th = ctx.tmap2d(host_cost, goal)
+            path, st = ctx.path2d(Th, start, goal)
+            tot.append((time.perf_counter() - t0) * 1e3)
+            lens.append(len(path))
+        res.update({"ms_to_path": round(float(np.median(tot)), 3),
+                    "ms_to_path_route": "drop-in: eik_tmap2d_f64 + eik_path2d_f64 on host arrays (pinned ring)"})
+    tot, devs = [], []
     for _ in range(reps):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -336,9 +365,81 @@ def ms_to_path(cost, ctx, fim, dev, stream, goal, edt, start=(256, 256), reps=3)
         t1 = time.perf_counter()
         tot.append((t1 - t0) * 1e3)
         devs.append(e0.elapsed_time(e1))
-        lens.append(n)
-    return {"ms_to_path": round(float(np.median(tot)), 3), "ms_to_path_device": round(float(np.median(devs)), 3),
-            "path_points": int(lens[0]), "path_status": int(st_d.item()), "path_from": list(start)}
+    # the walker alone on the resident field
+    pk = []
+    for _ in range(reps):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        ctx._chk(L.lib().eik_path2d_dev(ctx._h, T.data_ptr(), edt, H, W, np.array(start, np.float64),
+                                        np.array(goal, np.float64), 0.5, out_d.data_ptr(), cap, n_d.data_ptr(),
+                                        st_d.data_ptr(), stream.cuda_stream))
+        e1.record(stream)
+        torch.cuda.synchronize()
+        pk.append(e0.elapsed_time(e1))
+    n = int(n_d.item())
+    if "ms_to_path" not in res:
+        res["ms_to_path"] = round(float(np.median(tot)), 3)
+        res["ms_to_path_route"] = "torch .to(dev) + device solve + eik_path2d_dev"
+    res.update({"ms_to_path_torch": round(float(np.median(tot)), 3),
+                "ms_to_path_device": round(float(np.median(devs)), 3),
+                "path_kernel_ms": round(float(np.median(pk)), 3),
+                "path_us_per_step": round(float(np.median(pk)) * 1e3 / max(n, 1), 4),
+                "path_points": n, "path_status": int(st_d.item()), "path_from": list(start)})
+    return res
+
+
+def dd_field_check(args, ctx, dev, stream, blk, cost, T, H, W, seed, goal_g, tdt, edt, group, rounds_local,
+                   send, recv, lgoal):
+    """N > 1, after the timed steps: (1) every rank solves the WHOLE raster on its own GPU and
+    compares its block of the decomposed field with it (masks equal, fp64 <= 1e-11 / fp32 <= 1e-5
+    relative; no gather), min over ranks -> dd_field_ok; (2) with RCCL (not the shared-GPU gloo
+    rehearsal) one untimed solve of the relaunch schedule (dd.solve: batch_isend_irecv strips +
+    all_reduce of the active count over RCCL), its field checked the same way -> dd_rounds_field_ok."""
+    tol = 1e-11 if edt == L.EIK_F64 else 1e-5
+    full_c = terrain.cost_block(0, 0, H, W, H, W, seed=seed, device=dev).to(tdt).contiguous()
+    full_T = torch.empty_like(full_c)
+    f1 = eikonal.Fim2d(ctx, 1, H, W, edt)
+    f1.solve(full_c.data_ptr(), full_T.data_ptr(), [goal_g], stream.cuda_stream)
+    torch.cuda.synchronize()
+    f1.close()
+    ref = full_T[blk.y0:blk.y1, blk.x0:blk.x1].contiguous()
+    del full_c, full_T
+    torch.cuda.empty_cache()
+
+    def err_of(Tb):
+        fin = torch.isfinite(ref)
+        if not torch.equal(fin, torch.isfinite(Tb)):
+            return float("inf")
+        if not bool(fin.any()):
+            return 0.0
+        return float(((Tb[fin].double() - ref[fin].double()).abs() / ref[fin].double().clamp(min=1e-30)).max())
+
+    def worst(e):
+        t = torch.tensor([e], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        return t.item()
+
+    out = {}
+    e = worst(err_of(T))
+    out["dd_field_ok"] = bool(e <= tol)
+    out["dd_field_max_rel"] = e
+    if rounds_local is not None and os.environ.get("EIK_BENCH_DD_ROUNDS", "1") == "1":
+        try:
+            T2 = torch.empty_like(T)
+            ctx.set_option(L.OPT_QTIMEOUT, 30.0)
+            rounds_local.start(cost, T2, lgoal, stream.cuda_stream)
+            t0 = time.perf_counter()
+            nr = dd.solve(rounds_local, blk, send, recv, exchange_every=args.exchange_every)
+            torch.cuda.synchronize()
+            el = worst(time.perf_counter() - t0)
+            e2 = worst(err_of(T2))
+            out.update({"dd_rounds_field_ok": bool(e2 <= tol), "dd_rounds_field_max_rel": e2,
+                        "dd_rounds_rccl_rounds": nr, "dd_rounds_rccl_ms": round(el * 1e3, 3)})
+            del T2
+        except Exception as ex:  # report; the measured line stands
+            out["dd_rounds_error"] = repr(ex)[:200]
+    return out
 
 
 def timed_loop(fn, steps, warmup=1):
@@ -624,20 +725,85 @@ def bench_costmap(ctx, dev, stream, steps, goal, N=4096, res=0.05):
                               "node_join": [int(v) for v in rp["r"][2]]}}
 
 
-def cpu_baseline(cost, goal):
-    """Oracle C heap FMM (bit-exact restatement of the reference), 1 host thread."""
+def host_cpu():
+    """The host's CPU model, its logical CPU count and the CPUs this process may use (the GPU box
+    shows the whole machine's CPUs; OMP_NUM_THREADS there is this job's share)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    nproc = os.cpu_count()
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(avail, share) if share > 0 else avail
+    return {"model": model, "nproc": nproc, "affinity": avail, "threads_used": threads}
+
+
+def cpu_baseline(cost, goal, dev, B=128, N=1024):
+    """The reference's algorithm on the host cores (oracle/eikonal_oracle.c: the bit-exact heap-FMM
+    restatement of FastMarching.computeTmap), bounded samples:
+    * value: ONE full-field solve of the C2 raster (fp64), 1 thread -- the reference runs one
+      Python process, one core;
+    * C1 (configs[0]): the 256^2 uniform-cost map, goal at the centre, 1 thread;
+    * C3_all_cores: the 128 x 1024^2 batch with one map per thread over this job's
+      host cores (threads_used)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     c = cost.double().cpu().numpy()
+    hc = host_cpu()
     O.set_strict(False)
-    t0 = time.perf_counter()
-    O.fmm2d(c, goal)
-    el = time.perf_counter() - t0
-    O.set_strict(True)
+    try:
+        t0 = time.perf_counter()
+        O.fmm2d(c, goal)
+        el = time.perf_counter() - t0
+        # C1: configs[0] itself
+        u = np.ones((256, 256))
+        reps, t0 = 0, time.perf_counter()
+        while reps < 3 or time.perf_counter() - t0 < 0.5:
+            O.fmm2d(u, (128, 128))
+            reps += 1
+        c1 = (time.perf_counter() - t0) / reps
+        # C3 over the host cores: the bench's maps and goals
+        costs = np.empty((B, N, N))
+        goals = []
+        for b in range(B):
+            cb = terrain.cost_block(0, 0, N, N, N, N, seed=1000 + b, device=dev).double()
+            goals.append(c3_goal(cb, b, N))
+            costs[b] = cb.cpu().numpy()
+        t0 = time.perf_counter()
+        O.fmm2d_batch(costs, np.array(goals, np.int64), nthreads=hc["threads_used"])
+        c3 = time.perf_counter() - t0
+        del costs
+    finally:
+        O.set_strict(True)
     return {"value": round(c.size / el / 1e9, 6), "unit": "Gcells/s", "cores": 1, "kind": "port",
             "sample": f"one full-field solve of the same {c.shape[0]}x{c.shape[1]} raster in fp64 "
                       f"({el:.2f} s, oracle/eikonal_oracle.c heap FMM)",
-            "seconds": round(el, 3)}
+            "seconds": round(el, 3), "host": hc,
+            "C1": {"workload": "configs[0]: 256x256 uniform cost, goal at the centre, heap FMM, 1 thread",
+                   "ms": round(c1 * 1e3, 3), "value": round(256 * 256 / c1 / 1e9, 6), "unit": "Gcells/s"},
+            "C3_all_cores": {"workload": f"configs[2]: {B} x {N}x{N} terrain maps (the bench's seeds and goals), "
+                                        "one map per thread, heap FMM fp64",
+                             "cores": hc["threads_used"], "seconds": round(c3, 3),
+                             "value": round(B * N * N / c3 / 1e9, 6), "unit": "Gcells/s"}}
+
+
+def bench_c1(ctx, N=256, reps=20):
+    """configs[0] (the reference's CPU plumbing case) through the drop-in's host entry point:
+    256^2 uniform cost, goal at the centre, fp64, host array in -> host field out."""
+    u = np.ones((N, N))
+    ctx.tmap2d(u, (N // 2, N // 2))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ctx.tmap2d(u, (N // 2, N // 2))
+    sec = (time.perf_counter() - t0) / reps
+    return {"workload": "configs[0]: 256x256 uniform cost, goal at the centre, fp64, eik_tmap2d_f64 host -> host",
+            "ms": round(sec * 1e3, 4), "value": round(N * N / sec / 1e9, 4), "unit": "Gcells/s"}
 
 
 if __name__ == "__main__":

@@ -14,7 +14,12 @@ tests/test_costmap_oracle.py:
   cv2.floodFill(im, mask, (0, 0), 1) with default flags: 4-connected, fills the seed's
     connected set of pixels EQUAL to the seed value with 1
 scipy.signal.convolve2d and scipy.ndimage.distance_transform_edt are the reference's own calls.
-Parity of this module to the reference is therefore "pinned to restated cv2 semantics".
+Pinning (round 4): surface_normal, structural_disk, the head (:1101-1163) and the tail (:1180-1216,
+given the state after :1177 and :1192's dilation) are bit-identical to the REFERENCE's own
+functions and statements run on recorded inputs (tests/golden/make_golden_costmap.py ->
+costmap.npz, checked in tests/test_costmap_golden.py).  Parity unpinned: only the cv2 calls
+(image_filling's floodFill / bitwise_not :82-94, the erode / dilate of :1168-1177 and :1192),
+restated and pinned to brute-force definitions.
 """
 import math
 
@@ -112,37 +117,46 @@ def image_filling(im):
     return im | inv
 
 
-def cost_map(Zs, resolution, size, slope_max=0.20, diagonal=0.9, expansion=1.0, gradient=10.0):
-    """The cost raster of main() (Coupled_motion_planner.py:1100-1216) from the DEM Zs
-    (loaded at :1098-1099).  Cited lines are those of the reference file.  Returns (cMap, obstMap): cMap exactly as the reference holds it
-    before calling FM.biComputeTmap(cMap.T, ...) (i.e. indexed [x, y]), obstMap [y, x] float64."""
+def obstacle_head(Zs, resolution, size, slope_max=0.20):
+    """:1101, :1104, :1145-1163: DEM shift, normals, slope obstacles, cleared border, uint8."""
     Zs = np.asarray(Zs, dtype=np.float64)
     Zs = Zs - np.min(Zs)  # :1101
     _, _, Nz = surface_normal(resolution, size, Zs)  # :1104
     slope = np.arccos(Nz)  # :1145
-    obst = np.zeros(Zs.shape)
+    obst = np.zeros(Zs.shape)  # :1151
     obst[slope > slope_max] = 1  # :1154 (borders cleared :1157-1160)
     obst[0, :] = 0
     obst[-1, :] = 0
     obst[:, 0] = 0
     obst[:, -1] = 0
-    obst = np.uint8(obst)
-    obst = image_filling(obst)  # :1163-1164
+    return np.uint8(obst)  # :1163
+
+
+def obstacle_morphology(obst, resolution, diagonal=0.9):
+    """:1164-1177 (the cv2 block, restated): fill, erode / dilate r = 10, dilate r = diagonal / 2,
+    fill, erode."""
+    obst = image_filling(obst)  # :1164
     se = structural_disk(10)  # :1167-1169
     obst = erode(obst, se)
     obst = dilate(obst, se)
-    se = structural_disk(int(round((diagonal / 2) / resolution)))  # :1172-1178
+    se = structural_disk(int(round((diagonal / 2) / resolution)))  # :1172-1177
     obst = dilate(obst, se)
     obst = image_filling(obst)
-    obst = erode(obst, se)
-    obst[0, :] = 1  # :1180-1184
+    return erode(obst, se)
+
+
+def cost_tail(obst, resolution, expansion=1.0, gradient=10.0, dilated=None):
+    """:1180-1216 on the uint8 obstacle map after :1177 -> (cMap [x, y], obstMap float64 [y, x]).
+    `dilated` (tests): :1192's cv2.dilate result, else restated here."""
+    obst = np.array(obst, dtype=np.uint8)
+    obst[0, :] = 1  # :1180-1183
     obst[-1, :] = 1
     obst[:, 0] = 1
     obst[:, -1] = 1
-    obst = np.float64(obst)
+    obst = np.float64(obst)  # :1184
     high = obst * 300  # :1187
     se = structural_disk(int(round(expansion / resolution)))  # :1190-1192
-    dil = dilate(obst, se)
+    dil = dilate(obst, se) if dilated is None else dilated
     dist = resolution * ndimage.distance_transform_edt(obst == 0)  # :1194
     od = dil * (1 - dist / (np.max(dist)))  # :1196
     pos = od > 0
@@ -156,3 +170,14 @@ def cost_map(Zs, resolution, size, slope_max=0.20, diagonal=0.9, expansion=1.0, 
     cmap[:, 0] = np.inf
     cmap[:, -1] = np.inf
     return cmap, obst
+
+
+def cost_map(Zs, resolution, size, slope_max=0.20, diagonal=0.9, expansion=1.0, gradient=10.0):
+    """The cost raster of main() (Coupled_motion_planner.py:1101-1216) from the DEM Zs
+    (loaded at :1098-1099).  Returns (cMap, obstMap): cMap exactly as the reference holds it
+    before calling FM.biComputeTmap(cMap.T, ...) (i.e. indexed [x, y]), obstMap [y, x] float64.
+    The head and the tail are pinned to the reference's own statements run on recorded inputs
+    (tests/golden/costmap.npz, tests/test_costmap_golden.py); the cv2 middle to brute force."""
+    obst = obstacle_head(Zs, resolution, size, slope_max)
+    obst = obstacle_morphology(obst, resolution, diagonal)
+    return cost_tail(obst, resolution, expansion, gradient)

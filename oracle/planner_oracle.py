@@ -6,7 +6,8 @@ Reference: /root/reference/src/Coupled_motion_planner.py main()
   cost raster                  :1101-1216 -> costmap_oracle.cost_map()
   biComputeTmap / getPathGDM   :1222-1226 -> oracle.fmm2d_bidir() / oracle.gdm2d() (C restatement,
                                              bit-identical to the reference's FastMarching.py)
-  path assembly, pruning, z, heading :1228-1252 -> assemble(), statement by statement
+  path assembly, pruning, z, heading :1232-1255 -> assemble(), statement by statement (pinned
+                                     to the reference's statements run here: costmap.npz s*)
 """
 import numpy as np
 
@@ -21,7 +22,7 @@ def nodes(xm, ym, xr, yr, resolution):
 
 
 def assemble(pathS, pathG, Zs, xm, ym, xr, yr, initialHeading, resolution, zp=0.07):
-    """:1228-1252 verbatim in numpy; Zs is the raw DEM (the :1101 shift is applied here)."""
+    """:1232-1255 verbatim in numpy; Zs is the raw DEM (the :1101 shift is applied here)."""
     Zs = Zs - np.min(Zs)
     roverPos = [xr, yr]
     roverPath = np.vstack((np.flipud(pathS), pathG[1:, :]))

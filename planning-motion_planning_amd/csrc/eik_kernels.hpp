@@ -75,6 +75,7 @@ hipError_t fim2d_sweep(const Fim2dArgs& a, bool f64, int grid, hipStream_t st);
 // wide: the 4-waves-per-SIMD form of the fp32 kernel, for maps of >= kWideTiles tiles
 constexpr int64_t kWideTiles = 16384;
 hipError_t fim2d_persist(const Fim2dArgs& a, bool f64, int grid, hipStream_t st, bool wide = false, bool rewind = true);
+hipError_t fim2d_qrewind(const Fim2dArgs& a, hipStream_t st);
 int fim2d_persist_resident(bool f64, int cus, bool wide = false);
 hipError_t fim2d_merge_ghost(const Fim2dArgs& a, bool f64, int side, const void* recv, int64_t len, hipStream_t st);
 hipError_t fim2d_pack_edges(const Fim2dArgs& a, bool f64, void* n, void* s, void* w, void* e, hipStream_t st);

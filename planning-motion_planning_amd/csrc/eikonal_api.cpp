@@ -181,6 +181,7 @@ struct eik_fim2d {
     double sweep_ms = 0.0, solve_ms = 0.0;
     bool started = false;
     bool defer_sync = false;             // eik_fim2d_solve: the launch's read-back syncs with the finish
+    bool need_rewind = false;            // a launch without its queue rewind ran since the last init
     int persist_grid = 0;                // co-resident workgroups of the persistent kernel
     // live domain decomposition: hold word on the device, mailbox of the halo agent on the host
     DevBuf hold;
@@ -498,6 +499,7 @@ int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
     HIPCHK(c, hipMemcpyAsync(f->goals.p, f->h_goals, sizeof(int64_t) * 2 * f->B, hipMemcpyHostToDevice, f->stream));
     HIPCHK(c, fim2d_init(f->a, f->f64, (int)f->B, (const int64_t*)f->goals.p, (unsigned*)f->edge.p, f->stream));
     f->started = true;
+    f->need_rewind = false;  // the init cleared the queue words
     return EIK_OK;
 }
 
@@ -525,6 +527,15 @@ static int drain_timing(eik_fim2d* f) {
     return EIK_OK;
 }
 
+// A persistent launch's idle waiters take tickets past the tail; eik_fim2d_solve skips the rewind
+// kernel after its launch, so before anything appends to the same queue again (merge_ghost, the
+// next iterate) the ticket counter is restarted at the tail.
+static hipError_t rewind_if_needed(eik_fim2d* f) {
+    if (!f->need_rewind) return hipSuccess;
+    f->need_rewind = false;
+    return fim2d_qrewind(f->a, f->stream);
+}
+
 int eik_fim2d_iterate(eik_fim2d* f, int64_t max_iters, int64_t* active) {
     if (!f || !f->started) return EIK_ERR_ARG;
     eik_ctx* c = f->ctx;
@@ -550,8 +561,11 @@ int eik_fim2d_iterate(eik_fim2d* f, int64_t max_iters, int64_t* active) {
         const int g = std::min(grid, f->persist_grid);
         f->a.fresh_first = c->fresh_first;
         f->a.sched = c->sched;
-        // (eik_fim2d_solve: the next solve's init clears the queue, no rewind needed)
+        // eik_fim2d_solve launches without the queue rewind (the next solve's init clears the
+        // queue); a later merge_ghost / iterate on the same solve issues it first (need_rewind)
+        HIPCHK(c, rewind_if_needed(f));
         HIPCHK(c, fim2d_persist(f->a, f->f64, g, f->stream, wide, !f->defer_sync));
+        f->need_rewind = f->defer_sync;
         if (c->timing) HIPCHK(c, hipEventRecord(f->ev_pool[f->ev_used++], f->stream));
         ++f->iterations;
         HIPCHK(c, hipMemcpyAsync(f->h_q, f->qctl.p, kQueueCtlBytes, hipMemcpyDeviceToHost, f->stream));
@@ -672,6 +686,7 @@ int eik_fim2d_pack_edges(eik_fim2d* f, void* n, void* s, void* w, void* e) {
 int eik_fim2d_merge_ghost(eik_fim2d* f, int side, const void* recv) {
     if (!f || !f->started || side < 0 || side > 3 || !recv || !f->a.ghost[side]) return EIK_ERR_ARG;
     f->a.iter = (unsigned)f->iterations;  // enqueue for the next sweep launch
+    HIPCHK(f->ctx, rewind_if_needed(f));
     HIPCHK(f->ctx, fim2d_merge_ghost(f->a, f->f64, side, recv, side < 2 ? f->W : f->H, f->stream));
     return EIK_OK;
 }
@@ -764,6 +779,7 @@ int eik_fim2d_launch(eik_fim2d* f, int live) {
     const int g = std::max(live ? 2 : 1, std::min(grid, f->persist_grid));
     a.fresh_first = c->fresh_first;
     a.sched = c->sched;
+    HIPCHK(c, rewind_if_needed(f));
     HIPCHK(c, fim2d_persist(a, f->f64, g, f->stream, wide));
     if (c->timing) HIPCHK(c, hipEventRecord(f->ev_pool[f->ev_used++], f->stream));
     f->live_on = live != 0;

@@ -41,7 +41,9 @@ namespace eik {
 // cell then rises by at most 2^-500 over its upstream value, far below the 1e-9 field tolerance.
 template <typename R>
 __device__ __forceinline__ R stage_cost(R c) {
-    if constexpr (sizeof(R) == 8 && EIK_CHAIN) return __builtin_fmax(c, 0x1p-500);
+    // (only finite non-negative small costs: NaN and negative costs keep their own paths -- a NaN
+    // cost is never updated, i.e. blocked, as without the clamp)
+    if constexpr (sizeof(R) == 8 && EIK_CHAIN) return (c >= R(0) && c < 0x1p-500) ? R(0x1p-500) : c;
     else return c;
 }
 
@@ -71,7 +73,7 @@ struct alignas(2 * sizeof(R)) Cell {
     R t, c;
 };
 
-// LDS bank swizzle (EIK_SWZ, default on): a cell of an LDS column with bit 4 set holds (cost, T)
+// LDS bank swizzle (EIK_SWZ, default OFF -- measured below): a cell of an LDS column with bit 4 set holds (cost, T)
 // instead of (T, cost).  The sweeps' T-only accesses (ds_min, the upstream-x read, the start-row
 // read) of a skewed anti-diagonal put lane l at byte -(kLds - 1) * sizeof(Cell) * l from lane 0:
 // with T always the cell's first half that is bank -2l mod 32 (fp32, b32 banking) / -4l mod 64
@@ -852,6 +854,11 @@ hipError_t fim2d_persist(const Fim2dArgs& a, bool f64, int grid, hipStream_t st,
         hipLaunchKernelGGL((fim2d_persist_kernel<float, 1>), dim3(grid), dim3(kThreads), 0, st, a);
     // before anything (merge kernel, next launch) appends again
     if (rewind) hipLaunchKernelGGL(fim2d_qrewind_kernel, dim3(1), dim3(1), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t fim2d_qrewind(const Fim2dArgs& a, hipStream_t st) {
+    hipLaunchKernelGGL(fim2d_qrewind_kernel, dim3(1), dim3(1), 0, st, a);
     return hipGetLastError();
 }
 

@@ -304,7 +304,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
     };
     // fp64: costs as the sweep keeps them (>= 2^-500: the range-free square root, fim2d.hip stage_cost)
     auto scost = [](R c) -> R {
-        if constexpr (sizeof(R) == 8) return __builtin_fmax(c, 0x1p-500);
+        if constexpr (sizeof(R) == 8) return (c >= R(0) && c < 0x1p-500) ? R(0x1p-500) : c;  // NaN stays NaN
         else return c;
     };
     if (y0 + TH <= a.H && x0 + kTile <= a.W) {  // full tile: no per-cell range test

@@ -94,3 +94,22 @@ def test_costmap_dropin_and_solver(ctx):
     gy, gx = free[len(free) // 2]
     T = FM.computeTmap(cmap.T, [int(gx), int(gy)], [-1, -1])
     assert T[gy, gx] == 0 and np.isfinite(T).sum() > n * n // 4
+
+
+@pytest.mark.parametrize("k", range(3))
+def test_costmap_vs_reference_fixture(ctx, golden, k):
+    """The GPU builder against the reference's own statements (tests/golden/costmap.npz: the
+    reference's head :1101-1163 and tail :1180-1216 run in the build container, the cv2 middle
+    restated): normals <= 1e-12, obstacle masks bit-exact, costs <= 1e-12 relative."""
+    g = golden("costmap")
+    Z, res = g[f"c{k}_Z"], float(g[f"c{k}_res"])
+    n = Z.shape[0]
+    got = ctx.surface_normal(Z - Z.min(), n * res)
+    for a, key in zip(got, ("Nx", "Ny", "Nz")):
+        assert np.abs(a - g[f"c{k}_{key}"]).max() <= 1e-12
+    cost, obst = ctx.costmap(Z, res, n * res)
+    assert np.array_equal(obst.astype(np.float64), g[f"c{k}_obst_final"])
+    R = g[f"c{k}_cmap"].T
+    fin = np.isfinite(R)
+    assert np.array_equal(np.isfinite(cost), fin)
+    assert (np.abs(cost[fin] - R[fin]) / R[fin]).max() <= 1e-12

@@ -93,3 +93,99 @@ def test_dd_blocks_match_single_domain(mode, px, py, f64):
     else:
         assert (err / np.maximum(R[fin], 1e-30)).max() <= 2e-5
     assert rounds >= 2
+
+
+@pytest.mark.parametrize("f64", [True, False])
+def test_solve_then_merge_then_iterate(f64):
+    """The C ABI allows set_ghosts -> solve -> pack_edges -> exchange -> merge_ghost -> iterate:
+    eik_fim2d_solve launches without the queue rewind, so the merge's activations must not land
+    behind tickets the launch's idle waiters already took (the next launch would spin
+    until the queue timeout, or lose the ghost update).  2 x 1 blocks, the first local solve by
+    eik_fim2d_solve, then dd.solve's rounds; the assembled field equals the oracle's."""
+    import eikonal
+    from eikonal import _lib as L
+    from eikonal import dd
+
+    rng = np.random.default_rng(77)
+    H, W = 260, 330
+    cost = rng.uniform(1, 6, (H, W))
+    cost[rng.random((H, W)) < 0.08] = np.inf
+    goal = (W // 5, H // 2)
+    cost[goal[1], goal[0]] = 1.0
+    if not f64:
+        cost = cost.astype(np.float32).astype(np.float64)
+    dev = torch.device("cuda", 0)
+    dt = torch.float64 if f64 else torch.float32
+    ctx = eikonal.Context(0)
+    ctx.set_option(L.OPT_QTIMEOUT, 5.0)  # a lost / stuck queue entry fails fast instead of hanging
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    blocks = [dd.Block(H, W, 2, 1, r) for r in range(2)]
+    fims, sends, recvs, Ts, costs = [], [], [], [], []
+    for b in blocks:
+        c = torch.from_numpy(np.ascontiguousarray(cost[b.y0:b.y1, b.x0:b.x1])).to(dev, dt)
+        send, recv, ghost = dd.make_strips(b, dt, dev, float("inf"))
+        fim = eikonal.Fim2d(ctx, 1, b.h, b.w, L.EIK_F64 if f64 else L.EIK_F32)
+        fim.set_ghosts(*[g.data_ptr() if g is not None else None for g in ghost])
+        T = torch.empty_like(c)
+        fim.solve(c.data_ptr(), T.data_ptr(), [b.local_goal(*goal)], stream)  # no rewind after it
+        fims.append(fim), sends.append(send), recvs.append(recv), Ts.append(T), costs.append(c)
+    for rounds in range(1, 1000):
+        for fim, send in zip(fims, sends):
+            fim.pack_edges(*[t.data_ptr() if t is not None else None for t in send])
+        for r, b in enumerate(blocks):
+            for s in range(4):
+                if b.nb[s] is not None:
+                    recvs[r][s].copy_(sends[b.nb[s]][OPP[s]])
+        for r, b in enumerate(blocks):
+            for s in range(4):
+                if b.nb[s] is not None:
+                    fims[r].merge_ghost(s, recvs[r][s].data_ptr())
+        if sum(f.active() for f in fims) == 0:
+            break
+        for f in fims:
+            f.iterate(1)
+    torch.cuda.synchronize()
+    out = np.empty((H, W), np.float64)
+    for b, T in zip(blocks, Ts):
+        out[b.y0:b.y1, b.x0:b.x1] = T.cpu().double().numpy()
+    ctx.close()
+    R = oracle_field(cost, goal)
+    fin = np.isfinite(R)
+    assert np.array_equal(np.isfinite(out), fin)
+    err = np.abs(out[fin] - R[fin])
+    if f64:
+        assert err.max() <= 1e-9, err.max()
+    else:
+        assert (err / np.maximum(R[fin], 1e-30)).max() <= 2e-5
+
+
+@pytest.mark.parametrize("mode", ["persistent", "list"])
+def test_nan_cost_blocks_fp64_device(mode):
+    """fp64 device-buffer solve (eik_fim2d_solve, no host cost check) with a NaN block: the staged
+    cost clamp (>= 2^-500) must keep NaN a blocked cell, as +inf; field = the oracle's on the
+    raster with those cells at +inf."""
+    import eikonal
+    from eikonal import _lib as L
+
+    rng = np.random.default_rng(31)
+    H, W = 300, 280
+    cost = rng.uniform(1, 5, (H, W))
+    cost[100:140, 20:250] = np.nan
+    goal = (W // 2, 40)
+    dev = torch.device("cuda", 0)
+    ctx = eikonal.Context(0)
+    ctx.set_option(L.OPT_MODE, L.MODE_PERSISTENT if mode == "persistent" else L.MODE_LIST)
+    ctx.set_option(L.OPT_QTIMEOUT, 5.0)
+    c = torch.from_numpy(cost).to(dev)
+    T = torch.empty_like(c)
+    fim = eikonal.Fim2d(ctx, 1, H, W, L.EIK_F64)
+    fim.solve(c.data_ptr(), T.data_ptr(), [goal], torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize()
+    fim.close()
+    ctx.close()
+    Tg = T.cpu().numpy()
+    assert np.all(np.isinf(Tg[np.isnan(cost)]))
+    R = oracle_field(np.where(np.isnan(cost), np.inf, cost), goal)
+    fin = np.isfinite(R)
+    assert np.array_equal(np.isfinite(Tg), fin)
+    assert np.abs(Tg[fin] - R[fin]).max() <= 1e-9

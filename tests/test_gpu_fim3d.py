@@ -248,3 +248,32 @@ def test_path3d_windowed(ctx, shape, seed, pad):
     assert st == rst and path.shape == ref.shape, (st, rst, path.shape, ref.shape)
     assert np.abs(path - ref).max() <= 1e-9
     assert len(path) > 40
+
+
+@pytest.mark.parametrize("f64", [False, True])
+def test_layered_nan_cost_blocks(ctx, f64):
+    """A NaN cost on the device-buffer entry (no host cost check) acts as a blocked cell: the fp64
+    cost clamp of the layered solver (>= 2^-500 for the range-free square root) must not turn NaN
+    into a near-zero passable cost.  Field = the oracle's with those cells at +inf."""
+    import torch
+    from eikonal import _lib as L
+
+    c, goal = _layered_case((150, 170, 3), 23, pad=True, switch=False)
+    cn = c.copy()
+    cn[40:70, 50:120, 1:4] = np.nan  # a wall across the volume, every layer
+    dev = torch.device("cuda", 0)
+    cd = torch.from_numpy(cn.astype(np.float64 if f64 else np.float32)).to(dev)
+    Td = torch.empty_like(cd)
+    H, W, Lz = c.shape
+    ctx._chk(L.lib().eik_fim3d_solve(ctx._h, cd.data_ptr(), Td.data_ptr(), H, W, Lz, L.EIK_F64 if f64 else L.EIK_F32,
+                                     np.ascontiguousarray(goal, np.int64), torch.cuda.current_stream(dev).cuda_stream))
+    torch.cuda.synchronize()
+    ci = np.where(np.isnan(cn), np.inf, cn)
+    O.set_strict(False)
+    try:
+        R = O.fmm3d(ci, goal, None)
+    finally:
+        O.set_strict(True)
+    T = Td.cpu().numpy()
+    assert np.all(np.isinf(T[np.isnan(cn)]))
+    check(T, R, f64)

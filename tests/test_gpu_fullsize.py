@@ -51,7 +51,7 @@ def local_solve(torch, T, c):
     return torch.where(torch.isinf(lo), torch.full_like(lo, inf), w)
 
 
-def check_properties(torch, T32, c32, goal, rows=2048):
+def check_properties(torch, T32, c32, goal, rows=2048, tol=2e-5):
     H, W = T32.shape
     gx, gy = goal
     assert float(T32[gy, gx]) == 0.0
@@ -81,7 +81,7 @@ def check_properties(torch, T32, c32, goal, rows=2048):
         # closure: an unreached finite-cost cell has no reached neighbour
         open_ = ~finc & torch.isfinite(c[s:e])
         assert not bool(torch.isfinite(nmin[open_]).any()), "an unreached cell next to a reached one"
-    assert worst <= 2e-5, worst
+    assert worst <= tol, worst
     return worst
 
 
@@ -146,49 +146,67 @@ def test_c2_full_size_vs_oracle(env):
     assert np.abs(path - ref).max() <= 1e-9
 
 
-def test_c3_full_batch_vs_oracle(env):
+@pytest.mark.parametrize("f64", [False, True])
+def test_c3_full_batch_vs_oracle(env, f64):
+    """configs[2] as the bench runs it (bench.py bench_batch: 128 maps of 1024^2, seeds 1000..1127,
+    the same goals) in ONE batched persistent solve, fp32 and fp64 (the bench's credited
+    arithmetic); four of its maps against the oracle's fp64 heap FMM: masks equal, fp32 <= 2e-5
+    relative, fp64 <= 1e-9 absolute."""
     torch, eikonal, L, terrain, dev, ctx = env
+    import bench
+
     B, N = 128, 1024
-    cost = torch.empty((B, N, N), dtype=torch.float32, device=dev)
-    rng = np.random.default_rng(1000)
+    dt = torch.float64 if f64 else torch.float32
+    cost = torch.empty((B, N, N), dtype=dt, device=dev)
     goals = []
-    for b in range(B):  # the bench's batch (bench.py bench_batch)
-        cost[b] = terrain.cost_block(0, 0, N, N, N, N, seed=1000 + b, device=dev)
-        while True:
-            gx, gy = (int(v) for v in rng.integers(N // 8, N - N // 8, 2))
-            if float(cost[b, gy, gx]) < 50:
-                break
-        goals.append((gx, gy))
+    for b in range(B):
+        cost[b] = terrain.cost_block(0, 0, N, N, N, N, seed=1000 + b, device=dev).to(dt)
+        goals.append(bench.c3_goal(cost[b], b, N))
     T = torch.empty_like(cost)
-    fim = eikonal.Fim2d(ctx, B, N, N, L.EIK_F32)
+    fim = eikonal.Fim2d(ctx, B, N, N, L.EIK_F64 if f64 else L.EIK_F32)
     fim.solve(cost.data_ptr(), T.data_ptr(), goals, torch.cuda.current_stream(dev).cuda_stream)
     torch.cuda.synchronize()
     fim.close()
+    assert float(torch.isfinite(T).float().mean()) > 0.5
     O.set_strict(False)
     try:
         for b in (0, 37, 90, 127):
             R = O.fmm2d(cost[b].double().cpu().numpy(), goals[b])
-            Tg = T[b].cpu().numpy()
+            Tg = T[b].cpu().numpy().astype(np.float64)
             fin = np.isfinite(R)
             assert np.array_equal(np.isfinite(Tg), fin), b
-            rel = np.abs(Tg[fin].astype(np.float64) - R[fin]) / np.maximum(R[fin], 1e-30)
-            assert rel.max() <= 2e-5, (b, rel.max())
+            if f64:
+                err = np.abs(Tg[fin] - R[fin]).max()
+                assert err <= 1e-9, (b, err)
+            else:
+                rel = np.abs(Tg[fin] - R[fin]) / np.maximum(R[fin], 1e-30)
+                assert rel.max() <= 2e-5, (b, rel.max())
     finally:
         O.set_strict(True)
+    del cost, T
+    torch.cuda.empty_cache()
 
 
-def test_c4_full_size_properties(env):
+@pytest.mark.parametrize("f64", [False, True])
+def test_c4_full_size_properties(env, f64):
+    """configs[3] on one GPU (bench.py bench_c4: the 16384^2 raster, seed 7, goal at the centre),
+    fp32 (the 4-waves-per-SIMD kernel) and fp64: T[goal] = 0, the Godunov fixed point of every
+    reached cell's own neighbours (fp32 <= 2e-5, fp64 <= 1e-11 relative), descent and closure."""
     torch, eikonal, L, terrain, dev, ctx = env
     N = 16384
-    cost = terrain.cost_block(0, 0, N, N, N, N, seed=7, device=dev).contiguous()
+    dt = torch.float64 if f64 else torch.float32
+    cost = terrain.cost_block(0, 0, N, N, N, N, seed=7, device=dev).to(dt).contiguous()
     T = torch.empty_like(cost)
-    fim = eikonal.Fim2d(ctx, 1, N, N, L.EIK_F32)
+    fim = eikonal.Fim2d(ctx, 1, N, N, L.EIK_F64 if f64 else L.EIK_F32)
     goal = (N // 2, N // 2)
     fim.solve(cost.data_ptr(), T.data_ptr(), [goal], torch.cuda.current_stream(dev).cuda_stream)
     torch.cuda.synchronize()
     fim.close()
     assert float(torch.isfinite(T).float().mean()) > 0.9
-    check_properties(torch, T, cost, goal)
+    worst = check_properties(torch, T, cost, goal, tol=1e-11 if f64 else 2e-5)
+    print(f"C4 {'fp64' if f64 else 'fp32'} worst fixed-point residual {worst:.3e}")
+    del cost, T
+    torch.cuda.empty_cache()
 
 
 def local_solve3(torch, T, c):
