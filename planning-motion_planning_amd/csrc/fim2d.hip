@@ -66,6 +66,44 @@ __device__ __forceinline__ R stage_cost(R c) {
 #endif
 constexpr int kActStep = EIK_ACT_STEP;
 
+// EIK_ASYNC_WB (persistent in-place passes): a pass boundary issues the write-back's sc1 stores
+// and goes straight into the next sweep -- no drain, no halo-reload round trip on the tile's own
+// timeline.  The duties the boundary used to wait for run inside the next sweep, at group steps:
+//   kDrainStep      every wave waits for its own stores (s_waitcnt vmcnt(0)) and counts itself
+//                   in LDS (L.drained);
+//   kActIssueStep   wave 0, once all four waves have counted: the neighbour activations of the
+//                   previous pass's write-back (state-word atomics; the recipe of Guideline 16:
+//                   every storing wave drained before the signal, through an LDS counter);
+//   kActDoneStep    wave 0 finishes their queueing (qpush_complete);
+//   kConsumeStep    wave 1 consumes the activations that reached this busy tile (atomicAnd of
+//                   its state word) and charges the pass to the visit budget;
+//   kHaloLoadStep   wave 1, after that atomic has returned: loads the whole halo ring (4 sides);
+//   kHaloStoreStep  wave 1 stores it into the LDS ring (the remaining steps of this sweep may read
+//                   the fresher values: they only lower upper bounds) and publishes what it
+//                   consumed for the boundary's continue / direction decision.
+// A visit's last pass drains at the boundary as before (its activations and the finish follow).
+// Measured and OFF (profiles/r04c_async_wb_ab.log): C2 fp64 2.36 -> 3.3-4.0 ms for every choice of
+// steps, tile visits +40-120 %.  The drain is the front's hop either way -- a neighbour may only be
+// activated once the edge it reads has landed -- and the mid-sweep consumption and halo reload serve
+// fewer activations per pass than the boundary's.
+#ifndef EIK_ASYNC_WB
+#define EIK_ASYNC_WB 0
+#endif
+#ifndef EIK_DRAIN_STEP
+#define EIK_DRAIN_STEP 40
+#endif
+#ifndef EIK_CONSUME_STEP
+#define EIK_CONSUME_STEP 72
+#endif
+constexpr int kDrainStep = EIK_DRAIN_STEP;
+constexpr int kActIssueStep = EIK_DRAIN_STEP + 4;
+constexpr int kActDoneStep = EIK_DRAIN_STEP + 24;
+constexpr int kConsumeStep = EIK_CONSUME_STEP;
+constexpr int kHaloLoadStep = EIK_CONSUME_STEP + 16;
+constexpr int kHaloStoreStep = EIK_CONSUME_STEP + 36;
+static_assert(kDrainStep % kAhead == 0 && kConsumeStep % kAhead == 0 && kHaloStoreStep < 2 * kTile &&
+              kActDoneStep < 2 * kTile, "in-sweep duty steps: group boundaries of the 2 kTile-step sweep");
+
 // ------------------------------------------------------------------------- quadrant sweep
 // A tile cell in LDS: arrival time and cost side by side, so one ds_read_b64 (fp32) fetches both.
 template <typename R>
@@ -179,7 +217,7 @@ __device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lan
 #pragma unroll
     for (int u = 0; u < D; ++u) fetch(u);
     for (int s = 0; s < 2 * kTile; s += D) {
-        if (s == kActStep) hook();  // (EIK_ACT_SPLIT: the previous pass's queueing, wave 0)
+        hook(s);  // per group: the in-sweep duties of the persistent driver (process_tile)
         const int gcur = gb;  // this group's rows (its ds_min targets)
         gb = clampb(raw);     // the next group's (past the last step: guard / halo rows, unused)
         raw += DY * D * kRow;
@@ -215,7 +253,7 @@ __device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lan
 }
 template <typename R, int DX, int DY, bool TRACK>
 __device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lane, R keep) {
-    return sweep_quadrant<R, DX, DY, TRACK>(Ts, lane, keep, [] {});
+    return sweep_quadrant<R, DX, DY, TRACK>(Ts, lane, keep, [](int) {});
 }
 
 // LDS of one tile visit
@@ -231,6 +269,9 @@ struct TileLds {
     unsigned key[5];    // min new value entering: self, N, S, W, E (f32 bits; ordered mode)
     int defer, tile, last;
     unsigned dirs;      // quadrant sweeps of this visit (bit w: wave w's direction)
+    // EIK_ASYNC_WB: per-pass flags / consumed activations by pass parity, and the count of waves
+    // whose stores have drained (4 per pass, cumulative over the visit)
+    unsigned flagsP[2], pendP[2], drained;
 };
 
 // ---------------------------------------------------------------------------- tile body
@@ -260,6 +301,9 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
         L.flags = 0;
         L.flags_acc = 0;
         L.pend = 0;
+        L.flagsP[0] = L.flagsP[1] = 0u;  // (EIK_ASYNC_WB; read after the staging barrier)
+        L.pendP[0] = L.pendP[1] = 0u;
+        L.drained = 0u;
     }
     if (tid < 5) L.key[tid] = 0x7f800000u;
     // halo ring: wave 0 north row, 1 south row, 2 west column, 3 east column.  In a tile cut by
@@ -269,22 +313,35 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
     // the ring's own row / column is never an upstream value of a finite-cost cell).
     const int64_t sy = y0 + kTile < a.H ? y0 + kTile : a.H;
     const int64_t sx = x0 + kTile < a.W ? x0 + kTile : a.W;
-    int h, hcol;  // this lane's halo cell and its LDS column
-    if (wave == 0)      { hcol = lane + 1;              h = 0 * kLds + hcol; }
-    else if (wave == 1) { hcol = lane + 1;              h = (int)(sy - y0 + 1) * kLds + hcol; }
-    else if (wave == 2) { hcol = 0;                     h = (lane + 1) * kLds + hcol; }
-    else                { hcol = (int)(sx - x0 + 1);    h = (lane + 1) * kLds + hcol; }
-    // this lane's halo cell; in range of the raster: one unconditional load (no branch, so it
-    // issues together with the staging loads), else a ghost strip or +inf
-    const int64_t hy = wave == 0 ? y0 - 1 : wave == 1 ? sy : y0 + lane;
-    const int64_t hx = wave == 0 || wave == 1 ? x0 + lane : wave == 2 ? x0 - 1 : sx;
-    const bool h_in = hy >= 0 && hy < a.H && hx >= 0 && hx < a.W;
-    const int64_t h_idx = h_in ? hy * a.W + hx : 0;
-    auto load_halo = [&]() {
-        R v = T.ld(h_idx);
-        if (!h_in) v = load_T<R, COH>(a, T, hy, hx);
+    // lane's cell of halo side k (0 north row, 1 south row, 2 west column, 3 east column): its LDS
+    // cell and column, and its raster position (in range: one unconditional load, else a ghost
+    // strip or +inf)
+    struct Halo {
+        int h, hcol;
+        int64_t hy, hx, idx;
+        bool in;
+    };
+    auto halo_of = [&](int k) {
+        Halo q;
+        if (k == 0)      { q.hcol = lane + 1;            q.h = 0 * kLds + q.hcol; }
+        else if (k == 1) { q.hcol = lane + 1;            q.h = (int)(sy - y0 + 1) * kLds + q.hcol; }
+        else if (k == 2) { q.hcol = 0;                   q.h = (lane + 1) * kLds + q.hcol; }
+        else             { q.hcol = (int)(sx - x0 + 1);  q.h = (lane + 1) * kLds + q.hcol; }
+        q.hy = k == 0 ? y0 - 1 : k == 1 ? sy : y0 + lane;
+        q.hx = k == 0 || k == 1 ? x0 + lane : k == 2 ? x0 - 1 : sx;
+        q.in = q.hy >= 0 && q.hy < a.H && q.hx >= 0 && q.hx < a.W;
+        q.idx = q.in ? q.hy * a.W + q.hx : 0;
+        return q;
+    };
+    auto load_halo_of = [&](const Halo& q) {
+        R v = T.ld(q.idx);
+        if (!q.in) v = load_T<R, COH>(a, T, q.hy, q.hx);
         return v;
     };
+    // this wave's side (staging, and the synchronous in-place reload)
+    const Halo hw = halo_of(wave);
+    const int h = hw.h, hcol = hw.hcol;
+    auto load_halo = [&]() { return load_halo_of(hw); };
     // ---- stage the tile: 16 cells per thread (4 rows x 4 consecutive columns).  Every global
     // load of the visit (T, cost, halo) is issued before the first LDS store, and each path does
     // its own stores (no loaded value flows through a join, whose register copies would wait for
@@ -362,18 +419,68 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
         if (act_tile >= 0) qpush_complete(a, act_tile, act_old);
         act_tile = -1;
     };
+    // EIK_ASYNC_WB (persistent mode): the previous pass's write-back flags whose neighbour
+    // activations this sweep issues (wave 0), and wave 1's consumed activations / halo reload
+    constexpr bool kAsync = COH && EIK_ASYNC_WB;
+    unsigned act_f = 0u, pend_c = 0u;
+    unsigned long long charged = 0ull;
+    R hv4[4];
     for (int pass = 0;; ++pass) {
+        // in-sweep duties (EIK_ASYNC_WB, see kDrainStep), else wave 0's split activation
+        auto hook = [&](int st) {
+            if constexpr (kAsync) {
+                if (st == kDrainStep) {  // this wave's stores of the last boundary have landed
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if (lane == 0) atomicAdd(&L.drained, 1u);
+                }
+                if (wave == 0) {
+                    if (st == kActIssueStep && act_f != 0u) {
+                        // every wave has drained (Guideline 16 through an LDS counter), then signal
+                        const unsigned want = 4u * (unsigned)(pass + 1);
+                        while (__hip_atomic_load(&L.drained, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
+                            __builtin_amdgcn_s_sleep(1);
+                        act_tile = activate_neighbours_issue(a, tile, act_f, act_old);
+                    }
+                    if (st == kActDoneStep) act_complete();
+                } else if (wave == 1) {
+                    if (st == kConsumeStep && lane == 0) {
+                        if (a.sched & 1) pend_c = atomicAnd(&a.qstate[tile], kBusy | kVisited);
+                        if (pass > 0) charged = atomicAdd(a.visits + 1, 1ull) + 1ull;  // in-place passes: stats + budget
+                    }
+                    if (st == kHaloLoadStep) {
+                        // the consumption has returned: every activation it took had its edge
+                        // drained before it was signalled, so these loads see it
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        if (lane == 0 && pass > 0 && (charged & 63ull) == 0ull &&
+                            charged + __hip_atomic_load(a.visits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.qbudget)
+                            atomicOr(a.qerror, 2u);
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) hv4[k] = load_halo_of(halo_of(k));
+                    }
+                    if (st == kHaloStoreStep) {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            const Halo q = halo_of(k);
+                            cell_t(Ts, q.h, q.hcol) = hv4[k];
+                        }
+                        if (lane == 0) L.pendP[pass & 1] = pend_c;
+                    }
+                }
+            } else if (EIK_ACT_SPLIT && wave == 0 && st == kActStep) {
+                act_complete();
+            }
+        };
         // ---- sweep rounds (quadrant directions concurrently, one per wave; `dirs` selects them)
         const bool sweep = (dirs >> wave) & 1u;
         bool last_changed = false;
         if (a.max_rounds == 1) {  // single round: "changed" is read off the write-back below
             if (sweep) {
-                if (wave == 0)      sweep_quadrant<R, +1, +1, false>(Ts, lane, keep, act_complete);
-                else if (wave == 1) sweep_quadrant<R, -1, +1, false>(Ts, lane, keep);
-                else if (wave == 2) sweep_quadrant<R, +1, -1, false>(Ts, lane, keep);
-                else                sweep_quadrant<R, -1, -1, false>(Ts, lane, keep);
-            } else if (EIK_ACT_SPLIT && wave == 0) {
-                act_complete();
+                if (wave == 0)      sweep_quadrant<R, +1, +1, false>(Ts, lane, keep, hook);
+                else if (wave == 1) sweep_quadrant<R, -1, +1, false>(Ts, lane, keep, hook);
+                else if (wave == 2) sweep_quadrant<R, +1, -1, false>(Ts, lane, keep, hook);
+                else                sweep_quadrant<R, -1, -1, false>(Ts, lane, keep, hook);
+            } else {  // a wave without a sweep this pass still does its duties, in step order
+                for (int st = 0; st < 2 * kTile; st += kAhead) hook(st);
             }
             __syncthreads();
         } else {
@@ -390,6 +497,77 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
                 last_changed = (L.round >> (round & 31)) & 1u;
                 if (!last_changed || round + 1 >= a.max_rounds) break;
             }
+            if constexpr (kAsync) {  // (multi-round visits end after this pass: drain for the count)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        }
+
+        if constexpr (kAsync) {
+            // ---- asynchronous boundary: store the changed rows (sc1, not drained: the next
+            // sweep's kDrainStep waits for them), collect the flags, decide
+            unsigned fl = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int ry = (tid >> 4) + 16 * k;
+                const int64_t gy = y0 + ry;
+                R nv[4];
+                bool any = false;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    nv[e] = cell_t(Ts, (ry + 1) * kLds + cx + e + 1, cx + e + 1);
+                    any |= nv[e] < told[4 * k + e];
+                    if (nv[e] < told[4 * k + e] * keep && (full || (gy < a.H && x0 + cx + e < a.W))) {
+                        fl |= 128u;
+                        const int lx = cx + e + 1, ly = ry + 1;
+                        if (ry == 0 && nv[e] < cell_t(Ts, lx, lx)) fl |= 1u;
+                        if (ry == kTile - 1 && nv[e] < cell_t(Ts, (kLds - 1) * kLds + lx, lx)) fl |= 2u;
+                        if (cx + e == 0 && nv[e] < cell_t(Ts, ly * kLds, 0)) fl |= 4u;
+                        if (cx + e == kTile - 1 && nv[e] < cell_t(Ts, ly * kLds + kLds - 1, kLds - 1)) fl |= 8u;
+                        const int64_t gx = x0 + cx + e;
+                        if (gy == a.H - 1 && ry != kTile - 1) fl |= 32u;
+                        if (gx == a.W - 1 && cx + e != kTile - 1) fl |= 64u;
+                    }
+                }
+                if (any) {
+                    if (full) {
+                        T.st4(gy * a.W + x0 + cx, nv);
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const int64_t gx = x0 + cx + e;
+                            if (gy < a.H && gx < a.W && nv[e] < told[4 * k + e]) T.st(gy * a.W + gx, nv[e]);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) told[4 * k + e] = nv[e];  // what memory holds once they land
+            }
+            if (fl) atomicOr(&L.flagsP[pass & 1], fl);
+            if (tid == 0) {  // the other parity's words serve the next pass
+                L.flagsP[(pass + 1) & 1] = 0u;
+                L.pendP[(pass + 1) & 1] = 0u;
+            }
+            __syncthreads();
+            const unsigned f = L.flagsP[pass & 1];
+            const unsigned pend_all = L.pendP[pass & 1];
+            const unsigned pend = pend_all & (kPending | kFromN | kFromS | kFromW | kFromE);
+            const bool self = (f & 128u) != 0u;
+            if ((!self && !pend) || pass + 1 >= a.max_passes || a.max_rounds != 1) {
+                // the visit ends: every wave's stores land before the activations and the finish
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (tid == 0) {
+                    L.flags = f;
+                    L.pend = pend_all;
+                    L.last = a.max_rounds == 1 ? -1 : (int)last_changed;
+                }
+                __syncthreads();
+                break;
+            }
+            const bool defer = (a.sched & 2) && pass > 0;
+            act_f = defer ? 0u : f;  // wave 0 signals them from the next sweep, once drained
+            if (defer && tid == 0) L.flags_acc |= f & 0x6fu;
+            dirs = self ? 0xFu : sweep_dirs(pend);
+            continue;
         }
 
         EIK_PROBE(2);
