@@ -66,43 +66,12 @@ __device__ __forceinline__ R stage_cost(R c) {
 #endif
 constexpr int kActStep = EIK_ACT_STEP;
 
-// EIK_ASYNC_WB (persistent in-place passes): a pass boundary issues the write-back's sc1 stores
-// and goes straight into the next sweep -- no drain, no halo-reload round trip on the tile's own
-// timeline.  The duties the boundary used to wait for run inside the next sweep, at group steps:
-//   kDrainStep      every wave waits for its own stores (s_waitcnt vmcnt(0)) and counts itself
-//                   in LDS (L.drained);
-//   kActIssueStep   wave 0, once all four waves have counted: the neighbour activations of the
-//                   previous pass's write-back (state-word atomics; the recipe of Guideline 16:
-//                   every storing wave drained before the signal, through an LDS counter);
-//   kActDoneStep    wave 0 finishes their queueing (qpush_complete);
-//   kConsumeStep    wave 1 consumes the activations that reached this busy tile (atomicAnd of
-//                   its state word) and charges the pass to the visit budget;
-//   kHaloLoadStep   wave 1, after that atomic has returned: loads the whole halo ring (4 sides);
-//   kHaloStoreStep  wave 1 stores it into the LDS ring (the remaining steps of this sweep may read
-//                   the fresher values: they only lower upper bounds) and publishes what it
-//                   consumed for the boundary's continue / direction decision.
-// A visit's last pass drains at the boundary as before (its activations and the finish follow).
-// Measured and OFF (profiles/r04c_async_wb_ab.log): C2 fp64 2.36 -> 3.3-4.0 ms for every choice of
-// steps, tile visits +40-120 %.  The drain is the front's hop either way -- a neighbour may only be
-// activated once the edge it reads has landed -- and the mid-sweep consumption and halo reload serve
-// fewer activations per pass than the boundary's.
-#ifndef EIK_ASYNC_WB
-#define EIK_ASYNC_WB 0
-#endif
-#ifndef EIK_DRAIN_STEP
-#define EIK_DRAIN_STEP 40
-#endif
-#ifndef EIK_CONSUME_STEP
-#define EIK_CONSUME_STEP 72
-#endif
-constexpr int kDrainStep = EIK_DRAIN_STEP;
-constexpr int kActIssueStep = EIK_DRAIN_STEP + 4;
-constexpr int kActDoneStep = EIK_DRAIN_STEP + 24;
-constexpr int kConsumeStep = EIK_CONSUME_STEP;
-constexpr int kHaloLoadStep = EIK_CONSUME_STEP + 16;
-constexpr int kHaloStoreStep = EIK_CONSUME_STEP + 36;
-static_assert(kDrainStep % kAhead == 0 && kConsumeStep % kAhead == 0 && kHaloStoreStep < 2 * kTile &&
-              kActDoneStep < 2 * kTile, "in-sweep duty steps: group boundaries of the 2 kTile-step sweep");
+// (EIK_ASYNC_WB, round 4: the pass boundary's write-back drain moved into the next sweep -- every
+// wave waiting for its own stores mid-sweep, wave 0 activating the neighbours once all four had
+// drained, wave 1 consuming activations and reloading the halo ring mid-sweep.  Measured and
+// removed: C2 fp64 2.36 -> 3.3-4.0 ms for every choice of steps, tile visits +40-120 %
+// (profiles/r04c_async_wb_ab.log).  The drain is the front's hop either way -- a neighbour may be
+// activated only once the edge it reads has landed.)
 
 // ------------------------------------------------------------------------- quadrant sweep
 // A tile cell in LDS: arrival time and cost side by side, so one ds_read_b64 (fp32) fetches both.
@@ -269,9 +238,6 @@ struct TileLds {
     unsigned key[5];    // min new value entering: self, N, S, W, E (f32 bits; ordered mode)
     int defer, tile, last;
     unsigned dirs;      // quadrant sweeps of this visit (bit w: wave w's direction)
-    // EIK_ASYNC_WB: per-pass flags / consumed activations by pass parity, and the count of waves
-    // whose stores have drained (4 per pass, cumulative over the visit)
-    unsigned flagsP[2], pendP[2], drained;
 };
 
 // ---------------------------------------------------------------------------- tile body
@@ -301,9 +267,6 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
         L.flags = 0;
         L.flags_acc = 0;
         L.pend = 0;
-        L.flagsP[0] = L.flagsP[1] = 0u;  // (EIK_ASYNC_WB; read after the staging barrier)
-        L.pendP[0] = L.pendP[1] = 0u;
-        L.drained = 0u;
     }
     if (tid < 5) L.key[tid] = 0x7f800000u;
     // halo ring: wave 0 north row, 1 south row, 2 west column, 3 east column.  In a tile cut by
@@ -419,56 +382,10 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
         if (act_tile >= 0) qpush_complete(a, act_tile, act_old);
         act_tile = -1;
     };
-    // EIK_ASYNC_WB (persistent mode): the previous pass's write-back flags whose neighbour
-    // activations this sweep issues (wave 0), and wave 1's consumed activations / halo reload
-    constexpr bool kAsync = COH && EIK_ASYNC_WB;
-    unsigned act_f = 0u, pend_c = 0u;
-    unsigned long long charged = 0ull;
-    R hv4[4];
     for (int pass = 0;; ++pass) {
-        // in-sweep duties (EIK_ASYNC_WB, see kDrainStep), else wave 0's split activation
+        // in-sweep duties, by group step: wave 0's split activation (EIK_ACT_SPLIT)
         auto hook = [&](int st) {
-            if constexpr (kAsync) {
-                if (st == kDrainStep) {  // this wave's stores of the last boundary have landed
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    if (lane == 0) atomicAdd(&L.drained, 1u);
-                }
-                if (wave == 0) {
-                    if (st == kActIssueStep && act_f != 0u) {
-                        // every wave has drained (Guideline 16 through an LDS counter), then signal
-                        const unsigned want = 4u * (unsigned)(pass + 1);
-                        while (__hip_atomic_load(&L.drained, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
-                            __builtin_amdgcn_s_sleep(1);
-                        act_tile = activate_neighbours_issue(a, tile, act_f, act_old);
-                    }
-                    if (st == kActDoneStep) act_complete();
-                } else if (wave == 1) {
-                    if (st == kConsumeStep && lane == 0) {
-                        if (a.sched & 1) pend_c = atomicAnd(&a.qstate[tile], kBusy | kVisited);
-                        if (pass > 0) charged = atomicAdd(a.visits + 1, 1ull) + 1ull;  // in-place passes: stats + budget
-                    }
-                    if (st == kHaloLoadStep) {
-                        // the consumption has returned: every activation it took had its edge
-                        // drained before it was signalled, so these loads see it
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        if (lane == 0 && pass > 0 && (charged & 63ull) == 0ull &&
-                            charged + __hip_atomic_load(a.visits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.qbudget)
-                            atomicOr(a.qerror, 2u);
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) hv4[k] = load_halo_of(halo_of(k));
-                    }
-                    if (st == kHaloStoreStep) {
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) {
-                            const Halo q = halo_of(k);
-                            cell_t(Ts, q.h, q.hcol) = hv4[k];
-                        }
-                        if (lane == 0) L.pendP[pass & 1] = pend_c;
-                    }
-                }
-            } else if (EIK_ACT_SPLIT && wave == 0 && st == kActStep) {
-                act_complete();
-            }
+            if (EIK_ACT_SPLIT && wave == 0 && st == kActStep) act_complete();
         };
         // ---- sweep rounds (quadrant directions concurrently, one per wave; `dirs` selects them)
         const bool sweep = (dirs >> wave) & 1u;
@@ -497,77 +414,6 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
                 last_changed = (L.round >> (round & 31)) & 1u;
                 if (!last_changed || round + 1 >= a.max_rounds) break;
             }
-            if constexpr (kAsync) {  // (multi-round visits end after this pass: drain for the count)
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-        }
-
-        if constexpr (kAsync) {
-            // ---- asynchronous boundary: store the changed rows (sc1, not drained: the next
-            // sweep's kDrainStep waits for them), collect the flags, decide
-            unsigned fl = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int ry = (tid >> 4) + 16 * k;
-                const int64_t gy = y0 + ry;
-                R nv[4];
-                bool any = false;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    nv[e] = cell_t(Ts, (ry + 1) * kLds + cx + e + 1, cx + e + 1);
-                    any |= nv[e] < told[4 * k + e];
-                    if (nv[e] < told[4 * k + e] * keep && (full || (gy < a.H && x0 + cx + e < a.W))) {
-                        fl |= 128u;
-                        const int lx = cx + e + 1, ly = ry + 1;
-                        if (ry == 0 && nv[e] < cell_t(Ts, lx, lx)) fl |= 1u;
-                        if (ry == kTile - 1 && nv[e] < cell_t(Ts, (kLds - 1) * kLds + lx, lx)) fl |= 2u;
-                        if (cx + e == 0 && nv[e] < cell_t(Ts, ly * kLds, 0)) fl |= 4u;
-                        if (cx + e == kTile - 1 && nv[e] < cell_t(Ts, ly * kLds + kLds - 1, kLds - 1)) fl |= 8u;
-                        const int64_t gx = x0 + cx + e;
-                        if (gy == a.H - 1 && ry != kTile - 1) fl |= 32u;
-                        if (gx == a.W - 1 && cx + e != kTile - 1) fl |= 64u;
-                    }
-                }
-                if (any) {
-                    if (full) {
-                        T.st4(gy * a.W + x0 + cx, nv);
-                    } else {
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            const int64_t gx = x0 + cx + e;
-                            if (gy < a.H && gx < a.W && nv[e] < told[4 * k + e]) T.st(gy * a.W + gx, nv[e]);
-                        }
-                    }
-                }
-#pragma unroll
-                for (int e = 0; e < 4; ++e) told[4 * k + e] = nv[e];  // what memory holds once they land
-            }
-            if (fl) atomicOr(&L.flagsP[pass & 1], fl);
-            if (tid == 0) {  // the other parity's words serve the next pass
-                L.flagsP[(pass + 1) & 1] = 0u;
-                L.pendP[(pass + 1) & 1] = 0u;
-            }
-            __syncthreads();
-            const unsigned f = L.flagsP[pass & 1];
-            const unsigned pend_all = L.pendP[pass & 1];
-            const unsigned pend = pend_all & (kPending | kFromN | kFromS | kFromW | kFromE);
-            const bool self = (f & 128u) != 0u;
-            if ((!self && !pend) || pass + 1 >= a.max_passes || a.max_rounds != 1) {
-                // the visit ends: every wave's stores land before the activations and the finish
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (tid == 0) {
-                    L.flags = f;
-                    L.pend = pend_all;
-                    L.last = a.max_rounds == 1 ? -1 : (int)last_changed;
-                }
-                __syncthreads();
-                break;
-            }
-            const bool defer = (a.sched & 2) && pass > 0;
-            act_f = defer ? 0u : f;  // wave 0 signals them from the next sweep, once drained
-            if (defer && tid == 0) L.flags_acc |= f & 0x6fu;
-            dirs = self ? 0xFu : sweep_dirs(pend);
-            continue;
         }
 
         EIK_PROBE(2);
