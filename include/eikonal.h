@@ -149,7 +149,9 @@ int eik_tmap3d_f64(eik_ctx* ctx, const double* cost, int64_t H, int64_t W, int64
 /* FastMarching3D.computeTmap(costMap, goal, start) :126-145 as the planner calls it
  * (Coupled_motion_planner.py:1636): the loop breaks once `start` is popped (:141), so T is the
  * PARTIAL field -- cells popped before `start` (T < T[start]) and `start` at their final values,
- * the narrow band at its local solve over the closed cells, +inf elsewhere (eik_fim3d_early_exit).
+ * the narrow band (finite cost, a closed 6-neighbour) at its converged full-field value -- <= the
+ * reference's tentative value, which depends on its sequential update order --
+ * and +inf elsewhere (eik_fim3d_early_exit).
  * start == goal, a start outside the volume or an unreachable start -> the full field, as in the
  * reference (it never pops such a start). */
 int eik_tmap3d_early_f32(eik_ctx* ctx, const float* cost, int64_t H, int64_t W, int64_t L, const int64_t goal[3],

@@ -8,8 +8,8 @@ sumlist :103-107, getMinNB :109-123, interpolatePoint :275-314.
 Layout as in the reference: cost[y, x, z], nodes (x, y, z).  computeTmap returns the reference's
 PARTIAL field: its loop breaks once `start` is popped (:141), so cells popped before `start`
 (T < T[start]) and `start` hold their final values (same as the full field, <= 1e-9), the narrow
-band holds a tentative value (here: the local solve over the closed cells; the reference's value
-also depends on its sequential update order) and every other cell +inf.  getPathGDM's np.gradient
+band holds a tentative value (here: its converged full-field value, <= the reference's, whose
+value depends on its sequential update order: within 3 %, tests/band.py) and every other cell +inf.  getPathGDM's np.gradient
 (:200) sees those +inf cells, which is why the planner's end-effector path needs this field and
 not the full one (tests/golden/fm3d_early.npz: identical paths on cubes and arm volumes).
 start == goal, outside the volume or unreachable: the reference never pops it -> full field.

@@ -277,10 +277,10 @@ __device__ __forceinline__ void activate(const Fim2dArgs& a, int tile, int list,
 }
 
 // Neighbour activations of a write-back with flags f: thread q in 1..4 handles one side (their
-// atomics overlap); thread 0 flags changed subdomain edges for the halo exchange.
+// atomics overlap); thread 0 flags changed subdomain edges for the halo exchange.  (`tid`: the
+// caller's index for this role -- a lane of any one wave may serve, fim2d.hip's follow-through.)
 __device__ __forceinline__ void activate_neighbours(const Fim2dArgs& a, int tile, unsigned f, const unsigned* key,
-                                                    int list, unsigned stamp) {
-    const int tid = threadIdx.x;
+                                                    int list, unsigned stamp, int tid = threadIdx.x) {
     if (tid >= 5) return;
     const int map = tile / a.tiles_per_map;
     const int rem = tile - map * a.tiles_per_map;

@@ -4,7 +4,7 @@
 outputs (tests/golden/fm3d_early.npz: cubes + end-effector volumes; fmm3d.npz: layered + cubes).
 
 Tolerances: finite masks equal; closed cells (reference T < T[start]) <= 1e-9; band cells hold
-their final value, bracketed GPU <= reference <= 1.05 x GPU (the reference's tentative band value
+their final value, bracketed GPU <= reference <= 1.03 x GPU (the reference's tentative band value
 depends on its sequential update order; measured <= 1.5 % on the fixtures, <= 2.6 % on the
 random arm areas of tests/test_gpu_arm.py); paths <= 1e-9."""
 import numpy as np
@@ -12,6 +12,7 @@ import pytest
 
 import FastMarching.FastMarching3D as FM3D
 import oracle as O
+from band import BAND_BRACKET, band_ratio
 import planner
 
 pytestmark = pytest.mark.gpu
@@ -35,7 +36,9 @@ def check_early(T, R, s):
     assert np.abs(T[closed] - R[closed]).max() <= 1e-9
     assert abs(T[s[1], s[0], s[2]] - ts) <= 1e-9
     band = np.isfinite(R) & ~closed
-    assert np.all(T[band] <= R[band] + 1e-9) and np.all(R[band] <= 1.05 * T[band] + 1e-9)
+    assert np.all(T[band] <= R[band] + 1e-9)
+    r = band_ratio(T, R, band)
+    assert r <= BAND_BRACKET, f"band: reference / GPU up to {r:.4f} (bracket {BAND_BRACKET})"
 
 
 @pytest.mark.parametrize("name,p", CASES)
