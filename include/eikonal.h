@@ -222,6 +222,13 @@ int eik_node_shm_open(const char* name, int64_t bytes, int create, void** addr);
 int eik_node_shm_close(void* addr, int64_t bytes);
 int eik_node_shm_unlink(const char* name);
 
+/* Page-locked host memory for the drop-in's returned fields (FastMarching.computeTmap, ...): the
+ * host entry points copy a registered pinned buffer as ONE DMA at PCIe speed instead of through
+ * their staging ring (host threads memcpy'ing 8 MiB chunks), e.g. a field returned by
+ * eik_tmap2d_f64 and handed back to eik_path2d_f64.  Thread-safe; no context needed. */
+int eik_host_alloc(int64_t bytes, void** out);
+int eik_host_free(void* p);
+
 /* Device buffers shared between the processes of one node (hipIpc handles, 64 bytes). */
 int eik_ipc_alloc(eik_ctx* ctx, int64_t bytes, void** d_ptr, unsigned char handle[64]);
 int eik_ipc_free(eik_ctx* ctx, void* d_ptr);

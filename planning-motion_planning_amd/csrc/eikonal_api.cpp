@@ -221,6 +221,16 @@ static int bytes_per_pass(bool f64) { return (f64 ? 8 : 4) * (kTile * kTile + 4 
 // host_to_dev returns once the source has been read (the DMA of the last chunk may still run on
 // st); dev_to_host returns with the data in dst (it waits for st's earlier work).
 constexpr size_t kStageChunk = 8ull << 20;
+// pinned host blocks handed out by eik_host_alloc: a copy wholly inside one goes as one DMA
+static std::mutex g_pin_mu;
+static std::vector<std::pair<uintptr_t, size_t>> g_pinned;
+static bool is_pinned(const void* p, size_t bytes) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    for (const auto& b : g_pinned)
+        if (a >= b.first && a + bytes <= b.first + b.second) return true;
+    return false;
+}
 static hipError_t stage_init(eik_ctx* c) {
     for (int b = 0; b < 2; ++b) {
         if (!c->stage[b]) {
@@ -236,7 +246,7 @@ static hipError_t stage_init(eik_ctx* c) {
     return hipSuccess;
 }
 static hipError_t host_to_dev(eik_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st) {
-    if (bytes < 2 * kStageChunk) return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
+    if (bytes < 2 * kStageChunk || is_pinned(src, bytes)) return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
     hipError_t e = stage_init(c);
     if (e != hipSuccess) return e;
     int k = 0;
@@ -252,7 +262,7 @@ static hipError_t host_to_dev(eik_ctx* c, void* dst, const void* src, size_t byt
     return hipSuccess;
 }
 static hipError_t dev_to_host(eik_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st) {
-    if (bytes < 2 * kStageChunk) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st);
+    if (bytes < 2 * kStageChunk || is_pinned(dst, bytes)) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st);
     hipError_t e = stage_init(c);
     if (e != hipSuccess) return e;
     const size_t nch = (bytes + kStageChunk - 1) / kStageChunk;
@@ -823,6 +833,31 @@ int eik_fim2d_release(eik_fim2d* f, int64_t* active) {
 }
 
 // ---------------------------------------------------------------- inter-process buffers
+int eik_host_alloc(int64_t bytes, void** out) {
+    if (!out || bytes <= 0) return EIK_ERR_ARG;
+    *out = nullptr;
+    void* p = nullptr;
+    const hipError_t e = hipHostMalloc(&p, (size_t)bytes, hipHostMallocDefault);
+    if (e != hipSuccess) return set_err(nullptr, EIK_ERR_NOMEM, "pinned host allocation of %lld bytes: %s",
+                                        (long long)bytes, hipGetErrorString(e));
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    g_pinned.emplace_back(reinterpret_cast<uintptr_t>(p), (size_t)bytes);
+    *out = p;
+    return EIK_OK;
+}
+
+int eik_host_free(void* p) {
+    if (!p) return EIK_OK;
+    {
+        std::lock_guard<std::mutex> lk(g_pin_mu);
+        auto it = std::find_if(g_pinned.begin(), g_pinned.end(),
+                               [&](const std::pair<uintptr_t, size_t>& b) { return b.first == reinterpret_cast<uintptr_t>(p); });
+        if (it == g_pinned.end()) return EIK_ERR_ARG;
+        g_pinned.erase(it);
+    }
+    return hipHostFree(p) == hipSuccess ? EIK_OK : EIK_ERR_HIP;
+}
+
 int eik_ipc_alloc(eik_ctx* c, int64_t bytes, void** d_ptr, unsigned char handle[64]) {
     if (!c || !d_ptr || !handle || bytes <= 0) return EIK_ERR_ARG;
     static_assert(sizeof(hipIpcMemHandle_t) <= 64, "IPC handle size");

@@ -80,7 +80,35 @@ constexpr int kActStep = EIK_ACT_STEP;
 #ifndef EIK_FOLLOW
 #define EIK_FOLLOW 1
 #endif
+// at most this many follow-throughs per grabbed tile: an unbounded chain runs ahead of the front
+// along one line -- each followed tile sees one side's information only, so the chain leaves poor
+// upper bounds behind that the real front must revisit (C2 fp64 2.35 -> 4.4 ms, C4 11 -> 0.8 Gcells/s)
+#ifndef EIK_FOLLOW_MAX
+#define EIK_FOLLOW_MAX 1
+#endif
 constexpr int kRetireDrainStep = 24;   // a followed tile's first pass: sweeping waves count their drain
+
+// EIK_SPLIT_WB (persistent in-place passes): a split-role pass boundary.  Waves 2 and 3 store the
+// write-back (their own changed row chunks, then waves 0-1's, whose chunk masks go through LDS) and
+// do NOT wait for the stores; waves 0 and 1 consume the tile's activations (wave 0, awaited) and then
+// reload the whole halo ring -- their loads wait for no store, since they issued none.  The next pass
+// starts after the halo round trip alone; the storing waves wait for their own stores at
+// kSplitDrainStep of the next sweep (LDS counter), and wave 2 then activates the neighbours the
+// write-back improved (qpush issue, completed at kSplitActDoneStep): a neighbour is still activated
+// only once the edge it reads has landed.  A visit's last pass drains at its boundary as before.
+#ifndef EIK_SPLIT_WB
+#define EIK_SPLIT_WB 1
+#endif
+#ifndef EIK_FP32_BOUNDARY
+#define EIK_FP32_BOUNDARY 0
+#endif
+#ifndef EIK_SPLIT_DRAIN_STEP
+#define EIK_SPLIT_DRAIN_STEP 16
+#endif
+constexpr int kSplitDrainStep = EIK_SPLIT_DRAIN_STEP;
+constexpr int kSplitActStep = EIK_SPLIT_DRAIN_STEP + 4;
+constexpr int kSplitActDoneStep = EIK_SPLIT_DRAIN_STEP + 24;
+static_assert(kSplitDrainStep % kAhead == 0 && kSplitActDoneStep < 2 * kTile, "split boundary duty steps");
 
 // (EIK_ASYNC_WB, round 4: the pass boundary's write-back drain moved into the next sweep -- every
 // wave waiting for its own stores mid-sweep, wave 0 activating the neighbours once all four had
@@ -260,6 +288,10 @@ struct TileLds {
     int follow;
     unsigned drained;
     R emin[4];
+    // EIK_SPLIT_WB: the storing waves' drains (2 per pass boundary, cumulative over a visit) and the
+    // control threads' changed row chunks (bit k: row chunk k of thread t)
+    unsigned sdrained;
+    unsigned char chg[128];
 };
 
 // ---------------------------------------------------------------------------- tile body
@@ -275,7 +307,11 @@ __device__ __forceinline__ int process_tile(const Fim2dArgs& a, int tile, TileLd
     constexpr R INF = Real<R>::inf();
     Cell<R>* const Ts = L.Tc + kGuard * kLds;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    constexpr bool kFollow = COH && EIK_FOLLOW;
+    // (fp64 only by default: the extra boundary code costs the fp32 kernels registers -- 148 -> 196+
+    // VGPRs, i.e. 3 -> 2 workgroups per CU -- EIK_FP32_BOUNDARY=1 enables them there too)
+    constexpr bool kWide = sizeof(R) == 8 || EIK_FP32_BOUNDARY;
+    constexpr bool kFollow = COH && EIK_FOLLOW && kWide;
+    constexpr bool kSplit = COH && EIK_SPLIT_WB && kWide;
     // EIK_FOLLOW state across the followed tiles of one visit chain: the side of `tile` facing the
     // tile it was followed from (-1: a grabbed tile), this lane's value of that halo side (the
     // previous tile's edge), and the previous tile, retired during this tile's first pass with its
@@ -284,6 +320,7 @@ __device__ __forceinline__ int process_tile(const Fim2dArgs& a, int tile, TileLd
     R fh = INF;
     int ret_tile = -1;
     unsigned ret_f = 0u;
+    int nfollow = 0;  // follow-throughs so far from the grabbed tile
     for (;;) {  // one iteration per tile of the chain (one, unless EIK_FOLLOW continues)
         const int map = tile / a.tiles_per_map;
         const int rem = tile - map * a.tiles_per_map;
@@ -301,6 +338,7 @@ __device__ __forceinline__ int process_tile(const Fim2dArgs& a, int tile, TileLd
             L.pend = 0;
             L.fresh = 0u;
             L.drained = 0u;
+            L.sdrained = 0u;
             if (kFollow && fside >= 0) L.dirs = sweep_dirs(kFromN << fside);  // (a grabbed tile: the grab's)
         }
         if (tid < 5) L.key[tid] = 0x7f800000u;
@@ -438,6 +476,7 @@ __device__ __forceinline__ int process_tile(const Fim2dArgs& a, int tile, TileLd
             if (act_tile >= 0) qpush_complete(a, act_tile, act_old);
             act_tile = -1;
         };
+        unsigned act_f = 0u;  // EIK_SPLIT_WB: the flags wave 2 activates in the next sweep
         unsigned snap = ~0u;  // EIK_FOLLOW: wave 0 lanes 1..4, a neighbour's state word
         bool followed = false;
         // EIK_FOLLOW: retire the previous tile of the chain (one wave; after every wave's stores of
@@ -458,6 +497,20 @@ __device__ __forceinline__ int process_tile(const Fim2dArgs& a, int tile, TileLd
             // in-sweep duties, by group step: wave 0's split activation (EIK_ACT_SPLIT)
             auto hook = [&](int st) {
                 if (EIK_ACT_SPLIT && wave == 0 && st == kActStep) act_complete();
+                if constexpr (kSplit) {
+                    if (wave >= 2 && pass > 0 && st == kSplitDrainStep) {  // the last boundary's stores landed
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        if (lane == 0) atomicAdd(&L.sdrained, 1u);
+                    }
+                    if (wave == 2 && st == kSplitActStep && act_f != 0u) {
+                        const unsigned want = 2u * (unsigned)pass;
+                        while (__hip_atomic_load(&L.sdrained, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
+                            __builtin_amdgcn_s_sleep(1);
+                        act_tile = activate_neighbours_issue(a, tile, act_f, act_old, lane);
+                        act_f = 0u;
+                    }
+                    if (wave == 2 && st == kSplitActDoneStep) act_complete();
+                }
                 if constexpr (kFollow) {
                     // the previous tile of the chain is retired once every wave's stores landed
                     if (ret_tile >= 0 && st == kRetireDrainStep) {
@@ -522,7 +575,7 @@ __device__ __forceinline__ int process_tile(const Fim2dArgs& a, int tile, TileLd
             bool wb_done = false;
             if constexpr (kFollow) {
                 const unsigned fr = __builtin_amdgcn_readfirstlane(L.fresh);  // uniform (published before the sweep-end barrier)
-                if (a.max_rounds == 1 && fr) {
+                if (a.max_rounds == 1 && fr && nfollow < EIK_FOLLOW_MAX) {
                     // this tile's edge toward each fresh side: its smallest value (+inf: not reached)
                     auto edge_cell = [&](int side, int l) {
                         return side == 0 ? kLds + l + 1 : side == 1 ? kTile * kLds + l + 1
@@ -593,11 +646,116 @@ __device__ __forceinline__ int process_tile(const Fim2dArgs& a, int tile, TileLd
                             tile = fol;
                             fside = fs;
                             followed = true;
+                            ++nfollow;
                             __syncthreads();  // L.flags read everywhere before the next tile's init
                             break;
                         }
                         wb_done = true;  // lost the claim: this boundary goes on as usual
                     }
+                }
+            }
+
+            // ---- EIK_SPLIT_WB: the split-role boundary (see kSplitDrainStep)
+            if constexpr (kSplit) {
+                if (a.max_rounds == 1 && !wb_done) {
+                    const bool storer = wave >= 2;
+                    unsigned fl = 0, chg = 0;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int ry = (tid >> 4) + 16 * k;
+                        const int64_t gy = y0 + ry;
+                        R nv[4];
+                        bool any = false;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            nv[e] = cell_t(Ts, (ry + 1) * kLds + cx + e + 1, cx + e + 1);
+                            any |= nv[e] < told[4 * k + e];
+                            if (nv[e] < told[4 * k + e] * keep && (full || (gy < a.H && x0 + cx + e < a.W))) {
+                                fl |= 128u;
+                                const int lx = cx + e + 1, ly = ry + 1;
+                                if (ry == 0 && nv[e] < cell_t(Ts, lx, lx)) fl |= 1u;
+                                if (ry == kTile - 1 && nv[e] < cell_t(Ts, (kLds - 1) * kLds + lx, lx)) fl |= 2u;
+                                if (cx + e == 0 && nv[e] < cell_t(Ts, ly * kLds, 0)) fl |= 4u;
+                                if (cx + e == kTile - 1 && nv[e] < cell_t(Ts, ly * kLds + kLds - 1, kLds - 1)) fl |= 8u;
+                                const int64_t gx = x0 + cx + e;
+                                if (gy == a.H - 1 && ry != kTile - 1) fl |= 32u;
+                                if (gx == a.W - 1 && cx + e != kTile - 1) fl |= 64u;
+                            }
+                        }
+                        if (any) {
+                            if (!storer) {
+                                chg |= 1u << k;
+                            } else if (full) {
+                                T.st4(gy * a.W + x0 + cx, nv);
+                            } else {
+#pragma unroll
+                                for (int e = 0; e < 4; ++e) {
+                                    const int64_t gx = x0 + cx + e;
+                                    if (gy < a.H && gx < a.W && nv[e] < told[4 * k + e]) T.st(gy * a.W + gx, nv[e]);
+                                }
+                            }
+                        }
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) told[4 * k + e] = nv[e];  // what memory holds once they land
+                    }
+                    if (!storer) L.chg[tid] = (unsigned char)chg;
+                    if (fl) atomicOr(&L.flags, fl);
+                    // consume the activations that reached this busy tile (awaited: the halo loads
+                    // below are issued after it has been performed)
+                    if ((a.sched & 1) && tid == 0) L.pend = atomicAnd(&a.qstate[tile], kBusy | kVisited);
+                    __syncthreads();
+                    const unsigned f = L.flags;  // uniform
+                    const unsigned pend_all = L.pend;
+                    const unsigned pend = pend_all & (kPending | kFromN | kFromS | kFromW | kFromE);
+                    const bool self = (f & 128u) != 0u;
+                    if (storer) {  // waves 0-1's changed row chunks (an unchanged cell's LDS value is what memory holds)
+                        const int c = tid - 128;
+                        const unsigned cm = L.chg[c];
+                        const int ccx = (c & 15) * 4;
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            if ((cm >> k) & 1u) {
+                                const int ry = (c >> 4) + 16 * k;
+                                const int64_t gy = y0 + ry;
+                                R nv[4];
+#pragma unroll
+                                for (int e = 0; e < 4; ++e) nv[e] = cell_t(Ts, (ry + 1) * kLds + ccx + e + 1, ccx + e + 1);
+                                if (full) {
+                                    T.st4(gy * a.W + x0 + ccx, nv);
+                                } else {
+#pragma unroll
+                                    for (int e = 0; e < 4; ++e) {
+                                        const int64_t gx = x0 + ccx + e;
+                                        if (gy < a.H && gx < a.W) T.st(gy * a.W + gx, nv[e]);
+                                    }
+                                }
+                            }
+                        }
+                    }
+                    if ((!self && !pend) || pass + 1 >= a.max_passes) {
+                        // the visit ends: its stores land before the activations and the finish
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        if (tid == 0) L.last = -1;
+                        __syncthreads();
+                        break;
+                    }
+                    if (!storer) {  // the halo ring: wave 0 north and west, wave 1 south and east
+                        const Halo q0 = halo_of(wave), q1 = halo_of(wave + 2);
+                        const R v0 = load_halo_of(q0), v1 = load_halo_of(q1);
+                        if (tid == 64) charge_inplace_pass(a);  // in-place passes: stats and the visit budget
+                        cell_t(Ts, q0.h, q0.hcol) = v0;
+                        cell_t(Ts, q1.h, q1.hcol) = v1;
+                    }
+                    const bool defer = (a.sched & 2) && pass > 0;
+                    act_f = defer ? 0u : f;  // wave 2 activates them in the next sweep, once drained
+                    if (defer && tid == 0) L.flags_acc |= f & 0x6fu;
+                    dirs = self ? 0xFu : sweep_dirs(pend);
+                    __syncthreads();  // the halo ring is in; every wave has read L.flags / L.pend
+                    if (tid == 0) {
+                        L.flags = 0;
+                        L.pend = 0;
+                    }
+                    continue;
                 }
             }
 

@@ -305,8 +305,8 @@ __device__ __forceinline__ void activate_neighbours(const Fim2dArgs& a, int tile
 // The issue half of a persistent in-place pass's activations (EIK_ACT_SPLIT): thread q in 1..4
 // issues its side's state-word atomicOr and returns the neighbour (-1: none) with `old` to be
 // passed to qpush_complete later; thread 0 flags changed subdomain edges as above.
-__device__ __forceinline__ int activate_neighbours_issue(const Fim2dArgs& a, int tile, unsigned f, unsigned& old) {
-    const int tid = threadIdx.x;
+__device__ __forceinline__ int activate_neighbours_issue(const Fim2dArgs& a, int tile, unsigned f, unsigned& old,
+                                                         int tid = threadIdx.x) {
     old = 0u;
     if (tid >= 5) return -1;
     const int map = tile / a.tiles_per_map;

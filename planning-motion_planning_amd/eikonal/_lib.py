@@ -143,6 +143,8 @@ def lib():
         L.eik_node_shm_open.argtypes = [C.c_char_p, i64, C.c_int, P(vp)]
         L.eik_node_shm_close.argtypes = [vp, i64]
         L.eik_node_shm_unlink.argtypes = [C.c_char_p]
+        L.eik_host_alloc.argtypes = [i64, P(vp)]
+        L.eik_host_free.argtypes = [vp]
         L.eik_ipc_alloc.argtypes = [vp, i64, P(vp), C.c_char_p]
         L.eik_ipc_free.argtypes = [vp, vp]
         L.eik_ipc_open.argtypes = [vp, C.c_char_p, P(vp)]
@@ -172,7 +174,7 @@ EXPORTED = [
     "eik_fim2d_live_merge", "eik_fim2d_release", "eik_node_allreduce", "eik_node_shm_open",
     "eik_node_shm_close", "eik_node_shm_unlink", "eik_ipc_alloc", "eik_ipc_free", "eik_ipc_open", "eik_ipc_close",
     "eik_rover_assemble", "eik_rover_path_f64", "eik_arm_obst_map_f64", "eik_arm_tunnel_cost_f64",
-    "eik_arm_path_f64", "eik_tmap3d_batch_f64",
+    "eik_arm_path_f64", "eik_tmap3d_batch_f64", "eik_host_alloc", "eik_host_free",
 ]
 
 
@@ -277,7 +279,7 @@ class Context:
     def tmap2d(self, cost, goal, dtype=np.float64):
         cost = np.ascontiguousarray(cost, dtype=dtype)
         H, W = cost.shape
-        T = np.empty_like(cost)
+        T = result_empty(cost.shape, cost.dtype)
         fn = lib().eik_tmap2d_f64 if cost.dtype == np.float64 else lib().eik_tmap2d_f32
         self._chk(fn(self._h, cost, H, W, int(goal[0]), int(goal[1]), T))
         return T
@@ -292,7 +294,7 @@ class Context:
     def tmap2d_bidir(self, cost, goal, start):
         cost = np.ascontiguousarray(cost, dtype=np.float64)
         H, W = cost.shape
-        TG, TS = np.empty_like(cost), np.empty_like(cost)
+        TG, TS = result_empty(cost.shape, cost.dtype), result_empty(cost.shape, cost.dtype)
         join = np.zeros(2, np.uint32)
         self._chk(lib().eik_tmap2d_bidir_f64(self._h, cost, H, W, int(goal[0]), int(goal[1]), int(start[0]),
                                              int(start[1]), TG, TS, join))
@@ -314,7 +316,7 @@ class Context:
         early-exit field (break once `start` is popped, FastMarching3D.py:141)."""
         cost = np.ascontiguousarray(cost, dtype=dtype)
         H, W, Lz = cost.shape
-        T = np.empty_like(cost)
+        T = result_empty(cost.shape, cost.dtype)
         g = np.ascontiguousarray(np.asarray(goal).reshape(-1)[:3], np.int64)
         f64 = cost.dtype == np.float64
         if start is None:
@@ -409,7 +411,7 @@ class Context:
         cost = np.ascontiguousarray(cost, dtype=np.float64)
         B, H, W, Lz = cost.shape
         g = np.ascontiguousarray(goals, np.int64).reshape(-1)
-        T = np.empty_like(cost)
+        T = result_empty(cost.shape, cost.dtype)
         self._chk(lib().eik_tmap3d_batch_f64(self._h, cost, B, H, W, Lz, g, T))
         return T
 
@@ -510,6 +512,56 @@ class Fim2d:
         a = i64(0)
         self.ctx._chk(lib().eik_fim2d_release(self._h, C.byref(a)))
         return a.value
+
+
+# ----------------------------------------------------------------- pinned result arrays
+# The drop-in returns fields of up to hundreds of MiB (a 4096^2 float64 raster is 128 MiB) that the
+# caller hands straight back (computeTmap -> getPathGDM).  Allocated in page-locked memory
+# (eik_host_alloc), they cross PCIe as one DMA each way instead of through the C ABI's staging
+# ring.  Blocks are recycled by size: a returned array owns its block until the last view of it
+# is gone, then the block goes back to the pool (hipHostMalloc of 128 MiB costs milliseconds).
+PINNED_MIN_BYTES = 16 << 20  # below this the ABI copies directly anyway
+_pin_lock = threading.Lock()
+_pin_free = {}  # nbytes -> [ptr, ...]
+_PIN_POOL_MAX = 8  # free blocks kept per size
+
+
+class _PinnedBlock:
+    def __init__(self, nbytes):
+        self.nbytes = nbytes
+        with _pin_lock:
+            free = _pin_free.get(nbytes)
+            ptr = free.pop() if free else None
+        if ptr is None:
+            p = vp()
+            if lib().eik_host_alloc(int(nbytes), C.byref(p)) != EIK_OK:
+                raise MemoryError(lib().eik_last_error(None).decode())
+            ptr = p.value
+        self.ptr = ptr
+
+    def __del__(self):
+        try:
+            with _pin_lock:
+                free = _pin_free.setdefault(self.nbytes, [])
+                if len(free) < _PIN_POOL_MAX:
+                    free.append(self.ptr)
+                    return
+            lib().eik_host_free(self.ptr)
+        except Exception:
+            pass
+
+
+def result_empty(shape, dtype):
+    """An uninitialised C-contiguous array for a returned field: page-locked (recycled) when at
+    least PINNED_MIN_BYTES, else a plain numpy array."""
+    dtype = np.dtype(dtype)
+    n = int(np.prod(shape)) * dtype.itemsize
+    if n < PINNED_MIN_BYTES:
+        return np.empty(shape, dtype)
+    blk = _PinnedBlock(n)
+    buf = (C.c_byte * n).from_address(blk.ptr)
+    buf._owner = blk  # the block lives as long as any view of the array
+    return np.frombuffer(buf, dtype=dtype).reshape(shape)
 
 
 class IpcBuffer:

@@ -204,3 +204,29 @@ def test_walker_fast_math_exact():
             assert counts.tolist() == [0, 0, 0, 1 << 22], counts
     finally:
         c.close()
+
+
+def test_pinned_results_round_trip(ctx):
+    """Fields of >= 16 MiB come back in recycled page-locked blocks (eikonal._lib.result_empty) and
+    cross PCIe as one DMA each way: the field and the path from it equal the pageable route's
+    (a plain copy of the same field), and blocks are reused after the arrays are gone."""
+    from eikonal import _lib as L
+
+    rng = np.random.default_rng(12)
+    N = 1536  # 18 MiB of float64
+    cost = rng.uniform(1, 4, (N, N))
+    cost[rng.random((N, N)) < 0.05] = np.inf
+    goal, start = (N // 2, N // 3), (40, N - 60)
+    cost[goal[1], goal[0]] = cost[start[1], start[0]] = 1.0
+    T = ctx.tmap2d(cost, goal)
+    assert T.nbytes >= L.PINNED_MIN_BYTES and T.flags.c_contiguous and T.flags.writeable
+    Tp = np.array(T, copy=True)  # pageable
+    assert np.array_equal(T, Tp, equal_nan=True)
+    p1, s1 = ctx.path2d(T, start, goal)
+    p2, s2 = ctx.path2d(Tp, start, goal)
+    assert s1 == s2 and np.array_equal(p1, p2)
+    n_free = sum(len(v) for v in L._pin_free.values())
+    del T
+    assert sum(len(v) for v in L._pin_free.values()) == n_free + 1  # back in the pool
+    T2 = ctx.tmap2d(cost, goal)  # reuses it
+    assert np.array_equal(T2, Tp, equal_nan=True)
