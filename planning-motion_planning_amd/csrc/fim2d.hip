@@ -66,50 +66,13 @@ __device__ __forceinline__ R stage_cost(R c) {
 #endif
 constexpr int kActStep = EIK_ACT_STEP;
 
-// EIK_FOLLOW (persistent mode, default on): FOLLOW-THROUGH along the front.  When a pass of a
-// full tile A makes a FRESH neighbour B reachable (B never queued or visited: state word 0, and
-// A's edge toward it finite), the workgroup claims B (a CAS of its state word 0 -> BUSY) and
-// continues with it at once instead of queueing it: B's T is +inf (fresh), so its staging loads
-// only its costs and three halo sides; its fourth side is A's edge straight from LDS.  A's
-// write-back stores are issued in full after the claim (a fixed count, so the claim's result is
-// awaited without the stores' drain) and A is retired during B's first pass by a wave that
-// pass does not sweep: once every wave's stores have landed (LDS counter), A's other neighbours
-// are activated and A is re-queued (kSelf) or finished.  The front's hop into a fresh tile then
-// costs one sweep + the claim + one load round trip instead of the drain, the state-word / tail / slot atomics,
-// the idle workgroup's poll and claim, and the staging (the queue path: ~26 us per hop in fp64).
-#ifndef EIK_FOLLOW
-#define EIK_FOLLOW 1
-#endif
-// at most this many follow-throughs per grabbed tile: an unbounded chain runs ahead of the front
-// along one line -- each followed tile sees one side's information only, so the chain leaves poor
-// upper bounds behind that the real front must revisit (C2 fp64 2.35 -> 4.4 ms, C4 11 -> 0.8 Gcells/s)
-#ifndef EIK_FOLLOW_MAX
-#define EIK_FOLLOW_MAX 1
-#endif
-constexpr int kRetireDrainStep = 24;   // a followed tile's first pass: sweeping waves count their drain
-
-// EIK_SPLIT_WB (persistent in-place passes): a split-role pass boundary.  Waves 2 and 3 store the
-// write-back (their own changed row chunks, then waves 0-1's, whose chunk masks go through LDS) and
-// do NOT wait for the stores; waves 0 and 1 consume the tile's activations (wave 0, awaited) and then
-// reload the whole halo ring -- their loads wait for no store, since they issued none.  The next pass
-// starts after the halo round trip alone; the storing waves wait for their own stores at
-// kSplitDrainStep of the next sweep (LDS counter), and wave 2 then activates the neighbours the
-// write-back improved (qpush issue, completed at kSplitActDoneStep): a neighbour is still activated
-// only once the edge it reads has landed.  A visit's last pass drains at its boundary as before.
-#ifndef EIK_SPLIT_WB
-#define EIK_SPLIT_WB 1
-#endif
-#ifndef EIK_FP32_BOUNDARY
-#define EIK_FP32_BOUNDARY 0
-#endif
-#ifndef EIK_SPLIT_DRAIN_STEP
-#define EIK_SPLIT_DRAIN_STEP 16
-#endif
-constexpr int kSplitDrainStep = EIK_SPLIT_DRAIN_STEP;
-constexpr int kSplitActStep = EIK_SPLIT_DRAIN_STEP + 4;
-constexpr int kSplitActDoneStep = EIK_SPLIT_DRAIN_STEP + 24;
-static_assert(kSplitDrainStep % kAhead == 0 && kSplitActDoneStep < 2 * kTile, "split boundary duty steps");
-
+// (Also measured in round 4 and removed, profiles/r04d_follow_split_ab.log: EIK_FOLLOW -- a workgroup
+// whose pass made a FRESH neighbour reachable claimed it and continued with it, skipping the queue's
+// round trips; and EIK_SPLIT_WB -- two waves stored the write-back without waiting while two
+// reloaded the halo, the activations following the drain from inside the next sweep.  Both did 2-5x
+// the tile visits (C2 fp64 2.35 -> 3.3-6.8 ms, C4 at one GPU 11 -> 0.6-4.7 Gcells/s): tiles reached
+// ahead of the FIFO's order converge against incomplete halos and are revisited, and a delayed
+// activation costs the same.  The FIFO's breadth-first order is worth more than the hops it costs.)
 // (EIK_ASYNC_WB, round 4: the pass boundary's write-back drain moved into the next sweep -- every
 // wave waiting for its own stores mid-sweep, wave 0 activating the neighbours once all four had
 // drained, wave 1 consuming activations and reloading the halo ring mid-sweep.  Measured and
@@ -282,16 +245,6 @@ struct TileLds {
     unsigned key[5];    // min new value entering: self, N, S, W, E (f32 bits; ordered mode)
     int defer, tile, last;
     unsigned dirs;      // quadrant sweeps of this visit (bit w: wave w's direction)
-    // EIK_FOLLOW: fresh full neighbours at this pass's snapshot (bit = side N S W E), the edge
-    // minimum toward each, the claimed tile (-1: none), waves whose stores have landed
-    unsigned fresh;
-    int follow;
-    unsigned drained;
-    R emin[4];
-    // EIK_SPLIT_WB: the storing waves' drains (2 per pass boundary, cumulative over a visit) and the
-    // control threads' changed row chunks (bit k: row chunk k of thread t)
-    unsigned sdrained;
-    unsigned char chg[128];
 };
 
 // ---------------------------------------------------------------------------- tile body
@@ -303,585 +256,293 @@ struct TileLds {
 // Ends with a workgroup barrier; in COH mode every wave has drained its write-through stores
 // before it.
 template <typename R, bool COH>
-__device__ __forceinline__ int process_tile(const Fim2dArgs& a, int tile, TileLds<R>& L, R keep) {
+__device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileLds<R>& L, R keep) {
     constexpr R INF = Real<R>::inf();
     Cell<R>* const Ts = L.Tc + kGuard * kLds;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // (fp64 only by default: the extra boundary code costs the fp32 kernels registers -- 148 -> 196+
-    // VGPRs, i.e. 3 -> 2 workgroups per CU -- EIK_FP32_BOUNDARY=1 enables them there too)
-    constexpr bool kWide = sizeof(R) == 8 || EIK_FP32_BOUNDARY;
-    constexpr bool kFollow = COH && EIK_FOLLOW && kWide;
-    constexpr bool kSplit = COH && EIK_SPLIT_WB && kWide;
-    // EIK_FOLLOW state across the followed tiles of one visit chain: the side of `tile` facing the
-    // tile it was followed from (-1: a grabbed tile), this lane's value of that halo side (the
-    // previous tile's edge), and the previous tile, retired during this tile's first pass with its
-    // write-back flags
-    int fside = -1;
-    R fh = INF;
-    int ret_tile = -1;
-    unsigned ret_f = 0u;
-    int nfollow = 0;  // follow-throughs so far from the grabbed tile
-    for (;;) {  // one iteration per tile of the chain (one, unless EIK_FOLLOW continues)
-        const int map = tile / a.tiles_per_map;
-        const int rem = tile - map * a.tiles_per_map;
-        const int ty = rem / a.ntx, tx = rem - (rem / a.ntx) * a.ntx;
-        const R* __restrict__ cost = static_cast<const R*>(a.cost) + (int64_t)map * a.H * a.W;
-        const TMem<R, COH> T(static_cast<R*>(a.T) + (int64_t)map * a.H * a.W, a.H * a.W);
-        const int64_t y0 = (int64_t)ty * kTile, x0 = (int64_t)tx * kTile;
-        const bool full = (y0 + kTile <= a.H) && (x0 + kTile <= a.W) && ((a.W & 3) == 0);
+    const int map = tile / a.tiles_per_map;
+    const int rem = tile - map * a.tiles_per_map;
+    const int ty = rem / a.ntx, tx = rem - (rem / a.ntx) * a.ntx;
+    const R* __restrict__ cost = static_cast<const R*>(a.cost) + (int64_t)map * a.H * a.W;
+    const TMem<R, COH> T(static_cast<R*>(a.T) + (int64_t)map * a.H * a.W, a.H * a.W);
+    const int64_t y0 = (int64_t)ty * kTile, x0 = (int64_t)tx * kTile;
+    const bool full = (y0 + kTile <= a.H) && (x0 + kTile <= a.W) && ((a.W & 3) == 0);
 
-        EIK_PROBE(0);
-        if (tid == 0) {
-            L.round = 0;
-            L.flags = 0;
-            L.flags_acc = 0;
-            L.pend = 0;
-            L.fresh = 0u;
-            L.drained = 0u;
-            L.sdrained = 0u;
-            if (kFollow && fside >= 0) L.dirs = sweep_dirs(kFromN << fside);  // (a grabbed tile: the grab's)
+    EIK_PROBE(0);
+    if (tid == 0) {
+        L.round = 0;
+        L.flags = 0;
+        L.flags_acc = 0;
+        L.pend = 0;
+    }
+    if (tid < 5) L.key[tid] = 0x7f800000u;
+    // halo ring: wave 0 north row, 1 south row, 2 west column, 3 east column.  In a tile cut by
+    // the raster's south / east end the south row / east column is the one just past the raster
+    // (row H / column W) inside the tile: a subdomain's ghost strip lives there, and the in-place
+    // passes' halo reload must refresh it like any halo (the cells beyond it are +inf cost, so
+    // the ring's own row / column is never an upstream value of a finite-cost cell).
+    const int64_t sy = y0 + kTile < a.H ? y0 + kTile : a.H;
+    const int64_t sx = x0 + kTile < a.W ? x0 + kTile : a.W;
+    // lane's cell of halo side k (0 north row, 1 south row, 2 west column, 3 east column): its LDS
+    // cell and column, and its raster position (in range: one unconditional load, else a ghost
+    // strip or +inf)
+    struct Halo {
+        int h, hcol;
+        int64_t hy, hx, idx;
+        bool in;
+    };
+    auto halo_of = [&](int k) {
+        Halo q;
+        if (k == 0)      { q.hcol = lane + 1;            q.h = 0 * kLds + q.hcol; }
+        else if (k == 1) { q.hcol = lane + 1;            q.h = (int)(sy - y0 + 1) * kLds + q.hcol; }
+        else if (k == 2) { q.hcol = 0;                   q.h = (lane + 1) * kLds + q.hcol; }
+        else             { q.hcol = (int)(sx - x0 + 1);  q.h = (lane + 1) * kLds + q.hcol; }
+        q.hy = k == 0 ? y0 - 1 : k == 1 ? sy : y0 + lane;
+        q.hx = k == 0 || k == 1 ? x0 + lane : k == 2 ? x0 - 1 : sx;
+        q.in = q.hy >= 0 && q.hy < a.H && q.hx >= 0 && q.hx < a.W;
+        q.idx = q.in ? q.hy * a.W + q.hx : 0;
+        return q;
+    };
+    auto load_halo_of = [&](const Halo& q) {
+        R v = T.ld(q.idx);
+        if (!q.in) v = load_T<R, COH>(a, T, q.hy, q.hx);
+        return v;
+    };
+    // this wave's side (staging, and the synchronous in-place reload)
+    const Halo hw = halo_of(wave);
+    const int h = hw.h, hcol = hw.hcol;
+    auto load_halo = [&]() { return load_halo_of(hw); };
+    // ---- stage the tile: 16 cells per thread (4 rows x 4 consecutive columns).  Every global
+    // load of the visit (T, cost, halo) is issued before the first LDS store, and each path does
+    // its own stores (no loaded value flows through a join, whose register copies would wait for
+    // the loads): the compiler does not move the sc1 buffer loads across LDS stores, and the
+    // interleaved form cost one memory round trip per row group (5 serial trips per staging).
+    R told[16];
+    const int cx = (tid & 15) * 4;
+    auto store_tile = [&](const R (&cr)[16], R hv) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int ry = (tid >> 4) + 16 * k;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                Ts[(ry + 1) * kLds + cx + e + 1] = make_cell<R>(told[4 * k + e], stage_cost(cr[4 * k + e]), cx + e + 1);
         }
-        if (tid < 5) L.key[tid] = 0x7f800000u;
-        // halo ring: wave 0 north row, 1 south row, 2 west column, 3 east column.  In a tile cut by
-        // the raster's south / east end the south row / east column is the one just past the raster
-        // (row H / column W) inside the tile: a subdomain's ghost strip lives there, and the in-place
-        // passes' halo reload must refresh it like any halo (the cells beyond it are +inf cost, so
-        // the ring's own row / column is never an upstream value of a finite-cost cell).
-        const int64_t sy = y0 + kTile < a.H ? y0 + kTile : a.H;
-        const int64_t sx = x0 + kTile < a.W ? x0 + kTile : a.W;
-        // lane's cell of halo side k (0 north row, 1 south row, 2 west column, 3 east column): its LDS
-        // cell and column, and its raster position (in range: one unconditional load, else a ghost
-        // strip or +inf)
-        struct Halo {
-            int h, hcol;
-            int64_t hy, hx, idx;
-            bool in;
-        };
-        auto halo_of = [&](int k) {
-            Halo q;
-            if (k == 0)      { q.hcol = lane + 1;            q.h = 0 * kLds + q.hcol; }
-            else if (k == 1) { q.hcol = lane + 1;            q.h = (int)(sy - y0 + 1) * kLds + q.hcol; }
-            else if (k == 2) { q.hcol = 0;                   q.h = (lane + 1) * kLds + q.hcol; }
-            else             { q.hcol = (int)(sx - x0 + 1);  q.h = (lane + 1) * kLds + q.hcol; }
-            q.hy = k == 0 ? y0 - 1 : k == 1 ? sy : y0 + lane;
-            q.hx = k == 0 || k == 1 ? x0 + lane : k == 2 ? x0 - 1 : sx;
-            q.in = q.hy >= 0 && q.hy < a.H && q.hx >= 0 && q.hx < a.W;
-            q.idx = q.in ? q.hy * a.W + q.hx : 0;
-            return q;
-        };
-        auto load_halo_of = [&](const Halo& q) {
-            R v = T.ld(q.idx);
-            if (!q.in) v = load_T<R, COH>(a, T, q.hy, q.hx);
-            return v;
-        };
-        // this wave's side (staging, and the synchronous in-place reload)
-        const Halo hw = halo_of(wave);
-        const int h = hw.h, hcol = hw.hcol;
-        auto load_halo = [&]() { return load_halo_of(hw); };
-        // ---- stage the tile: 16 cells per thread (4 rows x 4 consecutive columns).  Every global
-        // load of the visit (T, cost, halo) is issued before the first LDS store, and each path does
-        // its own stores (no loaded value flows through a join, whose register copies would wait for
-        // the loads): the compiler does not move the sc1 buffer loads across LDS stores, and the
-        // interleaved form cost one memory round trip per row group (5 serial trips per staging).
-        R told[16];
-        const int cx = (tid & 15) * 4;
-        auto store_tile = [&](const R (&cr)[16], R hv) {
+        Ts[h] = make_cell<R>(hv, INF, hcol);
+    };
+    if (full) {
+        R cr[16];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int ry = (tid >> 4) + 16 * k;
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    Ts[(ry + 1) * kLds + cx + e + 1] = make_cell<R>(told[4 * k + e], stage_cost(cr[4 * k + e]), cx + e + 1);
-            }
-            Ts[h] = make_cell<R>(hv, INF, hcol);
-        };
-        if (kFollow && fside >= 0) {
-            // a followed tile (fresh, full, its halo ring inside the raster): T is +inf everywhere
-            // (never visited), so only the costs and three halo sides are loaded; the fourth side
-            // is the previous tile's edge
-            R cr[16];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const R* cp = &cost[(y0 + (tid >> 4) + 16 * k) * a.W + x0 + cx];
-                if constexpr (sizeof(R) == 4) {
-                    const float4 c4 = *reinterpret_cast<const float4*>(cp);
-                    cr[4 * k] = c4.x; cr[4 * k + 1] = c4.y; cr[4 * k + 2] = c4.z; cr[4 * k + 3] = c4.w;
-                } else {
-                    const double2 c0 = *reinterpret_cast<const double2*>(cp);
-                    const double2 c1 = *reinterpret_cast<const double2*>(cp + 2);
-                    cr[4 * k] = c0.x; cr[4 * k + 1] = c0.y; cr[4 * k + 2] = c1.x; cr[4 * k + 3] = c1.y;
-                }
-            }
-            const R hv = wave == fside ? fh : T.ld(hw.idx);
-#pragma unroll
-            for (int e = 0; e < 16; ++e) told[e] = INF;
-            store_tile(cr, hv);
-        } else if (full) {
-            R cr[16];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int64_t gy = y0 + (tid >> 4) + 16 * k;
-                R tv[4];
-                T.ld4(gy * a.W + x0 + cx, tv);
-                if constexpr (sizeof(R) == 4) {
-                    const float4 c4 = *reinterpret_cast<const float4*>(&cost[gy * a.W + x0 + cx]);
-                    cr[4 * k] = c4.x; cr[4 * k + 1] = c4.y; cr[4 * k + 2] = c4.z; cr[4 * k + 3] = c4.w;
-                } else {
-                    const double2 c0 = *reinterpret_cast<const double2*>(&cost[gy * a.W + x0 + cx]);
-                    const double2 c1 = *reinterpret_cast<const double2*>(&cost[gy * a.W + x0 + cx + 2]);
-                    cr[4 * k] = c0.x; cr[4 * k + 1] = c0.y; cr[4 * k + 2] = c1.x; cr[4 * k + 3] = c1.y;
-                }
-#pragma unroll
-                for (int e = 0; e < 4; ++e) told[4 * k + e] = tv[e];
-            }
-            store_tile(cr, load_halo());
-        } else {
-            R cr[16];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int64_t gy = y0 + (tid >> 4) + 16 * k;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int64_t gx = x0 + cx + e;
-                    const bool in = gy < a.H && gx < a.W;
-                    told[4 * k + e] = load_T<R, COH>(a, T, gy, gx);  // ghost cells land in padding
-                    cr[4 * k + e] = in ? cost[gy * a.W + gx] : INF;
-                }
-            }
-            store_tile(cr, load_halo());
-            // a cut tile's halo sits inside the tile: the ring's own row 65 / column 65, where DY < 0
-            // sweeps start and lane 0 of DX < 0 sweeps reads its upstream x, would keep a previous
-            // visit's values -- make them +inf (the moved halo row / column is <= 64, no overlap)
-            if (tid < kLds) {
-                if (sy - y0 < kTile) Ts[(kLds - 1) * kLds + tid] = Cell<R>{INF, INF};
-                if (sx - x0 < kTile) Ts[tid * kLds + (kLds - 1)] = Cell<R>{INF, INF};
-            }
-        }
-        if (lane < 4) cell_c(Ts, (lane >> 1) * (kLds - 1) * kLds + (lane & 1) * (kLds - 1), (lane & 1) * (kLds - 1)) = INF;  // corners
-        __syncthreads();
-        EIK_PROBE(1);
-
-        // PERSISTENT mode revisits a tile that changed IN PLACE, up to a.max_passes times
-        // (EIK_OPT_PASSES; by default 24 for one map, 2 for a batch): its interior is already in LDS
-        // and nobody else writes it while it is busy, so a pass only refreshes the halo ring,
-        // activates the neighbours its last write-back improved, and sweeps again -- no restaging,
-        // no queue round trip.  (List mode: one pass; a changed tile re-lists itself.)
-        // quadrant sweeps of this pass (bit w: wave w), in a register: the caller's L.dirs for the
-        // first pass, then set by the in-place branch below
-        unsigned dirs = L.dirs;
-        // EIK_ACT_SPLIT: this lane's activation issued at the last pass boundary (-1: none)
-        int act_tile = -1;
-        unsigned act_old = 0u;
-        auto act_complete = [&]() {
-            if (act_tile >= 0) qpush_complete(a, act_tile, act_old);
-            act_tile = -1;
-        };
-        unsigned act_f = 0u;  // EIK_SPLIT_WB: the flags wave 2 activates in the next sweep
-        unsigned snap = ~0u;  // EIK_FOLLOW: wave 0 lanes 1..4, a neighbour's state word
-        bool followed = false;
-        // EIK_FOLLOW: retire the previous tile of the chain (one wave; after every wave's stores of
-        // its last write-back have landed): its other neighbours' activations, then its re-queue
-        // (it changed: kSelf) or finish -- the persistent loop's activate_after + qfinish for it
-        auto retire = [&]() {
-            while (__hip_atomic_load(&L.drained, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 4u)
-                __builtin_amdgcn_s_sleep(1);
-            activate_neighbours(a, ret_tile, ret_f, L.key, 0, 0u, lane);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // activations counted before the finish
-            if (lane == 0) {
-                if (ret_f & 128u) atomicOr(&a.qstate[ret_tile], kPending | kSelf);
-                qfinish(a, ret_tile);
-                charge_visits(a, 1ull);
-            }
-        };
-        for (int pass = 0;; ++pass) {
-            // in-sweep duties, by group step: wave 0's split activation (EIK_ACT_SPLIT)
-            auto hook = [&](int st) {
-                if (EIK_ACT_SPLIT && wave == 0 && st == kActStep) act_complete();
-                if constexpr (kSplit) {
-                    if (wave >= 2 && pass > 0 && st == kSplitDrainStep) {  // the last boundary's stores landed
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        if (lane == 0) atomicAdd(&L.sdrained, 1u);
-                    }
-                    if (wave == 2 && st == kSplitActStep && act_f != 0u) {
-                        const unsigned want = 2u * (unsigned)pass;
-                        while (__hip_atomic_load(&L.sdrained, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
-                            __builtin_amdgcn_s_sleep(1);
-                        act_tile = activate_neighbours_issue(a, tile, act_f, act_old, lane);
-                        act_f = 0u;
-                    }
-                    if (wave == 2 && st == kSplitActDoneStep) act_complete();
-                }
-                if constexpr (kFollow) {
-                    // the previous tile of the chain is retired once every wave's stores landed
-                    if (ret_tile >= 0 && st == kRetireDrainStep) {
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        if (lane == 0) atomicAdd(&L.drained, 1u);
-                    }
-                }
-            };
-            // EIK_FOLLOW: snapshot of the full neighbours' state words (wave 0, lanes 1..4: side
-            // lane - 1), read during the sweep and published after it for this pass's boundary
-            if (kFollow && wave == 0) {
-                snap = ~0u;
-                const int q = lane - 1;
-                const int nty_ = q == 0 ? ty - 1 : q == 1 ? ty + 1 : ty;
-                const int ntx_ = q == 2 ? tx - 1 : q == 3 ? tx + 1 : tx;
-                // a candidate is full and its halo ring lies inside the raster (no ghost strip, no
-                // +inf border: its staging is plain loads), i.e. 1 <= ty', tx' and below the last
-                if (q >= 0 && q < 4 && full && nty_ >= 1 && ntx_ >= 1 && (int64_t)(nty_ + 1) * kTile < a.H &&
-                    (int64_t)(ntx_ + 1) * kTile < a.W)
-                    snap = __hip_atomic_load(&a.qstate[map * a.tiles_per_map + nty_ * a.ntx + ntx_], __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-            }
-            // ---- sweep rounds (quadrant directions concurrently, one per wave; `dirs` selects them)
-            const bool sweep = (dirs >> wave) & 1u;
-            bool last_changed = false;
-            if (a.max_rounds == 1) {  // single round: "changed" is read off the write-back below
-                if (sweep) {
-                    if (wave == 0)      sweep_quadrant<R, +1, +1, false>(Ts, lane, keep, hook);
-                    else if (wave == 1) sweep_quadrant<R, -1, +1, false>(Ts, lane, keep, hook);
-                    else if (wave == 2) sweep_quadrant<R, +1, -1, false>(Ts, lane, keep, hook);
-                    else                sweep_quadrant<R, -1, -1, false>(Ts, lane, keep, hook);
-                } else {  // a wave without a sweep this pass still does its duties, in step order
-                    for (int st = 0; st < 2 * kTile; st += kAhead) hook(st);
-                }
-                if (kFollow && wave == 0) {
-                    const unsigned long long m = __ballot(snap == 0u);  // lanes 1..4 only can hold 0
-                    if (lane == 0) L.fresh = (unsigned)(m >> 1) & 0xFu;
-                }
-                if (kFollow && ret_tile >= 0) {  // by the first wave this pass does not sweep
-                    const unsigned idle = ~dirs & 0xFu;
-                    if (wave == (idle ? (int)__builtin_ctz(idle) : 0)) retire();
-                    ret_tile = -1;
-                }
-                __syncthreads();
+        for (int k = 0; k < 4; ++k) {
+            const int64_t gy = y0 + (tid >> 4) + 16 * k;
+            R tv[4];
+            T.ld4(gy * a.W + x0 + cx, tv);
+            if constexpr (sizeof(R) == 4) {
+                const float4 c4 = *reinterpret_cast<const float4*>(&cost[gy * a.W + x0 + cx]);
+                cr[4 * k] = c4.x; cr[4 * k + 1] = c4.y; cr[4 * k + 2] = c4.z; cr[4 * k + 3] = c4.w;
             } else {
-                for (int round = 0;; ++round) {
-                    bool ch = false;
-                    if (sweep) {
-                        if (wave == 0)      ch = sweep_quadrant<R, +1, +1, true>(Ts, lane, keep);
-                        else if (wave == 1) ch = sweep_quadrant<R, -1, +1, true>(Ts, lane, keep);
-                        else if (wave == 2) ch = sweep_quadrant<R, +1, -1, true>(Ts, lane, keep);
-                        else                ch = sweep_quadrant<R, -1, -1, true>(Ts, lane, keep);
-                    }
-                    if (__any(ch) && lane == 0) atomicOr(&L.round, 1u << (round & 31));
-                    __syncthreads();
-                    last_changed = (L.round >> (round & 31)) & 1u;
-                    if (!last_changed || round + 1 >= a.max_rounds) break;
-                }
+                const double2 c0 = *reinterpret_cast<const double2*>(&cost[gy * a.W + x0 + cx]);
+                const double2 c1 = *reinterpret_cast<const double2*>(&cost[gy * a.W + x0 + cx + 2]);
+                cr[4 * k] = c0.x; cr[4 * k + 1] = c0.y; cr[4 * k + 2] = c1.x; cr[4 * k + 3] = c1.y;
             }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) told[4 * k + e] = tv[e];
+        }
+        store_tile(cr, load_halo());
+    } else {
+        R cr[16];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t gy = y0 + (tid >> 4) + 16 * k;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int64_t gx = x0 + cx + e;
+                const bool in = gy < a.H && gx < a.W;
+                told[4 * k + e] = load_T<R, COH>(a, T, gy, gx);  // ghost cells land in padding
+                cr[4 * k + e] = in ? cost[gy * a.W + gx] : INF;
+            }
+        }
+        store_tile(cr, load_halo());
+        // a cut tile's halo sits inside the tile: the ring's own row 65 / column 65, where DY < 0
+        // sweeps start and lane 0 of DX < 0 sweeps reads its upstream x, would keep a previous
+        // visit's values -- make them +inf (the moved halo row / column is <= 64, no overlap)
+        if (tid < kLds) {
+            if (sy - y0 < kTile) Ts[(kLds - 1) * kLds + tid] = Cell<R>{INF, INF};
+            if (sx - x0 < kTile) Ts[tid * kLds + (kLds - 1)] = Cell<R>{INF, INF};
+        }
+    }
+    if (lane < 4) cell_c(Ts, (lane >> 1) * (kLds - 1) * kLds + (lane & 1) * (kLds - 1), (lane & 1) * (kLds - 1)) = INF;  // corners
+    __syncthreads();
+    EIK_PROBE(1);
 
-            // ---- EIK_FOLLOW: continue with a fresh neighbour this pass made reachable
-            bool wb_done = false;
-            if constexpr (kFollow) {
-                const unsigned fr = __builtin_amdgcn_readfirstlane(L.fresh);  // uniform (published before the sweep-end barrier)
-                if (a.max_rounds == 1 && fr && nfollow < EIK_FOLLOW_MAX) {
-                    // this tile's edge toward each fresh side: its smallest value (+inf: not reached)
-                    auto edge_cell = [&](int side, int l) {
-                        return side == 0 ? kLds + l + 1 : side == 1 ? kTile * kLds + l + 1
-                             : side == 2 ? (l + 1) * kLds + 1 : (l + 1) * kLds + kTile;
-                    };
-                    if ((fr >> wave) & 1u) {
-                        const int c = edge_cell(wave, lane);
-                        R m = cell_t(Ts, c, c % kLds);
-#pragma unroll
-                        for (int o = 32; o >= 1; o >>= 1) m = fmin_nn(m, __shfl_xor(m, o));
-                        if (lane == 0) L.emin[wave] = m;
-                    }
-                    __syncthreads();
-                    int sb = -1;
-                    R eb = INF;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        if (((fr >> q) & 1u) && L.emin[q] < eb) {
-                            eb = L.emin[q];
-                            sb = q;
-                        }
-                    sb = __builtin_amdgcn_readfirstlane(sb);
-                    if (sb >= 0) {  // uniform
-                        const int nty_ = sb == 0 ? ty - 1 : sb == 1 ? ty + 1 : ty;
-                        const int ntx_ = sb == 2 ? tx - 1 : sb == 3 ? tx + 1 : tx;
-                        const int nb = map * a.tiles_per_map + nty_ * a.ntx + ntx_;
-                        const int fs = sb ^ 1;  // nb's side facing this tile
-                        // 1) the claim (returns BUSY | VISITED on success: nobody else grabs it)
-                        unsigned cas_old = 1u;
-                        if (tid == 0) cas_old = atomicCAS(&a.qstate[nb], 0u, kBusy | kVisited);
-                        // 2) this tile's write-back in full: a fixed number of stores after the claim,
-                        //    so the wait for its result does not wait for the stores' drain
-                        unsigned fl = 0;
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) {
-                            const int ry = (tid >> 4) + 16 * k;
-                            R nv[4];
-#pragma unroll
-                            for (int e = 0; e < 4; ++e) {
-                                nv[e] = cell_t(Ts, (ry + 1) * kLds + cx + e + 1, cx + e + 1);
-                                if (nv[e] < told[4 * k + e] * keep) {
-                                    fl |= 128u;
-                                    const int lx = cx + e + 1, ly = ry + 1;
-                                    if (ry == 0 && nv[e] < cell_t(Ts, lx, lx)) fl |= 1u;
-                                    if (ry == kTile - 1 && nv[e] < cell_t(Ts, (kLds - 1) * kLds + lx, lx)) fl |= 2u;
-                                    if (cx + e == 0 && nv[e] < cell_t(Ts, ly * kLds, 0)) fl |= 4u;
-                                    if (cx + e == kTile - 1 && nv[e] < cell_t(Ts, ly * kLds + kLds - 1, kLds - 1)) fl |= 8u;
-                                }
-                                told[4 * k + e] = nv[e];
-                            }
-                            T.st4((y0 + ry) * a.W + x0 + cx, nv);
-                        }
-                        // 3) the followed tile's side facing this one: this tile's edge
-                        if (wave == fs) {
-                            const int c = edge_cell(sb, lane);
-                            fh = cell_t(Ts, c, c % kLds);
-                        }
-                        if (fl) atomicOr(&L.flags, fl);
-                        if (tid == 0) L.follow = cas_old == 0u ? nb : -1;
-                        __syncthreads();
-                        const int fol = __builtin_amdgcn_readfirstlane(L.follow);
-                        if (fol >= 0) {  // uniform
-                            if (tid == 0) atomicAdd(a.qactive, 1);  // the claimed tile counts as busy
-                            // retired in its first pass: this tile's other activations (the
-                            // followed side needs none), its deferred ones, and "changed" (128)
-                            ret_f = __builtin_amdgcn_readfirstlane(((L.flags | L.flags_acc) & ~(1u << sb)) & 0xEFu);
-                            ret_tile = tile;
-                            tile = fol;
-                            fside = fs;
-                            followed = true;
-                            ++nfollow;
-                            __syncthreads();  // L.flags read everywhere before the next tile's init
-                            break;
-                        }
-                        wb_done = true;  // lost the claim: this boundary goes on as usual
-                    }
-                }
+    // PERSISTENT mode revisits a tile that changed IN PLACE, up to a.max_passes times
+    // (EIK_OPT_PASSES; by default 24 for one map, 2 for a batch): its interior is already in LDS
+    // and nobody else writes it while it is busy, so a pass only refreshes the halo ring,
+    // activates the neighbours its last write-back improved, and sweeps again -- no restaging,
+    // no queue round trip.  (List mode: one pass; a changed tile re-lists itself.)
+    // quadrant sweeps of this pass (bit w: wave w), in a register: the caller's L.dirs for the
+    // first pass, then set by the in-place branch below
+    unsigned dirs = L.dirs;
+    // EIK_ACT_SPLIT: this lane's activation issued at the last pass boundary (-1: none)
+    int act_tile = -1;
+    unsigned act_old = 0u;
+    auto act_complete = [&]() {
+        if (act_tile >= 0) qpush_complete(a, act_tile, act_old);
+        act_tile = -1;
+    };
+    for (int pass = 0;; ++pass) {
+        // in-sweep duties, by group step: wave 0's split activation (EIK_ACT_SPLIT)
+        auto hook = [&](int st) {
+            if (EIK_ACT_SPLIT && wave == 0 && st == kActStep) act_complete();
+        };
+        // ---- sweep rounds (quadrant directions concurrently, one per wave; `dirs` selects them)
+        const bool sweep = (dirs >> wave) & 1u;
+        bool last_changed = false;
+        if (a.max_rounds == 1) {  // single round: "changed" is read off the write-back below
+            if (sweep) {
+                if (wave == 0)      sweep_quadrant<R, +1, +1, false>(Ts, lane, keep, hook);
+                else if (wave == 1) sweep_quadrant<R, -1, +1, false>(Ts, lane, keep, hook);
+                else if (wave == 2) sweep_quadrant<R, +1, -1, false>(Ts, lane, keep, hook);
+                else                sweep_quadrant<R, -1, -1, false>(Ts, lane, keep, hook);
+            } else {  // a wave without a sweep this pass still does its duties, in step order
+                for (int st = 0; st < 2 * kTile; st += kAhead) hook(st);
             }
-
-            // ---- EIK_SPLIT_WB: the split-role boundary (see kSplitDrainStep)
-            if constexpr (kSplit) {
-                if (a.max_rounds == 1 && !wb_done) {
-                    const bool storer = wave >= 2;
-                    unsigned fl = 0, chg = 0;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const int ry = (tid >> 4) + 16 * k;
-                        const int64_t gy = y0 + ry;
-                        R nv[4];
-                        bool any = false;
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            nv[e] = cell_t(Ts, (ry + 1) * kLds + cx + e + 1, cx + e + 1);
-                            any |= nv[e] < told[4 * k + e];
-                            if (nv[e] < told[4 * k + e] * keep && (full || (gy < a.H && x0 + cx + e < a.W))) {
-                                fl |= 128u;
-                                const int lx = cx + e + 1, ly = ry + 1;
-                                if (ry == 0 && nv[e] < cell_t(Ts, lx, lx)) fl |= 1u;
-                                if (ry == kTile - 1 && nv[e] < cell_t(Ts, (kLds - 1) * kLds + lx, lx)) fl |= 2u;
-                                if (cx + e == 0 && nv[e] < cell_t(Ts, ly * kLds, 0)) fl |= 4u;
-                                if (cx + e == kTile - 1 && nv[e] < cell_t(Ts, ly * kLds + kLds - 1, kLds - 1)) fl |= 8u;
-                                const int64_t gx = x0 + cx + e;
-                                if (gy == a.H - 1 && ry != kTile - 1) fl |= 32u;
-                                if (gx == a.W - 1 && cx + e != kTile - 1) fl |= 64u;
-                            }
-                        }
-                        if (any) {
-                            if (!storer) {
-                                chg |= 1u << k;
-                            } else if (full) {
-                                T.st4(gy * a.W + x0 + cx, nv);
-                            } else {
-#pragma unroll
-                                for (int e = 0; e < 4; ++e) {
-                                    const int64_t gx = x0 + cx + e;
-                                    if (gy < a.H && gx < a.W && nv[e] < told[4 * k + e]) T.st(gy * a.W + gx, nv[e]);
-                                }
-                            }
-                        }
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) told[4 * k + e] = nv[e];  // what memory holds once they land
-                    }
-                    if (!storer) L.chg[tid] = (unsigned char)chg;
-                    if (fl) atomicOr(&L.flags, fl);
-                    // consume the activations that reached this busy tile (awaited: the halo loads
-                    // below are issued after it has been performed)
-                    if ((a.sched & 1) && tid == 0) L.pend = atomicAnd(&a.qstate[tile], kBusy | kVisited);
-                    __syncthreads();
-                    const unsigned f = L.flags;  // uniform
-                    const unsigned pend_all = L.pend;
-                    const unsigned pend = pend_all & (kPending | kFromN | kFromS | kFromW | kFromE);
-                    const bool self = (f & 128u) != 0u;
-                    if (storer) {  // waves 0-1's changed row chunks (an unchanged cell's LDS value is what memory holds)
-                        const int c = tid - 128;
-                        const unsigned cm = L.chg[c];
-                        const int ccx = (c & 15) * 4;
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) {
-                            if ((cm >> k) & 1u) {
-                                const int ry = (c >> 4) + 16 * k;
-                                const int64_t gy = y0 + ry;
-                                R nv[4];
-#pragma unroll
-                                for (int e = 0; e < 4; ++e) nv[e] = cell_t(Ts, (ry + 1) * kLds + ccx + e + 1, ccx + e + 1);
-                                if (full) {
-                                    T.st4(gy * a.W + x0 + ccx, nv);
-                                } else {
-#pragma unroll
-                                    for (int e = 0; e < 4; ++e) {
-                                        const int64_t gx = x0 + ccx + e;
-                                        if (gy < a.H && gx < a.W) T.st(gy * a.W + gx, nv[e]);
-                                    }
-                                }
-                            }
-                        }
-                    }
-                    if ((!self && !pend) || pass + 1 >= a.max_passes) {
-                        // the visit ends: its stores land before the activations and the finish
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        if (tid == 0) L.last = -1;
-                        __syncthreads();
-                        break;
-                    }
-                    if (!storer) {  // the halo ring: wave 0 north and west, wave 1 south and east
-                        const Halo q0 = halo_of(wave), q1 = halo_of(wave + 2);
-                        const R v0 = load_halo_of(q0), v1 = load_halo_of(q1);
-                        if (tid == 64) charge_inplace_pass(a);  // in-place passes: stats and the visit budget
-                        cell_t(Ts, q0.h, q0.hcol) = v0;
-                        cell_t(Ts, q1.h, q1.hcol) = v1;
-                    }
-                    const bool defer = (a.sched & 2) && pass > 0;
-                    act_f = defer ? 0u : f;  // wave 2 activates them in the next sweep, once drained
-                    if (defer && tid == 0) L.flags_acc |= f & 0x6fu;
-                    dirs = self ? 0xFu : sweep_dirs(pend);
-                    __syncthreads();  // the halo ring is in; every wave has read L.flags / L.pend
-                    if (tid == 0) {
-                        L.flags = 0;
-                        L.pend = 0;
-                    }
-                    continue;
-                }
-            }
-
-            EIK_PROBE(2);
-            // PERSISTENT mode, a.sched bit 0: consume the activations that reached this busy tile
-            // during the pass (neighbours' edges drained before their atomicOr, and this clear comes
-            // before the halo reload) -- an in-place pass then serves them instead of a re-queued
-            // visit.  Issued now, awaited with the write-back's drain.
-            unsigned pend_old = 0;
-            if (COH && (a.sched & 1) && tid == 0) pend_old = atomicAnd(&a.qstate[tile], kBusy | kVisited);
-            // ---- write back changed cells, collect side flags (and entering values, ordered mode).
-            // EIK_EDGE_FIRST (persistent mode, full tiles): only the tile's edge cells -- the values a
-            // neighbour's halo reads -- are stored and drained before the activations; the interior
-            // row chunks (bit k of defer_rows: this thread's row chunk k) are stored after the pass's
-            // halo has come in and drain during the next sweep, or before the visit's finish (the
-            // persistent loop drains every wave before qfinish).  Nobody else reads a busy tile's
-            // interior: its next visit starts after that finish.
-            unsigned fl = 0;
-            unsigned defer_rows = 0;
-            R kmin_self = INF, kmin[4] = {INF, INF, INF, INF};
-#pragma unroll
-            for (int k = 0; k < (wb_done ? 0 : 4); ++k) {
-                const int ry = (tid >> 4) + 16 * k;
-                const int64_t gy = y0 + ry;
-                R nv[4];
-                bool any = false;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    nv[e] = cell_t(Ts, (ry + 1) * kLds + cx + e + 1, cx + e + 1);
-                    any |= nv[e] < told[4 * k + e];
-                    // (a ghost cell inside a cut tile is lowered by the halo reload, never by a sweep)
-                    if (nv[e] < told[4 * k + e] * keep && (full || (gy < a.H && x0 + cx + e < a.W))) {
-                        fl |= 128u;  // changed in this visit
-                        kmin_self = umin(kmin_self, nv[e]);
-                        // A neighbour can only improve if this edge value undercuts the neighbour's
-                        // adjacent cell (the halo value, stale => larger => conservative).
-                        const int lx = cx + e + 1, ly = ry + 1;
-                        if (ry == 0 && nv[e] < cell_t(Ts, lx, lx)) { fl |= 1u; kmin[0] = umin(kmin[0], nv[e]); }
-                        if (ry == kTile - 1 && nv[e] < cell_t(Ts, (kLds - 1) * kLds + lx, lx)) { fl |= 2u; kmin[1] = umin(kmin[1], nv[e]); }
-                        if (cx + e == 0 && nv[e] < cell_t(Ts, ly * kLds, 0)) { fl |= 4u; kmin[2] = umin(kmin[2], nv[e]); }
-                        if (cx + e == kTile - 1 && nv[e] < cell_t(Ts, ly * kLds + kLds - 1, kLds - 1)) { fl |= 8u; kmin[3] = umin(kmin[3], nv[e]); }
-                        const int64_t gx = x0 + cx + e;  // subdomain edges inside a partial tile (DD)
-                        if (gy == a.H - 1 && ry != kTile - 1) fl |= 32u;
-                        if (gx == a.W - 1 && cx + e != kTile - 1) fl |= 64u;
-                    }
-                }
-                if (any) {
-                    if (COH && EIK_EDGE_FIRST && full && ry != 0 && ry != kTile - 1) {
-                        if (cx == 0 && nv[0] < told[4 * k]) T.st(gy * a.W + x0, nv[0]);
-                        if (cx == kTile - 4 && nv[3] < told[4 * k + 3]) T.st(gy * a.W + x0 + kTile - 1, nv[3]);
-                        defer_rows |= 1u << k;
-                    } else if (full) {
-                        T.st4(gy * a.W + x0 + cx, nv);
-                    } else {
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            const int64_t gx = x0 + cx + e;
-                            if (gy < a.H && gx < a.W && nv[e] < told[4 * k + e]) T.st(gy * a.W + gx, nv[e]);
-                        }
-                    }
-                }
-                if (COH) {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) told[4 * k + e] = nv[e];  // what memory holds now
-                }
-            }
-            if (fl) atomicOr(&L.flags, fl);
-            if (a.delta < INF) {
-                if (kmin_self < INF) atomicMin(&L.key[0], __float_as_uint((float)kmin_self));
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    if (kmin[q] < INF) atomicMin(&L.key[q + 1], __float_as_uint((float)kmin[q]));
-            }
-            if (tid == 0) L.last = a.max_rounds == 1 ? -1 : (int)last_changed;  // -1: see flags bit 7
-            if (COH && (a.sched & 1) && tid == 0) L.pend = pend_old;
-            if constexpr (COH) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
             __syncthreads();
-            EIK_PROBE(7);
-            // the deferred interior row chunks (told holds what they store)
-            auto store_deferred = [&]() {
-                asm volatile("" ::: "memory");  // not above the halo / activation round trips
+        } else {
+            for (int round = 0;; ++round) {
+                bool ch = false;
+                if (sweep) {
+                    if (wave == 0)      ch = sweep_quadrant<R, +1, +1, true>(Ts, lane, keep);
+                    else if (wave == 1) ch = sweep_quadrant<R, -1, +1, true>(Ts, lane, keep);
+                    else if (wave == 2) ch = sweep_quadrant<R, +1, -1, true>(Ts, lane, keep);
+                    else                ch = sweep_quadrant<R, -1, -1, true>(Ts, lane, keep);
+                }
+                if (__any(ch) && lane == 0) atomicOr(&L.round, 1u << (round & 31));
+                __syncthreads();
+                last_changed = (L.round >> (round & 31)) & 1u;
+                if (!last_changed || round + 1 >= a.max_rounds) break;
+            }
+        }
+
+        EIK_PROBE(2);
+        // PERSISTENT mode, a.sched bit 0: consume the activations that reached this busy tile
+        // during the pass (neighbours' edges drained before their atomicOr, and this clear comes
+        // before the halo reload) -- an in-place pass then serves them instead of a re-queued
+        // visit.  Issued now, awaited with the write-back's drain.
+        unsigned pend_old = 0;
+        if (COH && (a.sched & 1) && tid == 0) pend_old = atomicAnd(&a.qstate[tile], kBusy | kVisited);
+        // ---- write back changed cells, collect side flags (and entering values, ordered mode).
+        // EIK_EDGE_FIRST (persistent mode, full tiles): only the tile's edge cells -- the values a
+        // neighbour's halo reads -- are stored and drained before the activations; the interior
+        // row chunks (bit k of defer_rows: this thread's row chunk k) are stored after the pass's
+        // halo has come in and drain during the next sweep, or before the visit's finish (the
+        // persistent loop drains every wave before qfinish).  Nobody else reads a busy tile's
+        // interior: its next visit starts after that finish.
+        unsigned fl = 0;
+        unsigned defer_rows = 0;
+        R kmin_self = INF, kmin[4] = {INF, INF, INF, INF};
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    if (defer_rows & (1u << k)) {
-                        const R v[4] = {told[4 * k], told[4 * k + 1], told[4 * k + 2], told[4 * k + 3]};
-                        T.st4((y0 + (tid >> 4) + 16 * k) * a.W + x0 + cx, v);
+        for (int k = 0; k < 4; ++k) {
+            const int ry = (tid >> 4) + 16 * k;
+            const int64_t gy = y0 + ry;
+            R nv[4];
+            bool any = false;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                nv[e] = cell_t(Ts, (ry + 1) * kLds + cx + e + 1, cx + e + 1);
+                any |= nv[e] < told[4 * k + e];
+                // (a ghost cell inside a cut tile is lowered by the halo reload, never by a sweep)
+                if (nv[e] < told[4 * k + e] * keep && (full || (gy < a.H && x0 + cx + e < a.W))) {
+                    fl |= 128u;  // changed in this visit
+                    kmin_self = umin(kmin_self, nv[e]);
+                    // A neighbour can only improve if this edge value undercuts the neighbour's
+                    // adjacent cell (the halo value, stale => larger => conservative).
+                    const int lx = cx + e + 1, ly = ry + 1;
+                    if (ry == 0 && nv[e] < cell_t(Ts, lx, lx)) { fl |= 1u; kmin[0] = umin(kmin[0], nv[e]); }
+                    if (ry == kTile - 1 && nv[e] < cell_t(Ts, (kLds - 1) * kLds + lx, lx)) { fl |= 2u; kmin[1] = umin(kmin[1], nv[e]); }
+                    if (cx + e == 0 && nv[e] < cell_t(Ts, ly * kLds, 0)) { fl |= 4u; kmin[2] = umin(kmin[2], nv[e]); }
+                    if (cx + e == kTile - 1 && nv[e] < cell_t(Ts, ly * kLds + kLds - 1, kLds - 1)) { fl |= 8u; kmin[3] = umin(kmin[3], nv[e]); }
+                    const int64_t gx = x0 + cx + e;  // subdomain edges inside a partial tile (DD)
+                    if (gy == a.H - 1 && ry != kTile - 1) fl |= 32u;
+                    if (gx == a.W - 1 && cx + e != kTile - 1) fl |= 64u;
+                }
+            }
+            if (any) {
+                if (COH && EIK_EDGE_FIRST && full && ry != 0 && ry != kTile - 1) {
+                    if (cx == 0 && nv[0] < told[4 * k]) T.st(gy * a.W + x0, nv[0]);
+                    if (cx == kTile - 4 && nv[3] < told[4 * k + 3]) T.st(gy * a.W + x0 + kTile - 1, nv[3]);
+                    defer_rows |= 1u << k;
+                } else if (full) {
+                    T.st4(gy * a.W + x0 + cx, nv);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int64_t gx = x0 + cx + e;
+                        if (gy < a.H && gx < a.W && nv[e] < told[4 * k + e]) T.st(gy * a.W + gx, nv[e]);
                     }
                 }
-            };
+            }
             if (COH) {
-                const unsigned f = L.flags;  // uniform
-                const unsigned pend = L.pend & (kPending | kFromN | kFromS | kFromW | kFromE);
-                const bool self = (f & 128u) != 0u;
-                if ((!self && !pend) || pass + 1 >= a.max_passes || a.max_rounds != 1) {
-                    store_deferred();  // drained by the persistent loop before the finish
-                    break;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) told[4 * k + e] = nv[e];  // what memory holds now
+            }
+        }
+        if (fl) atomicOr(&L.flags, fl);
+        if (a.delta < INF) {
+            if (kmin_self < INF) atomicMin(&L.key[0], __float_as_uint((float)kmin_self));
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (kmin[q] < INF) atomicMin(&L.key[q + 1], __float_as_uint((float)kmin[q]));
+        }
+        if (tid == 0) L.last = a.max_rounds == 1 ? -1 : (int)last_changed;  // -1: see flags bit 7
+        if (COH && (a.sched & 1) && tid == 0) L.pend = pend_old;
+        if constexpr (COH) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+        __syncthreads();
+        EIK_PROBE(7);
+        // the deferred interior row chunks (told holds what they store)
+        auto store_deferred = [&]() {
+            asm volatile("" ::: "memory");  // not above the halo / activation round trips
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (defer_rows & (1u << k)) {
+                    const R v[4] = {told[4 * k], told[4 * k + 1], told[4 * k + 2], told[4 * k + 3]};
+                    T.st4((y0 + (tid >> 4) + 16 * k) * a.W + x0 + cx, v);
                 }
-                // the halo reload is issued first and the budget charge goes to wave 1, so wave 0's
-                // activation atomics are the only round trips the next pass waits for
-                const R hv = load_halo();
-                if (tid == 64) charge_inplace_pass(a);  // in-place passes: stats and the visit budget
-                // a.sched bit 1: after the first pass, neighbour activations wait for the visit's end
-                // (one activation with the converged edges instead of one per pass)
-                const bool defer = (a.sched & 2) && pass > 0;
-                if constexpr (EIK_ACT_SPLIT)
-                    act_tile = activate_neighbours_issue(a, tile, defer ? 0u : f, act_old);  // completed in the next sweep
-                else
-                    activate_neighbours(a, tile, defer ? 0u : f, L.key, 0, 0u);  // lanes 0..4 (T already drained)
-                if (defer && tid == 0) L.flags_acc |= f & 0x6fu;
-                dirs = self ? 0xFu : sweep_dirs(pend);  // a self revisit: every direction
-                cell_t(Ts, h, hcol) = hv;
-                store_deferred();  // after the halo value is in: they drain during the next sweep
-                __syncthreads();  // every wave has read L.flags and its halo side is in
-                if (tid == 0) {
-                    L.flags = 0;  // next OR-ed after the next sweep barrier
-                    L.pend = 0;   // consumed by this pass
-                }
-            } else {
+            }
+        };
+        if (COH) {
+            const unsigned f = L.flags;  // uniform
+            const unsigned pend = L.pend & (kPending | kFromN | kFromS | kFromW | kFromE);
+            const bool self = (f & 128u) != 0u;
+            if ((!self && !pend) || pass + 1 >= a.max_passes || a.max_rounds != 1) {
+                store_deferred();  // drained by the persistent loop before the finish
                 break;
             }
+            // the halo reload is issued first and the budget charge goes to wave 1, so wave 0's
+            // activation atomics are the only round trips the next pass waits for
+            const R hv = load_halo();
+            if (tid == 64) charge_inplace_pass(a);  // in-place passes: stats and the visit budget
+            // a.sched bit 1: after the first pass, neighbour activations wait for the visit's end
+            // (one activation with the converged edges instead of one per pass)
+            const bool defer = (a.sched & 2) && pass > 0;
+            if constexpr (EIK_ACT_SPLIT)
+                act_tile = activate_neighbours_issue(a, tile, defer ? 0u : f, act_old);  // completed in the next sweep
+            else
+                activate_neighbours(a, tile, defer ? 0u : f, L.key, 0, 0u);  // lanes 0..4 (T already drained)
+            if (defer && tid == 0) L.flags_acc |= f & 0x6fu;
+            dirs = self ? 0xFu : sweep_dirs(pend);  // a self revisit: every direction
+            cell_t(Ts, h, hcol) = hv;
+            store_deferred();  // after the halo value is in: they drain during the next sweep
+            __syncthreads();  // every wave has read L.flags and its halo side is in
+            if (tid == 0) {
+                L.flags = 0;  // next OR-ed after the next sweep barrier
+                L.pend = 0;   // consumed by this pass
+            }
+        } else {
+            break;
         }
-        act_complete();  // (never pending here: every issue is followed by a pass)
-        if (kFollow && followed) continue;  // the claimed tile: stage it and sweep on
-        EIK_PROBE(3);
-        return tile;
     }
+    act_complete();  // (never pending here: every issue is followed by a pass)
+    EIK_PROBE(3);
 }
 
 // Activations after a tile visit: the neighbours (with any deferred in-place ones), and the
@@ -1092,8 +753,7 @@ __global__ __launch_bounds__(kThreads, WPS) void fim2d_persist_kernel(Fim2dArgs 
         EIK_PROBE(6);
         tile = __builtin_amdgcn_readfirstlane(L.tile);
         if (tile < 0) break;  // uniform: solve finished (or failed)
-        tile = process_tile<R, true>(a, tile, L, keep);  // sc1 loads; sc1 stores drained + barrier
-                                                          // (EIK_FOLLOW: the chain's last tile)
+        process_tile<R, true>(a, tile, L, keep);  // sc1 loads; sc1 stores drained + barrier
     }
     if (threadIdx.x == 0 && nvis) atomicAdd(a.visits, (unsigned long long)nvis);
 }

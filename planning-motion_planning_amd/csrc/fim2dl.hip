@@ -59,8 +59,6 @@ struct TileLdsL {
     unsigned key[5];
     int tile;
     unsigned dirs;
-    unsigned sdrained;          // EIK_SPLIT_WB_L: storing waves' drains (2 per boundary, cumulative)
-    unsigned short chg[128];    // EIK_SPLIT_WB_L: waves 0-1's changed cells (bit j: cell t + 256 j)
 };
 // A sweep's 4-step group spans rows [-(kAhead - 1), TH + 1 + kAhead - 1]: every row it reads (T
 // and cost alike) is inside the guard rows of both arrays, and a guard row's +inf cost keeps its T
@@ -170,8 +168,8 @@ __device__ __forceinline__ double min_nn(double a, double b) { return fmin_nn(a,
 // concurrent sweeps cover every x/y neighbour pair and the n-D update is monotone, so the fixed
 // point is the one of reading both neighbours per axis -- 3 cell reads per step instead of 5).
 // TH tile rows: TH + 64 skewed steps.
-template <typename R, int TH, int NL, int DX, int DY, class Hook>
-__device__ __forceinline__ void sweep_layered(LCell<R>* __restrict__ Ts, int lane, Hook&& hook) {
+template <typename R, int TH, int NL, int DX, int DY>
+__device__ __forceinline__ void sweep_layered(LCell<R>* __restrict__ Ts, int lane) {
     constexpr R INF = Real<R>::inf();
     constexpr int S = (int)sizeof(LCell<R>);
     constexpr int kRow = kLds * S;
@@ -207,7 +205,6 @@ __device__ __forceinline__ void sweep_layered(LCell<R>* __restrict__ Ts, int lan
 #pragma unroll
     for (int u = 0; u < D; ++u) fetch(u);
     for (int s = 0; s < TH + kTile; s += D) {
-        hook(s);  // per group: the persistent driver's in-sweep duties (EIK_SPLIT_WB_L)
         const int gcur = gb;
         gb = clampb(raw);
         raw += DY * D * kRow;
@@ -235,14 +232,10 @@ __device__ __forceinline__ void sweep_layered(LCell<R>* __restrict__ Ts, int lan
     }
 }
 
-// EIK_SPLIT_WB_L: fim2d.hip's split-role pass boundary (EIK_SPLIT_WB) for the layered solver --
-// waves 2-3 store the write-back without waiting for it, waves 0-1 reload the halo ring, the next
-// pass starts after that round trip alone, and wave 2 activates the neighbours from the next sweep
-// once the stores have landed.  One workgroup per CU here: the drain it removes idled the whole CU.
-#ifndef EIK_SPLIT_WB_L
-#define EIK_SPLIT_WB_L 1
-#endif
-constexpr int kLSplitDrainStep = 16, kLSplitActStep = 20, kLSplitActDoneStep = 40;
+// (EIK_SPLIT_WB_L, round 4: fim2d.hip's split-role boundary -- two waves storing the write-back
+// without waiting, two reloading the halo, activations after the drain from the next sweep --
+// measured and removed: C5 fp64 1.96-2.01 -> 1.81-1.87, fp32 4.73-4.83 -> 4.19-4.35 Gcells/s,
+// profiles/r04e_layered_split_ab.log.)
 
 // EIK_ACT_SPLIT_L: the split activations of fim2d.hip's in-place passes (EIK_ACT_SPLIT) for the
 // layered solver.  Off: no gain on C5 (fp64 2.01-2.07 -> 2.00-2.03, fp32 4.80-4.85 -> 4.69-4.82
@@ -274,10 +267,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
     const TMem<R, COH> T(static_cast<R*>(a.T) + map * plane, plane);
     const int64_t y0 = (int64_t)ty * TH, x0 = (int64_t)tx * kTile;
 
-    if (tid == 0) {
-        L.flags = 0;
-        L.sdrained = 0u;
-    }
+    if (tid == 0) L.flags = 0;
     if (tid < 5) L.key[tid] = 0x7f800000u;
     // halo ring: wave 0 north row, 1 south row, 2 west column, 3 east column (out of range: +inf;
     // lanes >= TH of the column waves have none)
@@ -296,25 +286,6 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
         for (int z = 0; z < NL; ++z) v[z] = T.ld(hgi + z);
 #pragma unroll
         for (int z = 0; z < NL; ++z) v[z] = hin ? v[z] : INF;
-        return LCell<R>::make(v);
-    };
-    // halo side k for this lane (EIK_SPLIT_WB_L: waves 0-1 reload all four): its LDS cell, whether
-    // it exists (column sides: lanes < TH), and the value (+inf outside the raster)
-    auto halo_k = [&](int k, int& hk) -> LCell<R> {
-        int64_t yy, xx;
-        if (k == 0)      { hk = 0 * kLds + lane + 1;          yy = y0 - 1;      xx = x0 + lane; }
-        else if (k == 1) { hk = (TH + 1) * kLds + lane + 1;   yy = y0 + TH;     xx = x0 + lane; }
-        else if (k == 2) { hk = (lane + 1) * kLds + 0;        yy = y0 + lane;   xx = x0 - 1; }
-        else             { hk = (lane + 1) * kLds + kLds - 1; yy = y0 + lane;   xx = x0 + kTile; }
-        const bool cellk = k < 2 || lane < TH;
-        const bool ink = cellk && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
-        const int64_t gik = ink ? (yy * a.W + xx) * ls + a.z0 : 0;
-        R v[4] = {INF, INF, INF, INF};
-#pragma unroll
-        for (int z = 0; z < NL; ++z) v[z] = T.ld(gik + z);
-#pragma unroll
-        for (int z = 0; z < NL; ++z) v[z] = ink ? v[z] : INF;
-        if (!cellk) hk = -1;
         return LCell<R>::make(v);
     };
     // ---- stage: every global load of the visit (T, cost, halo) is issued before the first LDS
@@ -381,105 +352,18 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
     unsigned dirs = L.dirs;  // this pass's sweeps (register: see fim2d.hip process_tile)
     int act_tile = -1;       // EIK_ACT_SPLIT_L: this lane's activation issued at the last pass boundary
     unsigned act_old = 0u;
-    unsigned act_f = 0u;     // EIK_SPLIT_WB_L: the flags wave 2 activates in the next sweep
     for (int pass = 0;; ++pass) {
         if (EIK_ACT_SPLIT_L && act_tile >= 0) {  // wave 0 lanes 1..4, as its sweep starts (fim2d.hip)
             qpush_complete(a, act_tile, act_old);
             act_tile = -1;
         }
-        constexpr bool kSplitL = COH && EIK_SPLIT_WB_L;
-        auto hook = [&](int st) {
-            if constexpr (kSplitL) {
-                if (wave >= 2 && pass > 0 && st == kLSplitDrainStep) {  // the last boundary's stores landed
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    if (lane == 0) atomicAdd(&L.sdrained, 1u);
-                }
-                if (wave == 2 && st == kLSplitActStep && act_f != 0u) {
-                    const unsigned want = 2u * (unsigned)pass;
-                    while (__hip_atomic_load(&L.sdrained, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
-                        __builtin_amdgcn_s_sleep(1);
-                    act_tile = activate_neighbours_issue(a, tile, act_f, act_old, lane);
-                    act_f = 0u;
-                }
-                if (wave == 2 && st == kLSplitActDoneStep && act_tile >= 0) {
-                    qpush_complete(a, act_tile, act_old);
-                    act_tile = -1;
-                }
-            }
-        };
         if ((dirs >> wave) & 1u) {
-            if (wave == 0)      sweep_layered<R, TH, NL, +1, +1>(Ts, lane, hook);
-            else if (wave == 1) sweep_layered<R, TH, NL, -1, +1>(Ts, lane, hook);
-            else if (wave == 2) sweep_layered<R, TH, NL, +1, -1>(Ts, lane, hook);
-            else                sweep_layered<R, TH, NL, -1, -1>(Ts, lane, hook);
-        } else {  // duties of a wave without a sweep this pass, in step order
-            for (int st = 0; st < TH + kTile; st += kAhead) hook(st);
+            if (wave == 0)      sweep_layered<R, TH, NL, +1, +1>(Ts, lane);
+            else if (wave == 1) sweep_layered<R, TH, NL, -1, +1>(Ts, lane);
+            else if (wave == 2) sweep_layered<R, TH, NL, +1, -1>(Ts, lane);
+            else                sweep_layered<R, TH, NL, -1, -1>(Ts, lane);
         }
         __syncthreads();
-        if constexpr (kSplitL) {
-            // ---- split-role boundary (fim2d.hip EIK_SPLIT_WB)
-            const bool storer = wave >= 2;
-            unsigned fl = 0, chg = 0;
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                const int ry = wave + 4 * j;
-                const int64_t gy = y0 + ry, gx = x0 + lane;
-                const bool in = gy < a.H && gx < a.W;
-                const int64_t gi = (gy * a.W + gx) * ls + a.z0;
-                const LCell<R> nv4 = Ts[(ry + 1) * kLds + lane + 1];
-#pragma unroll
-                for (int z = 0; z < NL; ++z) {
-                    const R nv = nv4.get(z);
-                    if (in && nv < told[j][z]) {
-                        if (storer) T.st(gi + z, nv);
-                        else chg |= 1u << j;
-                    }
-                    if (nv < told[j][z] * R(keep)) {
-                        fl |= 128u;
-                        if (ry == 0 && nv < Ts[lane + 1].get(z)) fl |= 1u;
-                        if (ry == TH - 1 && nv < Ts[(TH + 1) * kLds + lane + 1].get(z)) fl |= 2u;
-                        if (lane == 0 && nv < Ts[(ry + 1) * kLds].get(z)) fl |= 4u;
-                        if (lane == kTile - 1 && nv < Ts[(ry + 1) * kLds + kLds - 1].get(z)) fl |= 8u;
-                    }
-                    told[j][z] = nv;  // what memory holds once the stores land
-                }
-            }
-            if (!storer) L.chg[tid] = (unsigned short)chg;
-            if (fl) atomicOr(&L.flags, fl);
-            __syncthreads();
-            const unsigned f = L.flags;  // uniform
-            if (storer) {  // waves 0-1's changed cells (all their layers: an unchanged value is what memory holds)
-                const int c = tid - 128, cw = c >> 6;
-                const unsigned cm = L.chg[c];
-#pragma unroll
-                for (int j = 0; j < NJ; ++j) {
-                    if ((cm >> j) & 1u) {
-                        const int ry = cw + 4 * j;
-                        const int64_t gi = ((y0 + ry) * a.W + x0 + lane) * ls + a.z0;
-                        const LCell<R> nv4 = Ts[(ry + 1) * kLds + lane + 1];
-#pragma unroll
-                        for (int z = 0; z < NL; ++z) T.st(gi + z, nv4.get(z));
-                    }
-                }
-            }
-            if (!(f & 128u) || pass + 1 >= kPasses) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the visit's last stores land first
-                __syncthreads();
-                break;
-            }
-            if (!storer) {  // the halo ring: wave 0 north and west, wave 1 south and east
-                int h0, h1;
-                const LCell<R> v0 = halo_k(wave, h0), v1 = halo_k(wave + 2, h1);
-                if (tid == 64) charge_inplace_pass(a);  // in-place passes: stats and the visit budget
-                if (h0 >= 0) Ts[h0] = v0;
-                if (h1 >= 0) Ts[h1] = v1;
-            }
-            act_f = f;  // wave 2 activates them in the next sweep, once the stores have landed
-            dirs = 0xFu;
-            __syncthreads();
-            if (tid == 0) L.flags = 0;
-            continue;
-        }
         // ---- write back changed cells, collect side flags
         unsigned fl = 0;
 #pragma unroll
