@@ -66,6 +66,11 @@ __device__ __forceinline__ R stage_cost(R c) {
 #endif
 constexpr int kActStep = EIK_ACT_STEP;
 
+// (EIK_LAZY_CLAIM, round 4: a grabbed tile claimed -- PENDING -> BUSY -- at its first pass boundary
+// instead of before its staging, taking the grab's exchange round trip off the front's hop; the
+// first boundary then has to reload the halo to tell new activations from the served ones.
+// Measured and removed: C2 fp64 2.34-2.37 -> 2.38-2.39 ms, C3 / C4 within noise,
+// profiles/r04f_lazy_claim_ab.log.)
 // (Also measured in round 4 and removed, profiles/r04d_follow_split_ab.log: EIK_FOLLOW -- a workgroup
 // whose pass made a FRESH neighbour reachable claimed it and continued with it, skipping the queue's
 // round trips; and EIK_SPLIT_WB -- two waves stored the write-back without waiting while two

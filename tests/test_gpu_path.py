@@ -228,5 +228,6 @@ def test_pinned_results_round_trip(ctx):
     n_free = sum(len(v) for v in L._pin_free.values())
     del T
     assert sum(len(v) for v in L._pin_free.values()) == n_free + 1  # back in the pool
-    T2 = ctx.tmap2d(cost, goal)  # reuses it
-    assert np.array_equal(T2, Tp, equal_nan=True)
+    T2 = ctx.tmap2d(cost, goal)  # reuses it (a second solve: equal up to the fp64 rounding of its schedule)
+    fin = np.isfinite(Tp)
+    assert np.array_equal(np.isfinite(T2), fin) and np.abs(T2[fin] - Tp[fin]).max() <= 1e-9
