@@ -54,8 +54,14 @@ struct DevBuf {
 };
 
 // Host memcpy split over a few worker threads and the caller (the pinned-staging copies below).
+// ONE pool per process, shared by every context (8 DD ranks sharing a node each started
+// their own threads), created on the first large copy; concurrent callers take turns.
 class CopyPool {
   public:
+    static CopyPool* shared() {
+        static CopyPool* p = new CopyPool((int)std::max(1u, std::min(3u, std::thread::hardware_concurrency() / 2)));
+        return p;  // (never destroyed: workers outlive the contexts, the process ends them)
+    }
     explicit CopyPool(int workers) {
         for (int i = 0; i < workers; ++i) th_.emplace_back([this] { loop(); });
     }
@@ -68,6 +74,7 @@ class CopyPool {
         for (auto& t : th_) t.join();
     }
     void copy(void* dst, const void* src, size_t len) {
+        std::lock_guard<std::mutex> turn(caller_);  // one copy at a time (contexts of other threads wait)
         const int parts = (int)th_.size() + 1;
         {
             std::lock_guard<std::mutex> g(m_);
@@ -86,6 +93,7 @@ class CopyPool {
     }
 
   private:
+    std::mutex caller_;
     void part(int k, int parts) {
         const size_t a = len_ * k / parts, e = len_ * (k + 1) / parts;
         std::memcpy(dst_ + a, src_ + a, e - a);
@@ -242,7 +250,7 @@ static hipError_t stage_init(eik_ctx* c) {
             if (e != hipSuccess) return e;
         }
     }
-    if (!c->pool) c->pool = new CopyPool((int)std::max(1u, std::min(3u, std::thread::hardware_concurrency() / 2)));
+    if (!c->pool) c->pool = CopyPool::shared();
     return hipSuccess;
 }
 static hipError_t host_to_dev(eik_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st) {
@@ -330,7 +338,7 @@ void eik_destroy(eik_ctx* c) {
         if (c->stage[b]) (void)hipHostFree(c->stage[b]);
         if (c->stage_ev[b]) (void)hipEventDestroy(c->stage_ev[b]);
     }
-    delete c->pool;
+    c->pool = nullptr;  // (the process-wide pool stays)
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     if (c->stream) (void)hipStreamDestroy(c->stream);
