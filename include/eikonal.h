@@ -125,6 +125,15 @@ int eik_tmap2d_f64(eik_ctx* ctx, const double* cost, int64_t H, int64_t W, int64
 int eik_tmap2d_bidir_f64(eik_ctx* ctx, const double* cost, int64_t H, int64_t W, int64_t gx, int64_t gy,
                          int64_t sx, int64_t sy, double* TG, double* TS, uint32_t join[2]);
 
+/* The join step of biComputeTmap alone (FastMarching.py:141-162) from two given FULL fields
+ * TG (goal front) and TS (start front), H*W fp64 each (+inf = unreached): nodeJoin and the two
+ * partial fields TGp / TSp, exactly as eik_tmap2d_bidir_f64 forms them after its solve.  members
+ * (optional): the cells ranked per front -- the join bounds the meeting iteration first and sorts
+ * only the cells under the bound (csrc/bidir.hip).  EIK_ERR_UNREACHABLE when no cell is finite in
+ * both fields. */
+int eik_bidir_join_f64(eik_ctx* ctx, const double* TG, const double* TS, int64_t H, int64_t W, double* TGp,
+                       double* TSp, uint32_t join[2], int64_t members[2]);
+
 /* B independent maps (goal sweep / terrain Monte-Carlo): cost, T: B*H*W; goals: B x (x, y). */
 int eik_tmap2d_batch_f32(eik_ctx* ctx, const float* cost, int64_t B, int64_t H, int64_t W, const int64_t* goals,
                          float* T);

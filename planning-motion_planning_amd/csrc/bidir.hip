@@ -6,10 +6,25 @@
 // (rankG(s_k) <= k, :153-155).  A front pops nodes in increasing T, so with
 //     rankG(n) = position of n in ascending TG,  rankS(n) = position in ascending TS
 // the stopping iteration is k* = min_n max(rankG(n), rankS(n)), and the join is g_{k*} when it
-// qualifies (the G test runs first), else s_{k*}.  Ranks come from two device radix sorts of
-// the fields' bit patterns (non-negative IEEE doubles sort as unsigned integers); ties of
-// exactly equal T are ranked by node index (the reference breaks them LIFO by insertion time,
-// which a field does not record -- SURVEY.md §7 "join approximated").
+// qualifies (the G test runs first), else s_{k*}.  Ties of exactly equal T are ranked by node
+// index (the reference breaks them LIFO by insertion time, which a field does not record --
+// SURVEY.md §7 "join approximated").
+//
+// Only the cells the fronts pop before they meet need a rank, so the join does not sort the
+// raster.  It bounds k* first and ranks only the cells under the bound:
+//   1. seed:   n0 = argmin over cells of max(TG, TS) (both finite) -> k* <= K0 = max(rankG(n0),
+//              rankS(n0)), both ranks counted exactly in one pass beside a 256-bin coarse
+//              histogram of each field over [0, 4 max(TG(n0), TS(n0))) (+ one overflow bin)
+//   2. select: per field the smallest value bucket holding >= K0+1 cells (coarse scan, then a
+//              1024-bin histogram inside that coarse bin) -> the member set {bucket(T) <=
+//              threshold}, a prefix of the field's pop order that holds every cell of rank <= K0
+//   3. rank:   compact the members in node order (stable select), radix-sort them by T (stable,
+//              so ties stay in node order) -> their exact ranks; non-members keep rank UINT_MAX
+//   4. join:   min over cells of max(rankG, rankS) as before.
+// A non-member has rank > K0 >= k*, so it can be neither the join nor a closed cell of a partial
+// field, and the members' ranks equal their ranks in the whole field (every cell below a member
+// in pop order is a member).  The bucket function is monotone in T, so the member set is a prefix.
+// The sort then covers ~K0 cells instead of H*W (the cells the fronts popped, plus one bucket).
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -18,28 +33,258 @@
 
 namespace eik {
 
-__global__ void iota_keys_kernel(const double* __restrict__ T, int64_t n, unsigned long long* __restrict__ keys,
-                                 unsigned* __restrict__ idx) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    keys[i] = (unsigned long long)__double_as_longlong(T[i]);
-    idx[i] = (unsigned)i;
+constexpr int kCoarse = 256;   // coarse value buckets over [0, 4M) per field, the last one open-ended
+constexpr int kFine = 1024;    // fine buckets inside the threshold's coarse bucket
+constexpr unsigned kNone = 0xFFFFFFFFu;
+
+// device control block of one join, in the work buffer after the sort scratch
+struct JoinSel {
+    unsigned long long n0;  // (bits(max(TG,TS)) with the low 29 bits cleared) | node; ~0: fronts never meet
+    unsigned r0[2];         // exact ranks of n0 in TG / TS
+    double scale;           // coarse buckets per unit of T: kCoarse / (4 M)
+    int cb[2];              // threshold coarse bucket per field (-1: no member; kCoarse-1: every finite cell)
+    int fb[2];              // threshold fine bucket inside cb
+    unsigned need[2];       // members still needed inside cb (K0 + 1 - cells of lower coarse buckets)
+    unsigned m[2];          // member count per field (select output)
+    unsigned hc[2][kCoarse];
+    unsigned hf[2][kFine];
+};
+
+__device__ __forceinline__ bool fin(double t) { return t < Real<double>::inf(); }
+
+__device__ __forceinline__ int coarse_of(double t, double s) {
+    const double q = t * s;
+    return q >= double(kCoarse - 1) ? kCoarse - 1 : (int)q;
 }
 
-// rank[sorted_idx[k]] = k for finite entries, UINT_MAX for unreached (never popped) ones
-__global__ void scatter_rank_kernel(const unsigned long long* __restrict__ skeys, const unsigned* __restrict__ sidx,
-                                    int64_t n, unsigned* __restrict__ rank) {
+__device__ __forceinline__ int fine_of(double t, double s, int c) {
+    const double q = (t * s - double(c)) * double(kFine);
+    return q >= double(kFine - 1) ? kFine - 1 : (q <= 0.0 ? 0 : (int)q);
+}
+
+// the member test (monotone in t): a prefix of the field's pop order
+struct JoinMember {
+    const double* T;
+    const JoinSel* sel;
+    int f;
+    __device__ bool operator()(const unsigned& i) const {
+        const double t = T[i];
+        const int tc = sel->cb[f];
+        if (tc < 0 || !fin(t)) return false;
+        const int c = coarse_of(t, sel->scale);
+        if (c != tc) return c < tc;
+        return tc == kCoarse - 1 || fine_of(t, sel->scale, c) <= sel->fb[f];
+    }
+};
+
+template <typename V>
+__device__ __forceinline__ V wave_min(V v) {
+    for (int off = 32; off > 0; off >>= 1) {
+        const V o = __shfl_xor(v, off, 64);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ unsigned wave_sum(unsigned v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// LDS histogram add, aggregated over the wave: neighbouring cells mostly share a bucket, so the
+// lanes agreeing with the first valid lane's bucket add once; the rest add one by one.  Called by
+// every lane of the wave (uniform control flow).
+__device__ __forceinline__ void hist_add(unsigned* h, int bin, bool valid) {
+    const unsigned long long vm = __ballot(valid);
+    if (!vm) return;
+    const int src = __ffsll((long long)vm) - 1;
+    const int b0 = __shfl(bin, src, 64);
+    const bool same = valid && bin == b0;
+    const unsigned long long sm = __ballot(same);
+    if (same) {
+        if ((int)(threadIdx.x & 63) == src) atomicAdd(&h[b0], (unsigned)__popcll(sm));
+    } else if (valid) {
+        atomicAdd(&h[bin], 1u);
+    }
+}
+
+constexpr int kPassBlocks = 1024;  // grid-stride passes over the raster: 4 workgroups per CU
+
+// 1a. n0: argmin of max(TG, TS) over the cells both fronts reach, to 2^-23 relative (the low 29
+//     bits of the value carry the node) -- any such cell bounds k*, the closest only tightens it
+__global__ __launch_bounds__(256) void join_seed_kernel(const double* __restrict__ TG, const double* __restrict__ TS,
+                                                        int64_t n, JoinSel* __restrict__ sel) {
+    __shared__ unsigned long long wmin[4];
+    unsigned long long v = ~0ull;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const double a = TG[i], b = TS[i];
+        if (fin(a) && fin(b)) {
+            const unsigned long long m = (unsigned long long)__double_as_longlong(a > b ? a : b);
+            const unsigned long long c = (m & ~((1ull << 29) - 1)) | (unsigned long long)i;
+            v = c < v ? c : v;
+        }
+    }
+    v = wave_min(v);
+    if ((threadIdx.x & 63) == 0) wmin[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long m = wmin[0];
+        for (int w = 1; w < 4; ++w) m = wmin[w] < m ? wmin[w] : m;
+        if (m != ~0ull) atomicMin(&sel->n0, m);
+    }
+}
+
+// 1b. the exact ranks of n0 in both fields (cells before it in (T, node) order) and the coarse
+//     histograms (the scale join_scale_kernel derived from n0)
+__global__ __launch_bounds__(256) void join_count_kernel(const double* __restrict__ TG, const double* __restrict__ TS,
+                                                         int64_t n, JoinSel* __restrict__ sel) {
+    __shared__ unsigned h[2][kCoarse];
+    __shared__ unsigned wsum[2][4];
+    const unsigned long long p = sel->n0;
+    if (p == ~0ull) return;
+    const int64_t node = (int64_t)(p & ((1ull << 29) - 1));
+    const double g0 = TG[node], s0 = TS[node];
+    const double s = sel->scale;
+    for (int b = threadIdx.x; b < 2 * kCoarse; b += blockDim.x) (&h[0][0])[b] = 0;
+    __syncthreads();
+    unsigned cg = 0, cs = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n; i0 += stride) {
+        const int64_t i = i0 + threadIdx.x;
+        const bool in = i < n;
+        const double a = in ? TG[i] : Real<double>::inf(), b = in ? TS[i] : Real<double>::inf();
+        cg += (a < g0 || (a == g0 && i < node)) ? 1u : 0u;
+        cs += (b < s0 || (b == s0 && i < node)) ? 1u : 0u;
+        const bool fa = fin(a), fb = fin(b);
+        hist_add(h[0], fa ? coarse_of(a, s) : 0, fa);
+        hist_add(h[1], fb ? coarse_of(b, s) : 0, fb);
+    }
+    __syncthreads();
+    cg = wave_sum(cg);
+    cs = wave_sum(cs);
+    if ((threadIdx.x & 63) == 0) {
+        wsum[0][threadIdx.x >> 6] = cg;
+        wsum[1][threadIdx.x >> 6] = cs;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        const unsigned t = wsum[threadIdx.x][0] + wsum[threadIdx.x][1] + wsum[threadIdx.x][2] + wsum[threadIdx.x][3];
+        if (t) atomicAdd(&sel->r0[threadIdx.x], t);
+    }
+    for (int b = threadIdx.x; b < 2 * kCoarse; b += blockDim.x) {
+        const unsigned v = (&h[0][0])[b];
+        if (v) atomicAdd(&(&sel->hc[0][0])[b], v);
+    }
+}
+
+// 2a. per field the first coarse bucket whose running count reaches K0 + 1 (one thread per field)
+__global__ void join_coarse_scan_kernel(JoinSel* __restrict__ sel) {
+    const int f = threadIdx.x;
+    if (f >= 2) return;
+    if (sel->n0 == ~0ull) {
+        sel->cb[f] = -1;
+        return;
+    }
+    const unsigned k0 = sel->r0[0] > sel->r0[1] ? sel->r0[0] : sel->r0[1];
+    unsigned cum = 0;
+    int c = kCoarse - 1;
+    for (int b = 0; b < kCoarse; ++b) {
+        if (cum + sel->hc[f][b] >= k0 + 1) {
+            c = b;
+            break;
+        }
+        cum += sel->hc[f][b];
+    }
+    sel->cb[f] = c;
+    sel->need[f] = k0 + 1 - cum;
+    sel->fb[f] = kFine - 1;
+}
+
+// 2b. fine histogram of the cells inside the threshold coarse bucket
+__global__ __launch_bounds__(256) void join_fine_kernel(const double* __restrict__ TG, const double* __restrict__ TS,
+                                                        int64_t n, JoinSel* __restrict__ sel) {
+    __shared__ unsigned h[2][kFine];
+    const int c0 = sel->cb[0], c1 = sel->cb[1];
+    const bool w0 = c0 >= 0 && c0 < kCoarse - 1, w1 = c1 >= 0 && c1 < kCoarse - 1;
+    if (!w0 && !w1) return;
+    const double s = sel->scale;
+    for (int b = threadIdx.x; b < 2 * kFine; b += blockDim.x) (&h[0][0])[b] = 0;
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n; i0 += stride) {
+        const int64_t i = i0 + threadIdx.x;
+        const bool in = i < n;
+        if (w0) {
+            const double a = in ? TG[i] : Real<double>::inf();
+            const bool v = fin(a) && coarse_of(a, s) == c0;
+            hist_add(h[0], v ? fine_of(a, s, c0) : 0, v);
+        }
+        if (w1) {
+            const double b = in ? TS[i] : Real<double>::inf();
+            const bool v = fin(b) && coarse_of(b, s) == c1;
+            hist_add(h[1], v ? fine_of(b, s, c1) : 0, v);
+        }
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < 2 * kFine; b += blockDim.x) {
+        const unsigned v = (&h[0][0])[b];
+        if (v) atomicAdd(&(&sel->hf[0][0])[b], v);
+    }
+}
+
+__global__ void join_fine_scan_kernel(JoinSel* __restrict__ sel) {
+    const int f = threadIdx.x;
+    if (f >= 2) return;
+    const int c = sel->cb[f];
+    if (c < 0 || c == kCoarse - 1) return;
+    unsigned cum = 0;
+    int t = kFine - 1;
+    for (int b = 0; b < kFine; ++b) {
+        cum += sel->hf[f][b];
+        if (cum >= sel->need[f]) {
+            t = b;
+            break;
+        }
+    }
+    sel->fb[f] = t;
+}
+
+// the scale both histograms and the member test use, from n0 (one thread)
+__global__ void join_scale_kernel(const double* __restrict__ TG, const double* __restrict__ TS,
+                                  JoinSel* __restrict__ sel) {
+    const unsigned long long p = sel->n0;
+    if (p == ~0ull) {
+        sel->scale = 1.0;
+        return;
+    }
+    const int64_t node = (int64_t)(p & ((1ull << 29) - 1));
+    const double g0 = TG[node], s0 = TS[node];
+    const double M = g0 > s0 ? g0 : s0;
+    sel->scale = double(kCoarse) / (4.0 * (M > 0.0 ? M : 1.0));
+}
+
+// 3. keys of the compacted members (node order) for the stable sort
+__global__ void join_gather_kernel(const double* __restrict__ T, const unsigned* __restrict__ list, int64_t m,
+                                   unsigned long long* __restrict__ keys, unsigned* __restrict__ idx) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    const unsigned i = list[j];
+    keys[j] = (unsigned long long)__double_as_longlong(T[i]);
+    idx[j] = i;
+}
+
+// rank[sorted_idx[k]] = k for the members; every other cell keeps UINT_MAX (memset)
+__global__ void scatter_rank_kernel(const unsigned* __restrict__ sidx, int64_t m, unsigned* __restrict__ rank) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
-    const bool fin = skeys[k] < 0x7FF0000000000000ull;
-    rank[sidx[k]] = fin ? (unsigned)k : 0xFFFFFFFFu;
+    if (k >= m) return;
+    rank[sidx[k]] = (unsigned)k;
 }
 
 // packed = (2*max(rG,rS) + (rG == max ? 0 : 1)) << 29 | node ; the min identifies the join.
 // Grid-stride over the cells, a wave then a workgroup (LDS) minimum, ONE atomicMin per workgroup:
 // one atomic per wave on the single result word serialised ~260k device-scope atomics for a
 // 4096^2 raster (2.98 ms, tools/rover_probe.py under rocprofv3).
-constexpr int kJoinBlocks = 1024;
 __global__ __launch_bounds__(256) void join_min_kernel(const unsigned* __restrict__ rg, const unsigned* __restrict__ rs,
                                                        int64_t n, unsigned long long* __restrict__ best) {
     __shared__ unsigned long long wmin[4];
@@ -47,16 +292,13 @@ __global__ __launch_bounds__(256) void join_min_kernel(const unsigned* __restric
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const unsigned a = rg[i], b = rs[i];
-        if (a != 0xFFFFFFFFu && b != 0xFFFFFFFFu) {
+        if (a != kNone && b != kNone) {
             const unsigned long long m = a > b ? a : b;
             const unsigned long long c = ((2ull * m + (a == m ? 0ull : 1ull)) << 29) | (unsigned long long)i;
             v = c < v ? c : v;
         }
     }
-    for (int off = 32; off > 0; off >>= 1) {
-        const unsigned long long o = __shfl_xor(v, off, 64);
-        v = o < v ? o : v;
-    }
+    v = wave_min(v);
     if ((threadIdx.x & 63) == 0) wmin[threadIdx.x >> 6] = v;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -66,39 +308,102 @@ __global__ __launch_bounds__(256) void join_min_kernel(const unsigned* __restric
     }
 }
 
-struct JoinScratch {
-    void* tmp = nullptr;
-    size_t tmp_bytes = 0;
+namespace {
+
+struct JoinLayout {
+    unsigned long long *k_in, *k_out;
+    unsigned *i_in, *i_out, *rg, *rs;
+    char* cub_tmp;
+    size_t cub_bytes;
+    JoinSel* sel;
+    size_t total;
 };
 
-// d_TG/d_TS: n doubles; d_work must hold 2n u64 + 4n u32 (+ cub scratch appended by caller).
+size_t cub_scratch(int64_t n) {
+    size_t sort_b = 0, sel_b = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort_b, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                             (unsigned*)nullptr, (unsigned*)nullptr, (int)n, 0, 64, (hipStream_t)0);
+    (void)hipcub::DeviceSelect::If(nullptr, sel_b, hipcub::CountingInputIterator<unsigned>(0u), (unsigned*)nullptr,
+                                   (unsigned*)nullptr, n, JoinMember{nullptr, nullptr, 0}, (hipStream_t)0);
+    return (std::max(sort_b, sel_b) + 255) & ~size_t(255);
+}
+
+// k_in | k_out (n u64) | i_in | i_out | rg | rs (n u32) | cub scratch | JoinSel
+JoinLayout layout(void* work, int64_t n) {
+    JoinLayout L{};
+    char* p = static_cast<char*>(work);
+    L.k_in = reinterpret_cast<unsigned long long*>(p);
+    L.k_out = L.k_in + n;
+    L.i_in = reinterpret_cast<unsigned*>(L.k_out + n);
+    L.i_out = L.i_in + n;
+    L.rg = L.i_out + n;
+    L.rs = L.rg + n;
+    const size_t head = ((size_t)n * (2 * 8 + 4 * 4) + 255) & ~size_t(255);
+    L.cub_tmp = p + head;
+    L.cub_bytes = cub_scratch(n);
+    L.sel = reinterpret_cast<JoinSel*>(L.cub_tmp + L.cub_bytes);
+    L.total = head + L.cub_bytes + ((sizeof(JoinSel) + 255) & ~size_t(255));
+    return L;
+}
+
+}  // namespace
+
+// d_TG/d_TS: n doubles (full fields); d_work: bidir_join_work_bytes(n).  One host synchronisation
+// (the member counts size the sorts).  members (optional, host): the two member-set sizes.
 hipError_t bidir_join(const double* d_TG, const double* d_TS, int64_t n, void* d_work, size_t work_bytes,
-                      unsigned long long* d_best, hipStream_t st) {
+                      unsigned long long* d_best, hipStream_t st, int64_t* members) {
     if (n >= (1ll << 29)) return hipErrorInvalidValue;
-    char* p = static_cast<char*>(d_work);
-    auto* k_in = reinterpret_cast<unsigned long long*>(p);
-    auto* k_out = k_in + n;
-    auto* i_in = reinterpret_cast<unsigned*>(k_out + n);
-    auto* i_out = i_in + n;
-    auto* rg = i_out + n;
-    auto* rs = rg + n;
-    char* cub_tmp = reinterpret_cast<char*>(rs + n);
-    const size_t used = (size_t)(cub_tmp - p);
-    size_t cub_bytes = 0;
-    hipError_t e1 = hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, k_in, k_out, i_in, i_out, (int)n, 0, 64, st);
-    if (e1 != hipSuccess) return e1;
-    if (used + cub_bytes > work_bytes) return hipErrorOutOfMemory;
-    const unsigned grid = (unsigned)((n + 255) / 256);
+    const JoinLayout L = layout(d_work, n);
+    if (L.total > work_bytes) return hipErrorOutOfMemory;
+    JoinSel* sel = L.sel;
+    hipError_t e = hipMemsetAsync(sel, 0, sizeof(JoinSel), st);
+    if (e == hipSuccess) e = hipMemsetAsync(&sel->n0, 0xFF, sizeof(sel->n0), st);
+    if (e != hipSuccess) return e;
+    const unsigned pgrid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(kPassBlocks, (n + 255) / 256));
+    hipLaunchKernelGGL(join_seed_kernel, dim3(pgrid), dim3(256), 0, st, d_TG, d_TS, n, sel);
+    hipLaunchKernelGGL(join_scale_kernel, dim3(1), dim3(1), 0, st, d_TG, d_TS, sel);
+    hipLaunchKernelGGL(join_count_kernel, dim3(pgrid), dim3(256), 0, st, d_TG, d_TS, n, sel);
+    hipLaunchKernelGGL(join_coarse_scan_kernel, dim3(1), dim3(64), 0, st, sel);
+    hipLaunchKernelGGL(join_fine_kernel, dim3(pgrid), dim3(256), 0, st, d_TG, d_TS, n, sel);
+    hipLaunchKernelGGL(join_fine_scan_kernel, dim3(1), dim3(64), 0, st, sel);
+    // stable compaction of the members: G into i_in, S into rs (free until its ranks are scattered)
+    const double* T[2] = {d_TG, d_TS};
+    unsigned* lists[2] = {L.i_in, L.rs};
     for (int f = 0; f < 2; ++f) {
-        hipLaunchKernelGGL(iota_keys_kernel, dim3(grid), dim3(256), 0, st, f == 0 ? d_TG : d_TS, n, k_in, i_in);
-        hipError_t e = hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, k_in, k_out, i_in, i_out, (int)n, 0, 64, st);
+        size_t b = L.cub_bytes;
+        e = hipcub::DeviceSelect::If(L.cub_tmp, b, hipcub::CountingInputIterator<unsigned>(0u), lists[f], &sel->m[f],
+                                     n, JoinMember{T[f], sel, f}, st);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(scatter_rank_kernel, dim3(grid), dim3(256), 0, st, k_out, i_out, n, f == 0 ? rg : rs);
     }
-    hipError_t e0 = hipMemsetAsync(d_best, 0xFF, sizeof(unsigned long long), st);
-    if (e0 != hipSuccess) return e0;
-    const unsigned jgrid = (unsigned)std::min<int64_t>(kJoinBlocks, (n + 255) / 256);
-    hipLaunchKernelGGL(join_min_kernel, dim3(jgrid), dim3(256), 0, st, rg, rs, n, d_best);
+    unsigned hm[2] = {0, 0};
+    e = hipMemcpyAsync(hm, sel->m, sizeof hm, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return e;
+    if (members) {
+        members[0] = hm[0];
+        members[1] = hm[1];
+    }
+    unsigned* rank[2] = {L.rg, L.rs};
+    for (int f = 0; f < 2; ++f) {
+        const int64_t m = hm[f];
+        if (m > 0) {
+            const unsigned g = (unsigned)((m + 255) / 256);
+            hipLaunchKernelGGL(join_gather_kernel, dim3(g), dim3(256), 0, st, T[f], lists[f], m, L.k_in, L.i_in);
+        }
+        e = hipMemsetAsync(rank[f], 0xFF, sizeof(unsigned) * (size_t)n, st);
+        if (e != hipSuccess) return e;
+        if (m > 0) {
+            size_t b = L.cub_bytes;
+            e = hipcub::DeviceRadixSort::SortPairs(L.cub_tmp, b, L.k_in, L.k_out, L.i_in, L.i_out, (int)m, 0, 64, st);
+            if (e != hipSuccess) return e;
+            const unsigned g = (unsigned)((m + 255) / 256);
+            hipLaunchKernelGGL(scatter_rank_kernel, dim3(g), dim3(256), 0, st, L.i_out, m, rank[f]);
+        }
+    }
+    e = hipMemsetAsync(d_best, 0xFF, sizeof(unsigned long long), st);
+    if (e != hipSuccess) return e;
+    const unsigned jgrid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(kPassBlocks, (n + 255) / 256));
+    hipLaunchKernelGGL(join_min_kernel, dim3(jgrid), dim3(256), 0, st, L.rg, L.rs, n, d_best);
     return hipGetLastError();
 }
 
@@ -126,20 +431,13 @@ __global__ void bidir_partial_kernel(double* __restrict__ T, const unsigned* __r
 hipError_t bidir_partial(double* d_TG, double* d_TS, int64_t H, int64_t W, const void* d_work,
                          const unsigned long long* d_best, hipStream_t st) {
     const int64_t n = H * W;
-    const char* p = static_cast<const char*>(d_work);
-    const unsigned* rg = reinterpret_cast<const unsigned*>(p + (size_t)n * (2 * 8 + 2 * 4));
-    const unsigned* rs = rg + n;
+    const JoinLayout L = layout(const_cast<void*>(d_work), n);
     const unsigned grid = (unsigned)((n + 255) / 256);
-    hipLaunchKernelGGL(bidir_partial_kernel, dim3(grid), dim3(256), 0, st, d_TG, rg, H, W, d_best);
-    hipLaunchKernelGGL(bidir_partial_kernel, dim3(grid), dim3(256), 0, st, d_TS, rs, H, W, d_best);
+    hipLaunchKernelGGL(bidir_partial_kernel, dim3(grid), dim3(256), 0, st, d_TG, L.rg, H, W, d_best);
+    hipLaunchKernelGGL(bidir_partial_kernel, dim3(grid), dim3(256), 0, st, d_TS, L.rs, H, W, d_best);
     return hipGetLastError();
 }
 
-size_t bidir_join_work_bytes(int64_t n) {
-    size_t cub_bytes = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                                       (unsigned*)nullptr, (unsigned*)nullptr, (int)n, 0, 64, (hipStream_t)0);
-    return (size_t)n * (2 * 8 + 4 * 4) + cub_bytes + 256;
-}
+size_t bidir_join_work_bytes(int64_t n) { return layout(nullptr, n).total; }
 
 }  // namespace eik

@@ -23,7 +23,7 @@
 
 namespace eik {
 hipError_t bidir_join(const double* d_TG, const double* d_TS, int64_t n, void* d_work, size_t work_bytes,
-                      unsigned long long* d_best, hipStream_t st);
+                      unsigned long long* d_best, hipStream_t st, int64_t* members = nullptr);
 size_t bidir_join_work_bytes(int64_t n);
 // after bidir_join on the same work buffer: the two fields -> biComputeTmap's partial fields
 hipError_t bidir_partial(double* d_TG, double* d_TS, int64_t H, int64_t W, const void* d_work,
@@ -1004,6 +1004,21 @@ int eik_tmap2d_batch_f32(eik_ctx* c, const float* cost, int64_t B, int64_t H, in
     return tmap_host<float>(c, cost, B, H, W, goals, T);
 }
 
+// nodeJoin + partial fields from the two device-resident full fields dT[0:n] (goal front) and
+// dT[n:2n] (start front), in place; *best = the packed join (~0: the fronts never meet).  Ends
+// with the stream synchronised on *best.
+static int join_and_partial(eik_ctx* c, double* dT, int64_t n, int64_t H, int64_t W, unsigned long long* best,
+                            int64_t members[2]) {
+    hipStream_t st = c->stream;
+    HIPCHK(c, c->work.ensure(bidir_join_work_bytes(n)));
+    HIPCHK(c, c->misc.ensure(64));
+    HIPCHK(c, bidir_join(dT, dT + n, n, c->work.p, c->work.bytes, (unsigned long long*)c->misc.p, st, members));
+    HIPCHK(c, bidir_partial(dT, dT + n, H, W, c->work.p, (const unsigned long long*)c->misc.p, st));
+    HIPCHK(c, hipMemcpyAsync(best, c->misc.p, sizeof *best, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    return EIK_OK;
+}
+
 int eik_tmap2d_bidir_f64(eik_ctx* c, const double* cost, int64_t H, int64_t W, int64_t gx, int64_t gy, int64_t sx,
                          int64_t sy, double* TG, double* TS, uint32_t join[2]) {
     if (!c || !cost || !TG || !TS || !join) return c ? set_err(c, EIK_ERR_ARG, "NULL argument") : EIK_ERR_ARG;
@@ -1030,21 +1045,44 @@ int eik_tmap2d_bidir_f64(eik_ctx* c, const double* cost, int64_t H, int64_t W, i
     HIPCHK(c, hipMemcpyAsync(dcost + n, dcost, sizeof(double) * n, hipMemcpyDeviceToDevice, c->stream));
     rc = eik_fim2d_solve(f, dcost, c->T.p, goals, c->stream);
     if (rc) return rc;
-    // join from the device-resident fields (c->T holds both maps back to back)
-    const size_t wb = bidir_join_work_bytes(n);
-    HIPCHK(c, c->work.ensure(wb));
-    HIPCHK(c, c->misc.ensure(64));
-    HIPCHK(c, bidir_join((const double*)c->T.p, (const double*)c->T.p + n, n, c->work.p, c->work.bytes,
-                         (unsigned long long*)c->misc.p, c->stream));
-    // the fronts' partial fields at the meeting iteration (FastMarching.py:141-162)
-    HIPCHK(c, bidir_partial((double*)c->T.p, (double*)c->T.p + n, H, W, c->work.p,
-                            (const unsigned long long*)c->misc.p, c->stream));
+    // join from the device-resident fields (c->T holds both maps back to back), then the fronts'
+    // partial fields at the meeting iteration (FastMarching.py:141-162)
     unsigned long long best = 0;
-    HIPCHK(c, hipMemcpyAsync(&best, c->misc.p, sizeof best, hipMemcpyDeviceToHost, c->stream));
+    rc = join_and_partial(c, (double*)c->T.p, n, H, W, &best, nullptr);
+    if (rc) return rc;
     HIPCHK(c, dev_to_host(c, TG, c->T.p, sizeof(double) * n, c->stream));
     HIPCHK(c, dev_to_host(c, TS, (double*)c->T.p + n, sizeof(double) * n, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (best == ~0ull) return set_err(c, EIK_ERR_UNREACHABLE, "goal and start are not connected");
+    const int64_t node = (int64_t)(best & ((1ull << 29) - 1));
+    join[0] = (uint32_t)(node % W);
+    join[1] = (uint32_t)(node / W);
+    return EIK_OK;
+}
+
+int eik_bidir_join_f64(eik_ctx* c, const double* TG, const double* TS, int64_t H, int64_t W, double* TGp,
+                       double* TSp, uint32_t join[2], int64_t members[2]) {
+    if (!c || !TG || !TS || !TGp || !TSp || !join) return c ? set_err(c, EIK_ERR_ARG, "NULL argument") : EIK_ERR_ARG;
+    if (H < 1 || W < 1) return set_err(c, EIK_ERR_ARG, "empty field");
+    const int64_t n = H * W;
+    if (n >= (1ll << 29)) return set_err(c, EIK_ERR_ARG, "bidirectional join supports < 2^29 cells");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, c->T.ensure(sizeof(double) * 2 * n));
+    double* dT = (double*)c->T.p;
+    HIPCHK(c, host_to_dev(c, dT, TG, sizeof(double) * n, c->stream));
+    HIPCHK(c, host_to_dev(c, dT + n, TS, sizeof(double) * n, c->stream));
+    unsigned long long best = 0;
+    int64_t mem[2] = {0, 0};
+    int rc = join_and_partial(c, dT, n, H, W, &best, mem);
+    if (rc) return rc;
+    if (members) {
+        members[0] = mem[0];
+        members[1] = mem[1];
+    }
+    if (best == ~0ull) return set_err(c, EIK_ERR_UNREACHABLE, "the fields share no finite cell");
+    HIPCHK(c, dev_to_host(c, TGp, dT, sizeof(double) * n, c->stream));
+    HIPCHK(c, dev_to_host(c, TSp, dT + n, sizeof(double) * n, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     const int64_t node = (int64_t)(best & ((1ull << 29) - 1));
     join[0] = (uint32_t)(node % W);
     join[1] = (uint32_t)(node / W);
@@ -1697,14 +1735,9 @@ int eik_rover_path_f64(eik_ctx* c, const double* Z, int64_t H, int64_t W, const 
     if (rc) return rc;
     rc = eik_fim2d_solve(f, dcost, dT, g, st);
     if (rc) return rc;
-    const size_t wb = bidir_join_work_bytes(n);
-    HIPCHK(c, c->work.ensure(wb));
-    HIPCHK(c, c->misc.ensure(64));
-    HIPCHK(c, bidir_join(dT, dT + n, n, c->work.p, c->work.bytes, (unsigned long long*)c->misc.p, st));
-    HIPCHK(c, bidir_partial(dT, dT + n, H, W, c->work.p, (const unsigned long long*)c->misc.p, st));  // :141-162
     unsigned long long best = 0;
-    HIPCHK(c, hipMemcpyAsync(&best, c->misc.p, sizeof best, hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipStreamSynchronize(st));
+    rc = join_and_partial(c, dT, n, H, W, &best, nullptr);  // :141-162
+    if (rc) return rc;
     if (best == ~0ull) return set_err(c, EIK_ERR_UNREACHABLE, "the rover cannot reach the sample");
     const int64_t node = (int64_t)(best & ((1ull << 29) - 1));
     const double jn[2] = {(double)(node % W), (double)(node / W)};

@@ -103,6 +103,7 @@ def lib():
         L.eik_tmap2d_f32.argtypes = [vp, _f32p, i64, i64, i64, i64, _f32p]
         L.eik_tmap2d_f64.argtypes = [vp, _f64p, i64, i64, i64, i64, _f64p]
         L.eik_tmap2d_bidir_f64.argtypes = [vp, _f64p, i64, i64, i64, i64, i64, i64, _f64p, _f64p, _u32p]
+        L.eik_bidir_join_f64.argtypes = [vp, _f64p, _f64p, i64, i64, _f64p, _f64p, _u32p, _i64p]
         L.eik_tmap2d_batch_f32.argtypes = [vp, _f32p, i64, i64, i64, _i64p, _f32p]
         L.eik_path2d_f64.argtypes = [vp, _f64p, i64, i64, _f64p, _f64p, C.c_double, _f64p, i64, P(i64), P(C.c_int)]
         L.eik_gradient2d_f64.argtypes = [vp, _f64p, i64, i64, _f64p, _f64p]
@@ -164,7 +165,7 @@ def lib():
 
 EXPORTED = [
     "eik_version", "eik_create", "eik_destroy", "eik_last_error", "eik_set_option", "eik_get_stats",
-    "eik_tmap2d_f32", "eik_tmap2d_f64", "eik_tmap2d_bidir_f64", "eik_tmap2d_batch_f32", "eik_path2d_f64",
+    "eik_tmap2d_f32", "eik_tmap2d_f64", "eik_tmap2d_bidir_f64", "eik_bidir_join_f64", "eik_tmap2d_batch_f32", "eik_path2d_f64",
     "eik_gradient2d_f64", "eik_fim2d_create", "eik_fim2d_destroy", "eik_fim2d_set_ghosts", "eik_fim2d_start",
     "eik_fim2d_iterate", "eik_fim2d_solve", "eik_fim2d_pack_edges", "eik_fim2d_merge_ghost", "eik_fim2d_active",
     "eik_fim2d_stats", "eik_path2d_dev", "eik_selftest_walker_math", "eik_tmap3d_f32", "eik_tmap3d_f64",
@@ -299,6 +300,20 @@ class Context:
         self._chk(lib().eik_tmap2d_bidir_f64(self._h, cost, H, W, int(goal[0]), int(goal[1]), int(start[0]),
                                              int(start[1]), TG, TS, join))
         return TG, TS, join
+
+    def bidir_join(self, TG, TS):
+        """The join step of biComputeTmap (FastMarching.py:141-162) on two given full fields ->
+        (TGp, TSp, nodeJoin uint32 (x, y), members: the cells ranked per front)."""
+        TG = np.ascontiguousarray(TG, dtype=np.float64)
+        TS = np.ascontiguousarray(TS, dtype=np.float64)
+        if TG.shape != TS.shape or TG.ndim != 2:
+            raise ValueError("TG and TS must be two H x W fields")
+        H, W = TG.shape
+        TGp, TSp = np.empty_like(TG), np.empty_like(TS)
+        join = np.zeros(2, np.uint32)
+        members = np.zeros(2, np.int64)
+        self._chk(lib().eik_bidir_join_f64(self._h, TG, TS, H, W, TGp, TSp, join, members))
+        return TGp, TSp, join, members
 
     def path2d(self, T, init, end, tau=0.5):
         T = np.ascontiguousarray(T, dtype=np.float64)
