@@ -90,11 +90,15 @@ typedef enum {
                                 reach it in place (no re-queued visit); 2 = after a visit's first
                                 pass, neighbour activations wait for the visit's end (default 1:
                                 profiles/r02d_grab_sched_ab.log)                                 */
-    EIK_OPT_PATH_LOOP = 12   /* 2D path kernel: 2 (default) = one exit branch per step (the step is
+    EIK_OPT_PATH_LOOP = 12,  /* 2D path kernel: 2 (default) = one exit branch per step (the step is
                                 computed before its special cases are tested) with the f64 sqrt /
                                 division free of range handling inside their safe domain; 1 = the
                                 same loop with the compiler's sqrt / division; 0 = the loop in
                                 the reference's statement order.  Same path bits in all three.  */
+    EIK_OPT_FRONTS_CAP = 13  /* biComputeTmap / rover path, rasters >= 2^20 cells: 1 (default) solves
+                                each front only up to a cap on T estimated from a coarse copy of
+                                the raster and falls back to the full solve when the capped fields
+                                cannot be shown to give the full fields' join; 0 = full fronts    */
 } eik_option;
 
 typedef enum { EIK_MODE_LIST = 0, EIK_MODE_PERSISTENT = 1 } eik_mode;
@@ -133,6 +137,11 @@ int eik_tmap2d_bidir_f64(eik_ctx* ctx, const double* cost, int64_t H, int64_t W,
  * both fields. */
 int eik_bidir_join_f64(eik_ctx* ctx, const double* TG, const double* TS, int64_t H, int64_t W, double* TGp,
                        double* TSp, uint32_t join[2], int64_t members[2]);
+
+/* How the last biComputeTmap / rover path formed its fronts: out[0] 1 = capped fronts, out[1] 1 =
+ * the capped result was replaced by the full solve, out[2..3] cells kept under the caps (goal,
+ * start front), out[4..5] cells the join ranked per front. */
+int eik_fronts_info(const eik_ctx* ctx, int64_t out[6]);
 
 /* B independent maps (goal sweep / terrain Monte-Carlo): cost, T: B*H*W; goals: B x (x, y). */
 int eik_tmap2d_batch_f32(eik_ctx* ctx, const float* cost, int64_t B, int64_t H, int64_t W, const int64_t* goals,

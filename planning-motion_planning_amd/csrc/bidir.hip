@@ -30,6 +30,7 @@
 #include <algorithm>
 
 #include "eik_common.hpp"
+#include "eik_kernels.hpp"
 
 namespace eik {
 
@@ -415,8 +416,11 @@ hipError_t bidir_join(const double* d_TG, const double* d_TS, int64_t n, void* d
 // and the paths descended from nodeJoin (:1225-1226) then match the reference's
 // (tests/test_gpu_path.py); every other cell is +inf, as the reference leaves it.  In place: a
 // cell's own value changes only to +inf, its neighbours' closedness comes from the ranks.
+// (cost, viol: the capped fronts' check, see FrontsCheck -- a band cell of finite cost left +inf by
+// the cap would have had a finite value in the full field)
 __global__ void bidir_partial_kernel(double* __restrict__ T, const unsigned* __restrict__ rank, int64_t H, int64_t W,
-                                     const unsigned long long* __restrict__ best) {
+                                     const unsigned long long* __restrict__ best, const double* __restrict__ cost,
+                                     unsigned* __restrict__ viol) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const unsigned long long b = *best;
     if (i >= H * W || b == ~0ull) return;  // fronts never met: the reference raises, fields unused
@@ -426,15 +430,134 @@ __global__ void bidir_partial_kernel(double* __restrict__ T, const unsigned* __r
     const bool band = (x > 0 && rank[i - 1] <= k) || (x + 1 < W && rank[i + 1] <= k) ||
                       (y > 0 && rank[i - W] <= k) || (y + 1 < H && rank[i + W] <= k);
     if (!band) T[i] = Real<double>::inf();
+    else if (viol && !fin(T[i]) && fin(cost[i])) atomicOr(viol, 1u);
 }
 
 hipError_t bidir_partial(double* d_TG, double* d_TS, int64_t H, int64_t W, const void* d_work,
-                         const unsigned long long* d_best, hipStream_t st) {
+                         const unsigned long long* d_best, hipStream_t st, const double* d_cost, unsigned* d_viol) {
     const int64_t n = H * W;
     const JoinLayout L = layout(const_cast<void*>(d_work), n);
     const unsigned grid = (unsigned)((n + 255) / 256);
-    hipLaunchKernelGGL(bidir_partial_kernel, dim3(grid), dim3(256), 0, st, d_TG, L.rg, H, W, d_best);
-    hipLaunchKernelGGL(bidir_partial_kernel, dim3(grid), dim3(256), 0, st, d_TS, L.rs, H, W, d_best);
+    hipLaunchKernelGGL(bidir_partial_kernel, dim3(grid), dim3(256), 0, st, d_TG, L.rg, H, W, d_best, d_cost, d_viol);
+    hipLaunchKernelGGL(bidir_partial_kernel, dim3(grid), dim3(256), 0, st, d_TS, L.rs, H, W, d_best, d_cost, d_viol);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------ capped fronts (solve_fronts)
+// The fronts only matter up to the meeting: every cell of rank <= k* and the band around them.
+// eikonal_api.cpp's solve_fronts estimates each front's value at the meeting on a coarse copy of
+// the raster (F x F blocks), solves the two full-resolution fronts with that value (+ margin) as
+// an activation cap (Fim2dArgs::tcap), and checks the result here: every kept cell (T <= cap) is
+// exact, so the join on the capped fields is the join on the full fields when the meeting rank is
+// below both fronts' kept cell counts and no band cell was cut off.  Otherwise: the uncapped solve.
+
+// coarse block cost: the mean finite cost of the F x F block, +inf when more than half of it is
+// +inf; and the raster's largest finite cost (a band cell exceeds a closed neighbour by <= its cost)
+__global__ __launch_bounds__(256) void coarse_cost_kernel(const double* __restrict__ cost, int64_t H, int64_t W, int F,
+                                                          double* __restrict__ out, int64_t Hc, int64_t Wc,
+                                                          FrontsCheck* __restrict__ chk) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    double mx = 0.0;
+    if (j < Hc * Wc) {
+        const int64_t cy = j / Wc, cx = j - cy * Wc;
+        const int64_t y1 = std::min<int64_t>(H, (cy + 1) * F), x1 = std::min<int64_t>(W, (cx + 1) * F);
+        double sum = 0.0;
+        int nf = 0, ni = 0;
+        for (int64_t y = cy * F; y < y1; ++y)
+            for (int64_t x = cx * F; x < x1; ++x) {
+                const double v = cost[y * W + x];
+                if (fin(v)) {
+                    sum += v;
+                    ++nf;
+                    mx = v > mx ? v : mx;
+                } else {
+                    ++ni;
+                }
+            }
+        out[j] = (nf == 0 || ni > nf) ? Real<double>::inf() : sum / nf;
+    }
+    unsigned long long b = (unsigned long long)__double_as_longlong(mx);
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(b, off, 64);
+        b = o > b ? o : b;
+    }
+    if ((threadIdx.x & 63) == 0 && b) atomicMax(&chk->maxcost_bits, b);
+}
+
+// T at rank k* in each field (k* <= every member count, so both cells exist)
+__global__ void join_tk_kernel(const unsigned* __restrict__ rg, const unsigned* __restrict__ rs,
+                               const double* __restrict__ TG, const double* __restrict__ TS, int64_t n,
+                               const unsigned long long* __restrict__ best, FrontsCheck* __restrict__ chk) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned long long b = *best;
+    if (i >= n || b == ~0ull) return;
+    const unsigned k = (unsigned)(b >> 30);
+    if (rg[i] == k) chk->tk[0] = TG[i];
+    if (rs[i] == k) chk->tk[1] = TS[i];
+}
+
+// caps from the coarse meeting: F x (coarse T at rank k*) x margin + the largest finite cost;
+// +inf (no cap) when the coarse fronts never met
+__global__ void fronts_caps_kernel(const unsigned long long* __restrict__ best_c, double F, double margin,
+                                   FrontsCheck* __restrict__ chk) {
+    const int f = threadIdx.x;
+    if (f >= 2) return;
+    const double mc = __longlong_as_double((long long)chk->maxcost_bits);
+    chk->caps[f] = *best_c == ~0ull ? Real<double>::inf() : F * chk->tk[f] * margin + mc;
+}
+
+// the capped fields: T above the map's cap -> +inf (an upper bound, not the converged value), and
+// the kept (finite) cells per map
+__global__ __launch_bounds__(256) void cap_clean_kernel(double* __restrict__ T, int64_t n, FrontsCheck* __restrict__ chk) {
+    __shared__ unsigned ws[2][4];
+    const double c0 = chk->caps[0], c1 = chk->caps[1];
+    unsigned k0 = 0, k1 = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 2 * n; i += stride) {
+        const bool m1 = i >= n;
+        const double v = T[i];
+        if (fin(v)) {
+            if (v > (m1 ? c1 : c0)) T[i] = Real<double>::inf();
+            else if (m1) ++k1;
+            else ++k0;
+        }
+    }
+    k0 = wave_sum(k0);
+    k1 = wave_sum(k1);
+    if ((threadIdx.x & 63) == 0) {
+        ws[0][threadIdx.x >> 6] = k0;
+        ws[1][threadIdx.x >> 6] = k1;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        const unsigned t = ws[threadIdx.x][0] + ws[threadIdx.x][1] + ws[threadIdx.x][2] + ws[threadIdx.x][3];
+        if (t) atomicAdd(&chk->kept[threadIdx.x], t);
+    }
+}
+
+hipError_t fronts_coarse_cost(const double* d_cost, int64_t H, int64_t W, int F, double* d_out, int64_t Hc, int64_t Wc,
+                              FrontsCheck* chk, hipStream_t st) {
+    hipError_t e = hipMemsetAsync(chk, 0, sizeof(FrontsCheck), st);
+    if (e != hipSuccess) return e;
+    const int64_t nc = Hc * Wc;
+    hipLaunchKernelGGL(coarse_cost_kernel, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, st, d_cost, H, W, F, d_out,
+                       Hc, Wc, chk);
+    return hipGetLastError();
+}
+
+// after bidir_join on the coarse fields (same work buffer): the caps
+hipError_t fronts_caps(const double* d_TG, const double* d_TS, int64_t n, const void* d_work,
+                       const unsigned long long* d_best, double F, double margin, FrontsCheck* chk, hipStream_t st) {
+    const JoinLayout L = layout(const_cast<void*>(d_work), n);
+    hipLaunchKernelGGL(join_tk_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, L.rg, L.rs, d_TG, d_TS, n,
+                       d_best, chk);
+    hipLaunchKernelGGL(fronts_caps_kernel, dim3(1), dim3(64), 0, st, d_best, F, margin, chk);
+    return hipGetLastError();
+}
+
+hipError_t fronts_clean(double* d_T, int64_t n, FrontsCheck* chk, hipStream_t st) {
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(kPassBlocks, (2 * n + 255) / 256));
+    hipLaunchKernelGGL(cap_clean_kernel, dim3(grid), dim3(256), 0, st, d_T, n, chk);
     return hipGetLastError();
 }
 

@@ -38,6 +38,10 @@ struct Fim2dArgs {
     unsigned long long qtimeout;  // spin limit, s_memrealtime ticks (100 MHz)
     unsigned long long qbudget;   // tile-visit cap (negative costs never converge)
     int max_passes;        // in-place sweep passes per persistent visit (EIK_OPT_PASSES)
+    // bidirectional fronts (eikonal_api.cpp solve_fronts): per map, an edge value above tcap[map]
+    // activates no neighbour -- every cell whose converged T is <= tcap depends only on cells below
+    // it, so it still converges exactly; nullptr: no cap
+    const double* tcap;
     // layered solver (fim2dl.hip): cell (y, x) holds ls consecutive values, layers z0.. solved
     int64_t ls;            // layer stride (1 for the 2D solver)
     int z0;                // first solved layer
@@ -202,5 +206,32 @@ hipError_t arm_obst_map(const double* Zs, const double* obst, int64_t m, int64_t
                         double resZ, int64_t sX, int64_t sY, int64_t sZ, double xm, double ym, double* fmap,
                         double* omap, double* gmap, unsigned* bad, hipStream_t st);
 hipError_t arm_tunnel(const ArmArgs& a, hipStream_t st);
+
+// ---- biComputeTmap's join (bidir.hip) -------------------------------------------------------
+// nodeJoin from two full fields (d_best: the packed join, ~0 = the fronts never meet); one host
+// synchronisation; members (optional, host): the cells ranked per front
+hipError_t bidir_join(const double* d_TG, const double* d_TS, int64_t n, void* d_work, size_t work_bytes,
+                      unsigned long long* d_best, hipStream_t st, int64_t* members = nullptr);
+size_t bidir_join_work_bytes(int64_t n);
+// after bidir_join on the same work buffer: the two fields -> biComputeTmap's partial fields;
+// d_cost / d_viol (optional): flag a band cell of finite cost left +inf (capped fronts)
+hipError_t bidir_partial(double* d_TG, double* d_TS, int64_t H, int64_t W, const void* d_work,
+                         const unsigned long long* d_best, hipStream_t st, const double* d_cost = nullptr,
+                         unsigned* d_viol = nullptr);
+// the capped fronts' device block (eikonal_api.cpp solve_fronts)
+struct FrontsCheck {
+    double caps[2];                   // per front: activation cap of the full-resolution solve
+    double tk[2];                     // coarse fields: T at the meeting rank
+    unsigned long long maxcost_bits;  // largest finite cost of the raster (double bits)
+    unsigned kept[2];                 // cells at or below the cap per front
+    unsigned viol;                    // a band cell was cut off by the cap
+    unsigned pad;
+    unsigned long long best_c;        // the coarse join
+};
+hipError_t fronts_coarse_cost(const double* d_cost, int64_t H, int64_t W, int F, double* d_out, int64_t Hc, int64_t Wc,
+                              FrontsCheck* chk, hipStream_t st);
+hipError_t fronts_caps(const double* d_TG, const double* d_TS, int64_t n, const void* d_work,
+                       const unsigned long long* d_best, double F, double margin, FrontsCheck* chk, hipStream_t st);
+hipError_t fronts_clean(double* d_T, int64_t n, FrontsCheck* chk, hipStream_t st);
 
 }  // namespace eik

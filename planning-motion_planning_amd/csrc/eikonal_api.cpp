@@ -21,15 +21,6 @@
 #include "eik_common.hpp"
 #include "eik_kernels.hpp"
 
-namespace eik {
-hipError_t bidir_join(const double* d_TG, const double* d_TS, int64_t n, void* d_work, size_t work_bytes,
-                      unsigned long long* d_best, hipStream_t st, int64_t* members = nullptr);
-size_t bidir_join_work_bytes(int64_t n);
-// after bidir_join on the same work buffer: the two fields -> biComputeTmap's partial fields
-hipError_t bidir_partial(double* d_TG, double* d_TS, int64_t H, int64_t W, const void* d_work,
-                         const unsigned long long* d_best, hipStream_t st);
-}  // namespace eik
-
 using namespace eik;
 
 namespace {
@@ -151,6 +142,10 @@ struct eik_ctx {
     eik_fim2d* cached_l = nullptr;  // queue state of the layered 3D solver (fim2dl.hip), fp32 tiles
     eik_fim2d* cached_l64 = nullptr;  // the same for the fp64 layered solver's 40-row tiles
     eik_fim2d* cached_fill = nullptr;  // reachability solver of the cost builder's hole filling
+    eik_fim2d* cached_fronts = nullptr;  // coarse B = 2 solver of the capped bidirectional fronts
+    int fronts_cap = 1;                // EIK_OPT_FRONTS_CAP
+    DevBuf fronts;                     // capped fronts: coarse cost (2 maps) | coarse T (2 maps) | FrontsCheck
+    int64_t fronts_info[6] = {};       // eik_fronts_info: capped, fallback, kept G / S, members G / S
     DevBuf cm_u8, cm_i32, cm_f32, cm_f64;  // cost-builder scratch
     DevBuf arm;                            // end-effector volume scratch (arm.hip)
     int resident_l[2][5] = {};  // co-resident workgroups of fim2dl_persist_kernel<R, nl> (f32, f64)
@@ -329,6 +324,7 @@ void eik_destroy(eik_ctx* c) {
     if (c->cached_l) eik_fim2d_destroy(c->cached_l);
     if (c->cached_l64) eik_fim2d_destroy(c->cached_l64);
     if (c->cached_fill) eik_fim2d_destroy(c->cached_fill);
+    if (c->cached_fronts) eik_fim2d_destroy(c->cached_fronts);
     if (c->h3) (void)hipHostFree(c->h3);
     if (c->h_q3) (void)hipHostFree(c->h_q3);
     for (hipEvent_t e : c->e3)
@@ -366,6 +362,7 @@ int eik_set_option(eik_ctx* c, int opt, double v) {
         case EIK_OPT_FRESH_FIRST: c->fresh_first = v != 0; break;
         case EIK_OPT_SCHED: c->sched = std::max(0, std::min(3, (int)v)); break;
         case EIK_OPT_PATH_LOOP: c->path_loop = std::max(0, std::min(2, (int)v)); break;
+        case EIK_OPT_FRONTS_CAP: c->fronts_cap = v != 0; break;
         default: return set_err(c, EIK_ERR_ARG, "unknown option %d", opt);
     }
     return EIK_OK;
@@ -1008,14 +1005,98 @@ int eik_tmap2d_batch_f32(eik_ctx* c, const float* cost, int64_t B, int64_t H, in
 // dT[n:2n] (start front), in place; *best = the packed join (~0: the fronts never meet).  Ends
 // with the stream synchronised on *best.
 static int join_and_partial(eik_ctx* c, double* dT, int64_t n, int64_t H, int64_t W, unsigned long long* best,
-                            int64_t members[2]) {
+                            int64_t members[2], const double* d_cost = nullptr, FrontsCheck* d_chk = nullptr,
+                            FrontsCheck* h_chk = nullptr) {
     hipStream_t st = c->stream;
     HIPCHK(c, c->work.ensure(bidir_join_work_bytes(n)));
     HIPCHK(c, c->misc.ensure(64));
     HIPCHK(c, bidir_join(dT, dT + n, n, c->work.p, c->work.bytes, (unsigned long long*)c->misc.p, st, members));
-    HIPCHK(c, bidir_partial(dT, dT + n, H, W, c->work.p, (const unsigned long long*)c->misc.p, st));
+    HIPCHK(c, bidir_partial(dT, dT + n, H, W, c->work.p, (const unsigned long long*)c->misc.p, st, d_cost,
+                            d_chk ? &d_chk->viol : nullptr));
     HIPCHK(c, hipMemcpyAsync(best, c->misc.p, sizeof *best, hipMemcpyDeviceToHost, st));
+    if (d_chk) HIPCHK(c, hipMemcpyAsync(h_chk, d_chk, sizeof *h_chk, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));
+    return EIK_OK;
+}
+
+// Capped fronts: rasters of at least kFrontsCapCells cells, F x F coarse blocks with F =
+// max(4, ceil(max(H, W) / 512)), cap = F x (coarse T at the meeting rank) x kFrontsMargin + the
+// largest finite cost
+constexpr int64_t kFrontsCapCells = 1 << 20;
+constexpr double kFrontsMargin = 1.25;
+
+// biComputeTmap's two fronts (FastMarching.py:114-162) as one B = 2 batch -- map 0 from the goal
+// (g[0], g[1]), map 1 from the start (g[2], g[3]) -- over the device cost dcost (both maps), into
+// dT, then nodeJoin (*best) and the partial fields.  The fronts only matter up to their meeting,
+// so by default (EIK_OPT_FRONTS_CAP) each is solved only up to a cap on T estimated from a coarse
+// copy of the raster (bidir.hip "capped fronts"); a capped result that cannot be shown equal to
+// the full one (meeting rank at or above a front's kept cells, a band cell cut off, no meeting)
+// is replaced by the uncapped solve.
+static int solve_fronts(eik_ctx* c, eik_fim2d* f, double* dcost, double* dT, const int64_t g[4], int64_t H, int64_t W,
+                        unsigned long long* best) {
+    hipStream_t st = c->stream;
+    const int64_t n = H * W;
+    for (int64_t& v : c->fronts_info) v = 0;
+    HIPCHK(c, c->work.ensure(bidir_join_work_bytes(n)));
+    const bool capped = c->fronts_cap && n >= kFrontsCapCells && std::min(H, W) >= 256;
+    if (capped) {
+        const int64_t F = std::max<int64_t>(4, (std::max(H, W) + 511) / 512);
+        const int64_t Hc = (H + F - 1) / F, Wc = (W + F - 1) / F, nc = Hc * Wc;
+        const size_t cb = sizeof(double) * 2 * nc;
+        HIPCHK(c, c->fronts.ensure(2 * cb + 256));
+        double* ccost = (double*)c->fronts.p;
+        double* cT = ccost + 2 * nc;
+        FrontsCheck* chk = (FrontsCheck*)((char*)c->fronts.p + 2 * cb);
+        HIPCHK(c, fronts_coarse_cost(dcost, H, W, (int)F, ccost, Hc, Wc, chk, st));
+        HIPCHK(c, hipMemcpyAsync(ccost + nc, ccost, sizeof(double) * nc, hipMemcpyDeviceToDevice, st));
+        eik_fim2d* fc = c->cached_fronts;
+        if (!fc || fc->H != Hc || fc->W != Wc) {
+            if (fc) eik_fim2d_destroy(fc);
+            c->cached_fronts = nullptr;
+            int rc = eik_fim2d_create(c, 2, Hc, Wc, EIK_F64, &fc);
+            if (rc) return rc;
+            c->cached_fronts = fc;
+        }
+        const int64_t gc[4] = {g[0] / F, g[1] / F, g[2] / F, g[3] / F};
+        const eik_stats keep = c->last;  // the coarse estimate's solve is not the caller's
+        int rc = eik_fim2d_solve(fc, ccost, cT, gc, st);
+        c->last = keep;
+        if (rc) return rc;
+        HIPCHK(c, bidir_join(cT, cT + nc, nc, c->work.p, c->work.bytes, &chk->best_c, st));
+        HIPCHK(c, fronts_caps(cT, cT + nc, nc, c->work.p, &chk->best_c, (double)F, kFrontsMargin, chk, st));
+        f->a.tcap = chk->caps;
+        rc = eik_fim2d_solve(f, dcost, dT, g, st);
+        f->a.tcap = nullptr;
+        if (rc) return rc;
+        HIPCHK(c, fronts_clean(dT, n, chk, st));
+        FrontsCheck h{};
+        int64_t mem[2] = {0, 0};
+        rc = join_and_partial(c, dT, n, H, W, best, mem, dcost, chk, &h);
+        if (rc) return rc;
+        const unsigned long long k = *best >> 30;
+        const bool ok = *best != ~0ull && h.viol == 0 && k < h.kept[0] && k < h.kept[1];
+        c->fronts_info[0] = std::isfinite(h.caps[0]) || std::isfinite(h.caps[1]);
+        c->fronts_info[2] = h.kept[0];
+        c->fronts_info[3] = h.kept[1];
+        c->fronts_info[4] = mem[0];
+        c->fronts_info[5] = mem[1];
+        if (ok || !c->fronts_info[0]) return EIK_OK;  // (no finite cap: that was the full solve)
+        c->fronts_info[1] = 1;  // the capped fronts did not settle the join: solve them in full
+    }
+    int rc = eik_fim2d_solve(f, dcost, dT, g, st);
+    if (rc) return rc;
+    int64_t mem[2] = {0, 0};
+    rc = join_and_partial(c, dT, n, H, W, best, mem);
+    if (!capped) {
+        c->fronts_info[4] = mem[0];
+        c->fronts_info[5] = mem[1];
+    }
+    return rc;
+}
+
+int eik_fronts_info(const eik_ctx* c, int64_t out[6]) {
+    if (!c || !out) return EIK_ERR_ARG;
+    for (int i = 0; i < 6; ++i) out[i] = c->fronts_info[i];
     return EIK_OK;
 }
 
@@ -1043,12 +1124,10 @@ int eik_tmap2d_bidir_f64(eik_ctx* c, const double* cost, int64_t H, int64_t W, i
     rc = check_cost(c, cost, dcost, n, c->stream);
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(dcost + n, dcost, sizeof(double) * n, hipMemcpyDeviceToDevice, c->stream));
-    rc = eik_fim2d_solve(f, dcost, c->T.p, goals, c->stream);
-    if (rc) return rc;
-    // join from the device-resident fields (c->T holds both maps back to back), then the fronts'
-    // partial fields at the meeting iteration (FastMarching.py:141-162)
+    // the fronts (c->T holds both maps back to back), nodeJoin and the partial fields at the
+    // meeting iteration (FastMarching.py:141-162)
     unsigned long long best = 0;
-    rc = join_and_partial(c, (double*)c->T.p, n, H, W, &best, nullptr);
+    rc = solve_fronts(c, f, dcost, (double*)c->T.p, goals, H, W, &best);
     if (rc) return rc;
     HIPCHK(c, dev_to_host(c, TG, c->T.p, sizeof(double) * n, c->stream));
     HIPCHK(c, dev_to_host(c, TS, (double*)c->T.p + n, sizeof(double) * n, c->stream));
@@ -1733,10 +1812,8 @@ int eik_rover_path_f64(eik_ctx* c, const double* Z, int64_t H, int64_t W, const 
     eik_fim2d* f = nullptr;
     rc = get_solver(c, 2, H, W, EIK_F64, &f);
     if (rc) return rc;
-    rc = eik_fim2d_solve(f, dcost, dT, g, st);
-    if (rc) return rc;
     unsigned long long best = 0;
-    rc = join_and_partial(c, dT, n, H, W, &best, nullptr);  // :141-162
+    rc = solve_fronts(c, f, dcost, dT, g, H, W, &best);  // :114-162
     if (rc) return rc;
     if (best == ~0ull) return set_err(c, EIK_ERR_UNREACHABLE, "the rover cannot reach the sample");
     const int64_t node = (int64_t)(best & ((1ull << 29) - 1));

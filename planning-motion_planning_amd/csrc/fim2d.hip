@@ -272,6 +272,7 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
     const TMem<R, COH> T(static_cast<R*>(a.T) + (int64_t)map * a.H * a.W, a.H * a.W);
     const int64_t y0 = (int64_t)ty * kTile, x0 = (int64_t)tx * kTile;
     const bool full = (y0 + kTile <= a.H) && (x0 + kTile <= a.W) && ((a.W & 3) == 0);
+    const R capv = a.tcap ? (R)a.tcap[map] : INF;  // edge values above it activate no neighbour
 
     EIK_PROBE(0);
     if (tid == 0) {
@@ -461,11 +462,13 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
                     kmin_self = umin(kmin_self, nv[e]);
                     // A neighbour can only improve if this edge value undercuts the neighbour's
                     // adjacent cell (the halo value, stale => larger => conservative).
+                    // (a.tcap: an edge value above the map's cap activates nobody)
                     const int lx = cx + e + 1, ly = ry + 1;
-                    if (ry == 0 && nv[e] < cell_t(Ts, lx, lx)) { fl |= 1u; kmin[0] = umin(kmin[0], nv[e]); }
-                    if (ry == kTile - 1 && nv[e] < cell_t(Ts, (kLds - 1) * kLds + lx, lx)) { fl |= 2u; kmin[1] = umin(kmin[1], nv[e]); }
-                    if (cx + e == 0 && nv[e] < cell_t(Ts, ly * kLds, 0)) { fl |= 4u; kmin[2] = umin(kmin[2], nv[e]); }
-                    if (cx + e == kTile - 1 && nv[e] < cell_t(Ts, ly * kLds + kLds - 1, kLds - 1)) { fl |= 8u; kmin[3] = umin(kmin[3], nv[e]); }
+                    const bool act = nv[e] <= capv;
+                    if (act && ry == 0 && nv[e] < cell_t(Ts, lx, lx)) { fl |= 1u; kmin[0] = umin(kmin[0], nv[e]); }
+                    if (act && ry == kTile - 1 && nv[e] < cell_t(Ts, (kLds - 1) * kLds + lx, lx)) { fl |= 2u; kmin[1] = umin(kmin[1], nv[e]); }
+                    if (act && cx + e == 0 && nv[e] < cell_t(Ts, ly * kLds, 0)) { fl |= 4u; kmin[2] = umin(kmin[2], nv[e]); }
+                    if (act && cx + e == kTile - 1 && nv[e] < cell_t(Ts, ly * kLds + kLds - 1, kLds - 1)) { fl |= 8u; kmin[3] = umin(kmin[3], nv[e]); }
                     const int64_t gx = x0 + cx + e;  // subdomain edges inside a partial tile (DD)
                     if (gy == a.H - 1 && ry != kTile - 1) fl |= 32u;
                     if (gx == a.W - 1 && cx + e != kTile - 1) fl |= 64u;

@@ -153,3 +153,66 @@ def test_join_members_bounded_on_terrain(ctx):
     rgp, rsp, rjoin, k = join_oracle(TG, TS)
     assert np.array_equal(join, rjoin) and np.array_equal(gp, rgp) and np.array_equal(sp, rsp)
     assert members.max() <= 0.5 * H * W, members
+
+
+# ---- capped fronts (eikonal_api.cpp solve_fronts): biComputeTmap on rasters of >= 2^20 cells
+# solves each front only up to a cap estimated on a coarse copy; the result must be the full
+# fronts' (the FIM is not bit-deterministic between two schedules: fields within 1e-9, and the
+# join and masks equal)
+def _raster(kind, rng):
+    H = W = 1024
+    cost = rng.uniform(1, 4, (H, W))
+    if kind == "wall_gap":  # a one-cell wall with a 3-cell gap: invisible to the 4 x 4 coarse blocks
+        cost[:, 500] = np.inf
+        cost[700:703, 500] = 1.0
+    elif kind == "obstacles":
+        cost[rng.random((H, W)) < 0.15] = np.inf
+    elif kind == "blocky":  # large impassable blocks and a high-cost band
+        cost[200:800, 300:340] = np.inf
+        cost[100:900, 600:620] = 300.0
+    cost[0, :] = cost[-1, :] = cost[:, 0] = cost[:, -1] = np.inf
+    return cost
+
+
+FRONT_CASES = [("uniform_far", (900, 880), (60, 50)), ("uniform_near", (520, 500), (480, 530)),
+               ("wall_gap", (900, 100), (100, 900)), ("obstacles", (800, 700), (150, 200)),
+               ("blocky", (950, 500), (50, 500)), ("same_node", (400, 400), (400, 400))]
+
+
+@pytest.fixture(scope="module")
+def ctx_full():
+    import eikonal
+
+    c = eikonal.Context(0, options="FRONTS_CAP=0")
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("kind,goal,start", FRONT_CASES, ids=[c[0] for c in FRONT_CASES])
+def test_capped_fronts_equal_full_fronts(ctx, ctx_full, kind, goal, start):
+    rng = np.random.default_rng(100 + [c[0] for c in FRONT_CASES].index(kind))
+    cost = _raster(kind.split("_")[0] if kind.startswith("uniform") else kind, rng)
+    if kind == "obstacles":
+        cost[goal[1], goal[0]] = cost[start[1], start[0]] = 1.0
+    TG, TS, join = ctx.tmap2d_bidir(cost, goal, start)
+    info = ctx.fronts_info()
+    FG, FS, fjoin = ctx_full.tmap2d_bidir(cost, goal, start)
+    assert not ctx_full.fronts_info()["capped"]
+    assert np.array_equal(join, fjoin), (kind, join, fjoin, info)
+    for a, b in ((TG, FG), (TS, FS)):
+        assert np.array_equal(np.isfinite(a), np.isfinite(b)), (kind, info)
+        f = np.isfinite(a)
+        assert np.abs(a[f] - b[f]).max() <= 1e-9, kind
+    print(f"{kind}: {info}, finite cells {int(np.isfinite(TG).sum())} / {int(np.isfinite(TS).sum())}")
+    if kind in ("uniform_far", "uniform_near", "same_node"):
+        assert info["capped"] and not info["fallback"], info
+        assert max(info["kept"]) < cost.size, info
+
+
+def test_capped_fronts_disconnected(ctx):
+    import eikonal
+
+    cost = np.ones((1024, 1024))
+    cost[:, 512] = np.inf
+    with pytest.raises(eikonal.EikError):
+        ctx.tmap2d_bidir(cost, (100, 100), (900, 900))

@@ -9,6 +9,8 @@ timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method threa
   > $O/r04h_tests.log 2>&1 || { echo "tests rc=$?"; tail -n 40 $O/r04h_tests.log; exit 1; }
 tail -n 1 $O/r04h_tests.log
 grep "k\* " $O/r04h_tests.log || true
+OPTS_LIST="FRONTS_CAP=1,FRONTS_CAP=0,FRONTS_CAP=1,FRONTS_CAP=0" timeout -k 10 300 python3 tools/rover_probe.py > $O/r04h_rover_ab.log 2>&1 || { echo "rover ab rc=$?"; tail -n 20 $O/r04h_rover_ab.log; exit 1; }
+grep -E "^FRONTS|bidir batch|single front" $O/r04h_rover_ab.log
 OPTS_LIST="," timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/r04h_prof -o rover -- python3 tools/rover_probe.py > $O/r04h_rover.log 2>&1 || { echo "rover rc=$?"; tail -n 20 $O/r04h_rover.log; exit 1; }
 cat $O/r04h_rover.log | grep -v "^W\|warn" | tail -n 12
 f=$(find $O/r04h_prof -name "*kernel_stats.csv" | head -1); cp "$f" $O/r04h_rover_kernel_stats.csv
@@ -23,6 +25,6 @@ PY
 for i in 1 2 3; do
   for d in lib lib_v1; do
     EIKONAL_LIB=planning-motion_planning_amd/$d/libeikonal.so timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra --steps 3 --warmup 1 > $O/r04g_$d.json 2> $O/r04g.err || { echo "bench $d rc=$?"; tail -n 20 $O/r04g.err; exit 1; }
-    python -c "import json,sys; d=json.load(open('$O/r04g_$d.json')); print('%-7s path %.3f ms  %.4f us/step  %d points  ms_to_path %.2f (torch %.2f)' % ('$d', d['path_kernel_ms'], d['path_us_per_step'], d['path_points'], d['ms_to_path'], d['ms_to_path_torch']))"
+    python -c "import json,sys; d=json.load(open('$O/r04g_$d.json')); print('%-7s C2 %.3f ms  path %.3f ms  %.4f us/step  %d points  ms_to_path %.2f (torch %.2f)' % ('$d', d['ms_per_step'], d['path_kernel_ms'], d['path_us_per_step'], d['path_points'], d['ms_to_path'], d['ms_to_path_torch']))"
   done
 done

@@ -22,7 +22,8 @@ for opts in os.environ.get("OPTS_LIST", ",PASSES=8,PASSES=24,,PASSES=8,PASSES=24
         t0 = time.perf_counter()
         r = ctx.rover_path(Zc, q)
         ts.append((time.perf_counter() - t0) * 1e3)
-    print(f"{opts or 'default'}: {np.median(ts):.2f} ms, waypoints {len(r[0])}, join {list(r[2])}", flush=True)
+    print(f"{opts or 'default'}: {np.median(ts):.2f} ms, waypoints {len(r[0])}, join {list(r[2])}, "
+          f"fronts {ctx.fronts_info()}", flush=True)
     ctx.close()
 # the two fronts alone on the planner's own cost raster (host entry, one B = 2 batch), and each
 # front as a single-map solve, with the solver stats
@@ -38,7 +39,7 @@ for rep in range(3):
     ctx.tmap2d_bidir(cc, (gx, gy), (sx, sy))
     s = ctx.stats()
     print(f"bidir batch: wall {(time.perf_counter() - t0) * 1e3:.2f} ms, solve {s['solve_ms']:.2f} ms, visits "
-          f"{s['tile_visits']}, in-place {s['inplace_passes']}", flush=True)
+          f"{s['tile_visits']}, in-place {s['inplace_passes']}, fronts {ctx.fronts_info()}", flush=True)
 dc = torch.from_numpy(cost).to(dev)
 T = torch.empty_like(dc)
 f1 = eikonal.Fim2d(ctx, 1, N, N, L.EIK_F64)
