@@ -97,8 +97,9 @@ typedef enum {
                                 the reference's statement order.  Same path bits in all three.  */
     EIK_OPT_FRONTS_CAP = 13  /* biComputeTmap / rover path, rasters >= 2^20 cells: 1 (default) solves
                                 each front only up to a cap on T estimated from a coarse copy of
-                                the raster and falls back to the full solve when the capped fields
-                                cannot be shown to give the full fields' join; 0 = full fronts    */
+                                the raster (x 1.25) and falls back to the full solve when the
+                                capped fields cannot be shown to give the full fields' join; a
+                                value v > 1: the same with margin v; 0 = full fronts            */
 } eik_option;
 
 typedef enum { EIK_MODE_LIST = 0, EIK_MODE_PERSISTENT = 1 } eik_mode;

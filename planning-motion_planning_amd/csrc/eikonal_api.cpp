@@ -119,6 +119,8 @@ class CopyPool {
 
 }  // namespace
 
+constexpr double kFrontsMargin = 1.25;  // capped bidirectional fronts (solve_fronts)
+
 struct eik_ctx {
     int device = 0;
     int cu_count = 256;
@@ -143,7 +145,7 @@ struct eik_ctx {
     eik_fim2d* cached_l64 = nullptr;  // the same for the fp64 layered solver's 40-row tiles
     eik_fim2d* cached_fill = nullptr;  // reachability solver of the cost builder's hole filling
     eik_fim2d* cached_fronts = nullptr;  // coarse B = 2 solver of the capped bidirectional fronts
-    int fronts_cap = 1;                // EIK_OPT_FRONTS_CAP
+    double fronts_cap = 1.25;          // EIK_OPT_FRONTS_CAP: cap margin (0: full fronts)
     DevBuf fronts;                     // capped fronts: coarse cost (2 maps) | coarse T (2 maps) | FrontsCheck
     int64_t fronts_info[6] = {};       // eik_fronts_info: capped, fallback, kept G / S, members G / S
     DevBuf cm_u8, cm_i32, cm_f32, cm_f64;  // cost-builder scratch
@@ -362,7 +364,7 @@ int eik_set_option(eik_ctx* c, int opt, double v) {
         case EIK_OPT_FRESH_FIRST: c->fresh_first = v != 0; break;
         case EIK_OPT_SCHED: c->sched = std::max(0, std::min(3, (int)v)); break;
         case EIK_OPT_PATH_LOOP: c->path_loop = std::max(0, std::min(2, (int)v)); break;
-        case EIK_OPT_FRONTS_CAP: c->fronts_cap = v != 0; break;
+        case EIK_OPT_FRONTS_CAP: c->fronts_cap = v <= 0 ? 0.0 : v == 1 ? kFrontsMargin : std::max(1.0, v); break;
         default: return set_err(c, EIK_ERR_ARG, "unknown option %d", opt);
     }
     return EIK_OK;
@@ -1020,10 +1022,9 @@ static int join_and_partial(eik_ctx* c, double* dT, int64_t n, int64_t H, int64_
 }
 
 // Capped fronts: rasters of at least kFrontsCapCells cells, F x F coarse blocks with F =
-// max(4, ceil(max(H, W) / 512)), cap = F x (coarse T at the meeting rank) x kFrontsMargin + the
-// largest finite cost
+// max(4, ceil(max(H, W) / 512)), cap = F x (coarse T at the meeting rank) x margin (kFrontsMargin,
+// EIK_OPT_FRONTS_CAP) + the largest finite cost
 constexpr int64_t kFrontsCapCells = 1 << 20;
-constexpr double kFrontsMargin = 1.25;
 
 // biComputeTmap's two fronts (FastMarching.py:114-162) as one B = 2 batch -- map 0 from the goal
 // (g[0], g[1]), map 1 from the start (g[2], g[3]) -- over the device cost dcost (both maps), into
@@ -1038,7 +1039,7 @@ static int solve_fronts(eik_ctx* c, eik_fim2d* f, double* dcost, double* dT, con
     const int64_t n = H * W;
     for (int64_t& v : c->fronts_info) v = 0;
     HIPCHK(c, c->work.ensure(bidir_join_work_bytes(n)));
-    const bool capped = c->fronts_cap && n >= kFrontsCapCells && std::min(H, W) >= 256;
+    const bool capped = c->fronts_cap > 0 && n >= kFrontsCapCells && std::min(H, W) >= 256;
     if (capped) {
         const int64_t F = std::max<int64_t>(4, (std::max(H, W) + 511) / 512);
         const int64_t Hc = (H + F - 1) / F, Wc = (W + F - 1) / F, nc = Hc * Wc;
@@ -1063,7 +1064,7 @@ static int solve_fronts(eik_ctx* c, eik_fim2d* f, double* dcost, double* dT, con
         c->last = keep;
         if (rc) return rc;
         HIPCHK(c, bidir_join(cT, cT + nc, nc, c->work.p, c->work.bytes, &chk->best_c, st));
-        HIPCHK(c, fronts_caps(cT, cT + nc, nc, c->work.p, &chk->best_c, (double)F, kFrontsMargin, chk, st));
+        HIPCHK(c, fronts_caps(cT, cT + nc, nc, c->work.p, &chk->best_c, (double)F, c->fronts_cap, chk, st));
         f->a.tcap = chk->caps;
         rc = eik_fim2d_solve(f, dcost, dT, g, st);
         f->a.tcap = nullptr;

@@ -66,6 +66,12 @@ __device__ __forceinline__ R stage_cost(R c) {
 #endif
 constexpr int kActStep = EIK_ACT_STEP;
 
+// EIK_TCAP (default on): Fim2dArgs::tcap, the capped bidirectional fronts' activation cap
+// (eikonal_api.cpp solve_fronts).  0 compiles the check out (A/B of its cost on the uncapped solves).
+#ifndef EIK_TCAP
+#define EIK_TCAP 1
+#endif
+
 // (EIK_LAZY_CLAIM, round 4: a grabbed tile claimed -- PENDING -> BUSY -- at its first pass boundary
 // instead of before its staging, taking the grab's exchange round trip off the front's hop; the
 // first boundary then has to reload the halo to tell new activations from the served ones.
@@ -272,7 +278,7 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
     const TMem<R, COH> T(static_cast<R*>(a.T) + (int64_t)map * a.H * a.W, a.H * a.W);
     const int64_t y0 = (int64_t)ty * kTile, x0 = (int64_t)tx * kTile;
     const bool full = (y0 + kTile <= a.H) && (x0 + kTile <= a.W) && ((a.W & 3) == 0);
-    const R capv = a.tcap ? (R)a.tcap[map] : INF;  // edge values above it activate no neighbour
+    const R capv = EIK_TCAP && a.tcap ? (R)a.tcap[map] : INF;  // edge values above it activate no neighbour
 
     EIK_PROBE(0);
     if (tid == 0) {
@@ -464,7 +470,7 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
                     // adjacent cell (the halo value, stale => larger => conservative).
                     // (a.tcap: an edge value above the map's cap activates nobody)
                     const int lx = cx + e + 1, ly = ry + 1;
-                    const bool act = nv[e] <= capv;
+                    const bool act = !EIK_TCAP || nv[e] <= capv;
                     if (act && ry == 0 && nv[e] < cell_t(Ts, lx, lx)) { fl |= 1u; kmin[0] = umin(kmin[0], nv[e]); }
                     if (act && ry == kTile - 1 && nv[e] < cell_t(Ts, (kLds - 1) * kLds + lx, lx)) { fl |= 2u; kmin[1] = umin(kmin[1], nv[e]); }
                     if (act && cx + e == 0 && nv[e] < cell_t(Ts, ly * kLds, 0)) { fl |= 4u; kmin[2] = umin(kmin[2], nv[e]); }

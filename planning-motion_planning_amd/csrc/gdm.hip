@@ -157,12 +157,11 @@ enum { kGdmDone = 0, kGdmFallback = 1, kGdmError = 2 };
 // earlier: the path is bit-identical to the single-lane form.
 constexpr int kPW = 64;                          // window side (nodes), one builder lane per column
 constexpr int kPathThreads = 1024;               // 16 waves: walker + 15 builders
-// EIK_PATH_SIMD0_FREE: the waves that share the walker's SIMD (4, 8, 12: waves are dealt to the
-// CU's four SIMDs in turn) do not build, so builds never take the walker's issue slots
-#ifndef EIK_PATH_SIMD0_FREE
-#define EIK_PATH_SIMD0_FREE 0
-#endif
-constexpr int kBuilders = EIK_PATH_SIMD0_FREE ? kPathThreads / 64 - 4 : kPathThreads / 64 - 1;
+// (Round 4, measured and removed: EIK_PATH_SIMD0_FREE -- the waves sharing the walker's SIMD (4, 8,
+// 12) did not build, so builds never took the walker's issue slots.  Walk 2.512-2.532 ms against
+// 2.513-2.527 ms, 0.406-0.410 us/step both (profiles/r04g_walker_simd0_ab.log): the walker's step
+// is its own dependent f64 chain, not issue-bound.)
+constexpr int kBuilders = kPathThreads / 64 - 1;
 constexpr int kRowsPerBuilder = (kPW + kBuilders - 1) / kBuilders;
 constexpr int kPrefetch = 16;                    // nodes from an inner edge that trigger a prefetch
 constexpr unsigned long long kPathSpin = 200000000ull;  // 2 s of s_memrealtime (100 MHz): never hang
@@ -229,8 +228,7 @@ __device__ void build_window(PathLds& s, const R* __restrict__ T, int64_t H, int
 template <typename R>
 __device__ void path_builder(PathLds& s, const R* __restrict__ T, int64_t H, int64_t W) {
     const int wv = (int)(threadIdx.x >> 6);
-    if (EIK_PATH_SIMD0_FREE && (wv & 3) == 0) return;  // the walker's SIMD partners stay idle
-    const int w = EIK_PATH_SIMD0_FREE ? wv - 1 - (wv >> 2) : wv - 1;  // builder index 0 .. kBuilders - 1
+    const int w = wv - 1;  // builder index 0 .. kBuilders - 1
     int seen = 0;
     unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
