@@ -40,7 +40,7 @@ struct Fim2dArgs {
     int max_passes;        // in-place sweep passes per persistent visit (EIK_OPT_PASSES)
     // bidirectional fronts (eikonal_api.cpp solve_fronts): per map, an edge value above tcap[map]
     // activates no neighbour -- every cell whose converged T is <= tcap depends only on cells below
-    // it, so it still converges exactly; nullptr: no cap
+    // it, so it still converges exactly; nullptr: no cap (honoured by the fp64 persistent kernel only)
     const double* tcap;
     // layered solver (fim2dl.hip): cell (y, x) holds ls consecutive values, layers z0.. solved
     int64_t ls;            // layer stride (1 for the 2D solver)

@@ -66,12 +66,6 @@ __device__ __forceinline__ R stage_cost(R c) {
 #endif
 constexpr int kActStep = EIK_ACT_STEP;
 
-// EIK_TCAP (default on): Fim2dArgs::tcap, the capped bidirectional fronts' activation cap
-// (eikonal_api.cpp solve_fronts).  0 compiles the check out (A/B of its cost on the uncapped solves).
-#ifndef EIK_TCAP
-#define EIK_TCAP 1
-#endif
-
 // (EIK_LAZY_CLAIM, round 4: a grabbed tile claimed -- PENDING -> BUSY -- at its first pass boundary
 // instead of before its staging, taking the grab's exchange round trip off the front's hop; the
 // first boundary then has to reload the halo to tell new activations from the served ones.
@@ -266,7 +260,10 @@ struct TileLds {
 // The caller sets L.dirs (quadrant sweeps to run) before the barrier that precedes the call.
 // Ends with a workgroup barrier; in COH mode every wave has drained its write-through stores
 // before it.
-template <typename R, bool COH>
+// CAP: honour Fim2dArgs::tcap (the capped bidirectional fronts, eikonal_api.cpp solve_fronts) -- a
+// separate instantiation: the compare in the edge test cost the uncapped fp64 solve 4-5 % (C2 2.36
+// -> 2.47 ms, profiles/r04i_tcap_ab.log)
+template <typename R, bool COH, bool CAP = false>
 __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileLds<R>& L, R keep) {
     constexpr R INF = Real<R>::inf();
     Cell<R>* const Ts = L.Tc + kGuard * kLds;
@@ -278,7 +275,7 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
     const TMem<R, COH> T(static_cast<R*>(a.T) + (int64_t)map * a.H * a.W, a.H * a.W);
     const int64_t y0 = (int64_t)ty * kTile, x0 = (int64_t)tx * kTile;
     const bool full = (y0 + kTile <= a.H) && (x0 + kTile <= a.W) && ((a.W & 3) == 0);
-    const R capv = EIK_TCAP && a.tcap ? (R)a.tcap[map] : INF;  // edge values above it activate no neighbour
+    const R capv = CAP ? (R)a.tcap[map] : INF;  // edge values above it activate no neighbour
 
     EIK_PROBE(0);
     if (tid == 0) {
@@ -470,7 +467,7 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
                     // adjacent cell (the halo value, stale => larger => conservative).
                     // (a.tcap: an edge value above the map's cap activates nobody)
                     const int lx = cx + e + 1, ly = ry + 1;
-                    const bool act = !EIK_TCAP || nv[e] <= capv;
+                    const bool act = !CAP || nv[e] <= capv;
                     if (act && ry == 0 && nv[e] < cell_t(Ts, lx, lx)) { fl |= 1u; kmin[0] = umin(kmin[0], nv[e]); }
                     if (act && ry == kTile - 1 && nv[e] < cell_t(Ts, (kLds - 1) * kLds + lx, lx)) { fl |= 2u; kmin[1] = umin(kmin[1], nv[e]); }
                     if (act && cx + e == 0 && nv[e] < cell_t(Ts, ly * kLds, 0)) { fl |= 4u; kmin[2] = umin(kmin[2], nv[e]); }
@@ -721,7 +718,7 @@ __device__ void live_agent(const Fim2dArgs& a, unsigned* sh) {
 // VGPRs -> 3 workgroups per CU; 4: <= 128 VGPRs -> 4 per CU, a few spills).  Large rasters
 // (maps of >= kWideTiles tiles: the throughput-bound regime) run the 4-wave form -- 16384^2 on one GPU
 // +10-15 %, 4096^2 -3 % (profiles/r02r_wps_ab.log).
-template <typename R, int WPS>
+template <typename R, int WPS, bool CAP = false>
 __global__ __launch_bounds__(kThreads, WPS) void fim2d_persist_kernel(Fim2dArgs a) {
     __shared__ TileLds<R> L;
     if (a.live && blockIdx.x == gridDim.x - 1) {
@@ -767,7 +764,7 @@ __global__ __launch_bounds__(kThreads, WPS) void fim2d_persist_kernel(Fim2dArgs 
         EIK_PROBE(6);
         tile = __builtin_amdgcn_readfirstlane(L.tile);
         if (tile < 0) break;  // uniform: solve finished (or failed)
-        process_tile<R, true>(a, tile, L, keep);  // sc1 loads; sc1 stores drained + barrier
+        process_tile<R, true, CAP>(a, tile, L, keep);  // sc1 loads; sc1 stores drained + barrier
     }
     if (threadIdx.x == 0 && nvis) atomicAdd(a.visits, (unsigned long long)nvis);
 }
@@ -891,7 +888,11 @@ int fim2d_persist_resident(bool f64, int cus, bool wide) {
 }
 
 hipError_t fim2d_persist(const Fim2dArgs& a, bool f64, int grid, hipStream_t st, bool wide, bool rewind) {
-    if (f64)
+    // (a.tcap: fp64 only -- the fp32 kernels and list mode solve in full, which the capped fronts'
+    // clean pass and check accept as well)
+    if (f64 && a.tcap)
+        hipLaunchKernelGGL((fim2d_persist_kernel<double, 1, true>), dim3(grid), dim3(kThreads), 0, st, a);
+    else if (f64)
         hipLaunchKernelGGL((fim2d_persist_kernel<double, 1>), dim3(grid), dim3(kThreads), 0, st, a);
     else if (wide)
         hipLaunchKernelGGL((fim2d_persist_kernel<float, 4>), dim3(grid), dim3(kThreads), 0, st, a);
