@@ -174,6 +174,7 @@ struct eik_fim2d {
     Fim2dArgs a{};
     hipStream_t stream = nullptr;
     DevBuf lists, counts, mark, edge, goals, key;
+    DevBuf ecol;                         // every tile's two edge columns (Fim2dArgs::ecol)
     DevBuf qctl, qslot, qstate;          // persistent-mode FIFO
     int* h_counts = nullptr;             // pinned
     unsigned* h_q = nullptr;             // pinned copy of qctl
@@ -416,6 +417,7 @@ static int fim2d_create_rows(eik_ctx* c, int64_t B, int64_t H, int64_t W, int dt
         (e = f->counts.ensure(sizeof(int) * 64)) != hipSuccess || (e = f->mark.ensure(sizeof(unsigned) * tiles)) != hipSuccess ||
         (e = f->key.ensure(sizeof(unsigned) * tiles)) != hipSuccess ||
         (e = f->edge.ensure(sizeof(unsigned) * 4)) != hipSuccess || (e = f->goals.ensure(sizeof(int64_t) * 2 * B)) != hipSuccess ||
+        (e = f->ecol.ensure((dtype == EIK_F64 ? 8 : 4) * 2 * kTile * (size_t)tiles)) != hipSuccess ||
         (e = hipHostMalloc((void**)&f->h_counts, sizeof(int) * 64)) != hipSuccess ||
         (e = hipHostMalloc((void**)&f->h_visits, 2 * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipHostMalloc((void**)&f->h_goals, sizeof(int64_t) * 2 * B)) != hipSuccess ||
@@ -424,6 +426,7 @@ static int fim2d_create_rows(eik_ctx* c, int64_t B, int64_t H, int64_t W, int dt
         return set_err(c, EIK_ERR_NOMEM, "fim2d allocation: %s", hipGetErrorString(e));
     }
     a.lists = (int*)f->lists.p;
+    a.ecol = f->ecol.p;
     a.counts = (int*)f->counts.p;
     a.mark = (unsigned*)f->mark.p;
     a.key = (unsigned*)f->key.p;
