@@ -42,7 +42,7 @@ struct Fim2dArgs {
     // activates no neighbour -- every cell whose converged T is <= tcap depends only on cells below
     // it, so it still converges exactly; nullptr: no cap (honoured by the fp64 persistent kernel only)
     const double* tcap;
-    // every tile's west / east edge column, [tile][2][kTile] R, kept equal to T's (EIK_ECOL): the
+    // every tile's west / east edge column, [tile][2][kTile] R, kept equal to T's (fim2d.hip kEcol): the
     // west / east halo of a tile visit is one contiguous 64-cell read instead of 64 rows' lines
     void* ecol;
     // layered solver (fim2dl.hip): cell (y, x) holds ls consecutive values, layers z0.. solved

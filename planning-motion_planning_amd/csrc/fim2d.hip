@@ -85,13 +85,21 @@ constexpr int kActStep = EIK_ACT_STEP;
 // (profiles/r04c_async_wb_ab.log).  The drain is the front's hop either way -- a neighbour may be
 // activated only once the edge it reads has landed.)
 
-// EIK_ECOL: the W / E halo columns of a visit come from Fim2dArgs::ecol, a copy of every tile's two
+// EIK_ECOL_F64 / _F32 (kEcol): the W / E halo columns of a visit come from Fim2dArgs::ecol, a copy of every tile's two
 // edge columns stored beside T by the write-back (and the init / seed kernels), instead of from T:
 // a column of T spans 64 rows, i.e. 64 lines of 64-128 B for 256-512 B of data (the fp64 solve's
 // reads were 1.01 GB per launch against 0.58 GB algorithmic, profiles/r03s_pmc_traffic_f64.json).
-#ifndef EIK_ECOL
-#define EIK_ECOL 0
+// Per dtype: on in fp64 (C2 within noise, 2.36-2.44 vs 2.37-2.41 ms; PMC traffic per launch 2.94 ->
+// 2.56 GB, reads 0.88 -> 0.45 GB: profiles/r04j_ecol_ab.log), off in fp32 (C2 1.60-1.63 -> 1.65-1.66 ms:
+// the 147 -> 164 VGPRs of the one-wave kernel, profiles/r04k_ecol_f32_ab.log).
+#ifndef EIK_ECOL_F64
+#define EIK_ECOL_F64 1
 #endif
+#ifndef EIK_ECOL_F32
+#define EIK_ECOL_F32 0
+#endif
+template <typename R>
+constexpr bool kEcol = sizeof(R) == 8 ? EIK_ECOL_F64 : EIK_ECOL_F32;
 
 // ------------------------------------------------------------------------- quadrant sweep
 // A tile cell in LDS: arrival time and cost side by side, so one ds_read_b64 (fp32) fetches both.
@@ -281,7 +289,7 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
     const int ty = rem / a.ntx, tx = rem - (rem / a.ntx) * a.ntx;
     const R* __restrict__ cost = static_cast<const R*>(a.cost) + (int64_t)map * a.H * a.W;
     const TMem<R, COH> T(static_cast<R*>(a.T) + (int64_t)map * a.H * a.W, a.H * a.W);
-    // edge columns of every tile (EIK_ECOL): index (t * 2 + side) * kTile + row, side 0 west / 1 east
+    // edge columns of every tile (kEcol): index (t * 2 + side) * kTile + row, side 0 west / 1 east
     const TMem<R, COH> E(static_cast<R*>(a.ecol), (int64_t)a.capacity * 2 * kTile);
     auto eidx = [&](int t, int side, int row) { return ((int64_t)t * 2 + side) * kTile + row; };
     const int64_t y0 = (int64_t)ty * kTile, x0 = (int64_t)tx * kTile;
@@ -321,13 +329,13 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
         q.hx = k == 0 || k == 1 ? x0 + lane : k == 2 ? x0 - 1 : sx;
         q.in = q.hy >= 0 && q.hy < a.H && q.hx >= 0 && q.hx < a.W;
         q.idx = q.in ? q.hy * a.W + q.hx : 0;
-        // EIK_ECOL: the west halo is the west neighbour's east column, the east halo the east
+        // kEcol: the west halo is the west neighbour's east column, the east halo the east
         // neighbour's west column (both tiles of this map when in range)
-        if (EIK_ECOL && k >= 2 && q.in) q.idx = eidx(k == 2 ? tile - 1 : tile + 1, k == 2 ? 1 : 0, lane);
+        if (kEcol<R> && k >= 2 && q.in) q.idx = eidx(k == 2 ? tile - 1 : tile + 1, k == 2 ? 1 : 0, lane);
         return q;
     };
     auto load_halo_of = [&](const Halo& q, int k) {  // k: wave-uniform
-        R v = EIK_ECOL && k >= 2 ? E.ld(q.idx) : T.ld(q.idx);
+        R v = kEcol<R> && k >= 2 ? E.ld(q.idx) : T.ld(q.idx);
         if (!q.in) v = load_T<R, COH>(a, T, q.hy, q.hx);
         return v;
     };
@@ -505,10 +513,10 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
                         if (gy < a.H && gx < a.W && nv[e] < told[4 * k + e]) T.st(gy * a.W + gx, nv[e]);
                     }
                 }
-                // the edge columns' copies (EIK_ECOL), drained with T's stores; a cut tile's cells past
+                // the edge columns' copies (kEcol), drained with T's stores; a cut tile's cells past
                 // the raster are never read as a halo, so the copy may hold them too
-                if (EIK_ECOL && cx == 0 && nv[0] < told[4 * k]) E.st(eidx(tile, 0, ry), nv[0]);
-                if (EIK_ECOL && cx == kTile - 4 && nv[3] < told[4 * k + 3]) E.st(eidx(tile, 1, ry), nv[3]);
+                if (kEcol<R> && cx == 0 && nv[0] < told[4 * k]) E.st(eidx(tile, 0, ry), nv[0]);
+                if (kEcol<R> && cx == kTile - 4 && nv[3] < told[4 * k + 3]) E.st(eidx(tile, 1, ry), nv[3]);
             }
             if (COH) {
 #pragma unroll
@@ -832,7 +840,7 @@ __global__ void fim2d_seed_kernel(Fim2dArgs a, const int64_t* __restrict__ goals
     if (gx < 0 || gy < 0 || gx >= a.W || gy >= a.H) return;
     static_cast<R*>(a.T)[(int64_t)m * a.H * a.W + gy * a.W + gx] = R(0);
     const int tile = m * a.tiles_per_map + (int)(gy / kTile) * a.ntx + (int)(gx / kTile);
-    if (EIK_ECOL && a.ecol && (gx % kTile == 0 || gx % kTile == kTile - 1))  // the edge columns' copy
+    if (kEcol<R> && a.ecol && (gx % kTile == 0 || gx % kTile == kTile - 1))  // the edge columns' copy
         static_cast<R*>(a.ecol)[((int64_t)tile * 2 + (gx % kTile == 0 ? 0 : 1)) * kTile + gy % kTile] = R(0);
     if (a.mode == kModePersistent) {
         qpush(a, tile, kSelf);
@@ -944,12 +952,12 @@ hipError_t fim2d_init(const Fim2dArgs& a, bool f64, int nmaps, const int64_t* d_
     if (f64) {
         hipLaunchKernelGGL(fim2d_init_kernel<double>, dim3(grid), dim3(256), 0, st, static_cast<double*>(a.T), n,
                            a.mark, ntiles, a.key, a.minkey, a.qstate, a.qslot, nslots, counts, qctl, visits, edge,
-                           EIK_ECOL ? static_cast<double*>(a.ecol) : nullptr);
+                           kEcol<double> ? static_cast<double*>(a.ecol) : nullptr);
         hipLaunchKernelGGL(fim2d_seed_kernel<double>, dim3((nmaps + 255) / 256), dim3(256), 0, st, a, d_goals, nmaps);
     } else {
         hipLaunchKernelGGL(fim2d_init_kernel<float>, dim3(grid), dim3(256), 0, st, static_cast<float*>(a.T), n,
                            a.mark, ntiles, a.key, a.minkey, a.qstate, a.qslot, nslots, counts, qctl, visits, edge,
-                           EIK_ECOL ? static_cast<float*>(a.ecol) : nullptr);
+                           kEcol<float> ? static_cast<float*>(a.ecol) : nullptr);
         hipLaunchKernelGGL(fim2d_seed_kernel<float>, dim3((nmaps + 255) / 256), dim3(256), 0, st, a, d_goals, nmaps);
     }
     return hipGetLastError();
