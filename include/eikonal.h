@@ -306,6 +306,9 @@ int eik_surface_normal_f64(eik_ctx* ctx, const double* Z, int64_t H, int64_t W, 
                            double* Nz);
 /* image_filling(im) :82-94 (cv2.floodFill from (0, 0), 4-connected) on a 0/1 uint8 image */
 int eik_image_fill_u8(eik_ctx* ctx, const uint8_t* im, int64_t H, int64_t W, uint8_t* out);
+/* cv2.erode / cv2.dilate with the reference's structural_disk(radius) (Coupled_motion_planner.py:96-105,
+ * :1168-1177, :1192) on a 0/1 uint8 mask: erode != 0 -> erosion; pixels outside the image take no part. */
+int eik_disk_morph_u8(eik_ctx* ctx, const uint8_t* im, int64_t H, int64_t W, int radius, int erode, uint8_t* out);
 
 /* ---- rover path of the planner -----------------------------------
  * Coupled_motion_planner.py main(), step 1 (:1097-1258): DEM -> cost raster (eik_costmap_*) ->

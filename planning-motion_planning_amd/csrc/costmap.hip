@@ -312,37 +312,67 @@ __global__ void cm_morph_kernel(const unsigned char* __restrict__ A, const int* 
     out[i] = erode ? (unsigned char)(A[i] && D[i] > r2) : (unsigned char)(D[i] <= r2);
 }
 
-// Disk morphology needs distances only up to r: a radius-bounded separable transform, one
-// thread per pixel.  Pass V: gv(p) = min |dy| <= r with a feature at (y + dy, x), else r + 1.
-// Pass H: p is within r of a feature iff some |dx| <= r has dx^2 + gv(y, x + dx)^2 <= r^2
-// (the nearest feature q has |qy - py| <= r and |qx - px| <= r) -- exact, like the full EDT.
+// Disk morphology needs distances only up to r: a radius-bounded separable transform.  Pass V:
+// gv(p) = min |dy| <= r with a feature at (y + dy, x), else r + 1.  Pass H: p is within r of a
+// feature iff some |dx| <= r has dx^2 + gv(y, x + dx)^2 <= r^2 (the nearest feature q has
+// |qy - py| <= r and |qx - px| <= r) -- exact, like the full EDT.
+// Both passes scan a segment of kSeg pixels per thread, with r pixels of context on each side: pass V
+// keeps the nearest feature row above / below (forward, then backward), pass H the reach of every
+// source s (gv(s) <= r covers |x - s| <= w(s) = floor(sqrt(r^2 - gv(s)^2))), rightward then leftward --
+// O(1) reads per pixel instead of O(r) (round 4: 183 -> ~30 us per pass at 4096^2).
 __global__ void cm_bnd_cols_kernel(const unsigned char* __restrict__ A, int64_t H, int64_t W, int r,
                                    unsigned char want, unsigned char* __restrict__ gv) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= H * W) return;
-    const int64_t y = i / W, x = i - (i / W) * W;
-    int d = r + 1;
-    for (int k = 0; k <= r; ++k) {
-        const bool up = y - k >= 0 && A[(y - k) * W + x] == want;
-        const bool dn = y + k < H && A[(y + k) * W + x] == want;
-        if (up || dn) { d = k; break; }
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= W) return;
+    const int64_t y0 = (int64_t)blockIdx.y * kSeg, y1 = y0 + kSeg < H ? y0 + kSeg : H;
+    const int64_t far = -(int64_t)r - 2;
+    int64_t up = far;  // nearest feature row <= y
+    for (int64_t y = y0 - r > 0 ? y0 - r : 0; y < y1; ++y) {
+        if (A[y * W + x] == want) up = y;
+        if (y >= y0) gv[y * W + x] = (unsigned char)(y - up <= r ? y - up : r + 1);
     }
-    gv[i] = (unsigned char)d;
+    int64_t dn = -1;  // nearest feature row >= y (-1: none)
+    for (int64_t y = (y1 - 1 + r < H - 1 ? y1 - 1 + r : H - 1); y >= y0; --y) {
+        if (A[y * W + x] == want) dn = y;
+        if (y < y1 && dn >= 0 && dn - y <= r && dn - y < gv[y * W + x]) gv[y * W + x] = (unsigned char)(dn - y);
+    }
+}
+
+// w(g) = floor(sqrt(r^2 - g^2)) for g <= r (exact on integers), -1 when g > r
+__device__ __forceinline__ int bnd_halfwidth(int g, int r) {
+    if (g > r) return -1;
+    const int v = r * r - g * g;
+    int w = (int)__builtin_sqrtf((float)v);
+    while (w * w > v) --w;
+    while ((w + 1) * (w + 1) <= v) ++w;
+    return w;
 }
 
 __global__ void cm_bnd_rows_kernel(const unsigned char* __restrict__ A, const unsigned char* __restrict__ gv, int64_t H,
                                    int64_t W, int r, int erode, unsigned char* __restrict__ out) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= H * W) return;
-    const int64_t y = i / W, x = i - (i / W) * W;
-    const int r2 = r * r;
-    bool near = false;
-    for (int k = 0; k <= r && !near; ++k) {
-        const int k2 = k * k;
-        if (x - k >= 0) { const int g = gv[y * W + x - k]; near |= g <= r && k2 + g * g <= r2; }
-        if (x + k < W) { const int g = gv[y * W + x + k]; near |= g <= r && k2 + g * g <= r2; }
+    const int64_t nseg = (W + kSeg - 1) / kSeg;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= H * nseg) return;
+    const int64_t y = t / nseg, x0 = (t - y * nseg) * kSeg, x1 = x0 + kSeg < W ? x0 + kSeg : W;
+    const unsigned char* row = gv + y * W;
+    unsigned char* o = out + y * W;
+    // rightward: the furthest right any source s <= x reaches
+    int64_t reach = -1;
+    for (int64_t s = x0 - r > 0 ? x0 - r : 0; s < x1; ++s) {
+        const int w = bnd_halfwidth(row[s], r);
+        if (w >= 0 && s + w > reach) reach = s + w;
+        if (s >= x0) o[s] = (unsigned char)(reach >= s);
     }
-    out[i] = erode ? (unsigned char)(A[i] && !near) : (unsigned char)near;
+    // leftward: the furthest left any source s >= x reaches; then the final value
+    int64_t lreach = W + r + 1;
+    for (int64_t s = (x1 - 1 + r < W - 1 ? x1 - 1 + r : W - 1); s >= x0; --s) {
+        const int w = bnd_halfwidth(row[s], r);
+        if (w >= 0 && s - w < lreach) lreach = s - w;
+        if (s < x1) {
+            const bool near = o[s] || lreach <= s;
+            o[s] = erode ? (unsigned char)(A[y * W + s] && !near) : (unsigned char)near;
+        }
+    }
 }
 
 hipError_t cm_morph(const unsigned char* A, int64_t H, int64_t W, int r, bool erode, unsigned char* out, int* g, int* D,
@@ -358,9 +388,11 @@ hipError_t cm_morph(const unsigned char* A, int64_t H, int64_t W, int r, bool er
         return hipGetLastError();
     }
     unsigned char* gv = reinterpret_cast<unsigned char*>(g);
-    const unsigned grid = (unsigned)((n + 255) / 256);
-    hipLaunchKernelGGL(cm_bnd_cols_kernel, dim3(grid), dim3(256), 0, st, A, H, W, r, (unsigned char)(erode ? 0 : 1), gv);
-    hipLaunchKernelGGL(cm_bnd_rows_kernel, dim3(grid), dim3(256), 0, st, A, gv, H, W, r, erode ? 1 : 0, out);
+    const dim3 gcols((unsigned)((W + 255) / 256), (unsigned)((H + kSeg - 1) / kSeg));
+    hipLaunchKernelGGL(cm_bnd_cols_kernel, gcols, dim3(256), 0, st, A, H, W, r, (unsigned char)(erode ? 0 : 1), gv);
+    const int64_t rows_threads = H * ((W + kSeg - 1) / kSeg);
+    hipLaunchKernelGGL(cm_bnd_rows_kernel, dim3((unsigned)((rows_threads + 255) / 256)), dim3(256), 0, st, A, gv, H, W, r,
+                       erode ? 1 : 0, out);
     return hipGetLastError();
 }
 
@@ -480,7 +512,14 @@ __global__ void cm_ccl_border_kernel(int64_t H, int64_t W, const int* __restrict
         b = a + W;
     }
     const int ra = lroot[a], rb = lroot[b];
-    if (ra >= 0 && rb >= 0 && ra != rb) ccl_union(parent, ra, rb, 1);
+    if (ra < 0 || rb < 0 || ra == rb) return;
+    // the previous pair along the same border (y - 1 / x - 1) joins the same two local components in
+    // most places: only the first pair of such a run unions (a union is idempotent; the run's first
+    // pair always does it).  Most pixels are in one component, whose root every union would contend on.
+    const int64_t pa = t < nv ? a - W : a - 1, pb = t < nv ? b - W : b - 1;
+    const bool has_prev = t < nv ? (t % H) > 0 : ((t - nv) % W) > 0;
+    if (has_prev && lroot[pa] == ra && lroot[pb] == rb) return;
+    ccl_union(parent, ra, rb, 1);
 }
 
 __global__ void cm_ccl_resolve_kernel(int64_t n, const int* __restrict__ lroot, int* parent) {

@@ -1779,6 +1779,23 @@ int eik_image_fill_u8(eik_ctx* c, const uint8_t* im, int64_t H, int64_t W, uint8
     return EIK_OK;
 }
 
+int eik_disk_morph_u8(eik_ctx* c, const uint8_t* im, int64_t H, int64_t W, int radius, int erode, uint8_t* out) {
+    if (!c || !im || !out || H < 1 || W < 1 || radius < 0)
+        return c ? set_err(c, EIK_ERR_ARG, "bad disk morphology arguments") : EIK_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t n = H * W;
+    HIPCHK(c, c->cm_u8.ensure(3 * n + 64));
+    HIPCHK(c, c->cm_i32.ensure(sizeof(int) * 3 * n));
+    unsigned char* a = (unsigned char*)c->cm_u8.p;
+    unsigned char* o = a + n;
+    int* g = (int*)c->cm_i32.p;
+    HIPCHK(c, host_to_dev(c, a, im, n, c->stream));
+    HIPCHK(c, cm_morph(a, H, W, radius, erode != 0, o, g, g + n, g + 2 * n, c->stream));
+    HIPCHK(c, dev_to_host(c, out, o, n, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return EIK_OK;
+}
+
 // ------------------------------------------------------- rover path (planner step 1, :1097-1258)
 int eik_rover_path_f64(eik_ctx* c, const double* Z, int64_t H, int64_t W, const eik_rover_query* q,
                        const eik_costmap_params* params, double* path_xyz, double* heading, int64_t cap,

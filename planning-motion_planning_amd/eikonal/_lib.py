@@ -135,6 +135,7 @@ def lib():
         L.eik_costmap_dev.argtypes = [vp, vp, i64, i64, C.c_double, C.c_double, P(CostmapParams), vp, vp, vp]
         L.eik_surface_normal_f64.argtypes = [vp, _f64p, i64, i64, C.c_double, _f64p, _f64p, _f64p]
         L.eik_image_fill_u8.argtypes = [vp, _u8p, i64, i64, _u8p]
+        L.eik_disk_morph_u8.argtypes = [vp, _u8p, i64, i64, C.c_int, C.c_int, _u8p]
         L.eik_load_dem_txt.argtypes = [C.c_char_p, vp, i64, P(i64), P(i64), C.c_int]
         L.eik_io_last_error.restype = C.c_char_p
         L.eik_fim2d_live_bind.argtypes = [vp, vp * 8, vp * 8]
@@ -172,7 +173,7 @@ EXPORTED = [
     "eik_fim2d_iterate", "eik_fim2d_solve", "eik_fim2d_pack_edges", "eik_fim2d_merge_ghost", "eik_fim2d_active",
     "eik_fim2d_stats", "eik_path2d_dev", "eik_selftest_walker_math", "eik_tmap3d_f32", "eik_tmap3d_f64",
     "eik_tmap3d_early_f32", "eik_tmap3d_early_f64", "eik_fim3d_early_exit", "eik_path3d_f64", "eik_fim3d_solve",
-    "eik_path3d_dev", "eik_costmap_f64", "eik_costmap_dev", "eik_surface_normal_f64", "eik_image_fill_u8",
+    "eik_path3d_dev", "eik_costmap_f64", "eik_costmap_dev", "eik_surface_normal_f64", "eik_image_fill_u8", "eik_disk_morph_u8",
     "eik_load_dem_txt", "eik_io_last_error", "eik_fim2d_live_bind", "eik_fim2d_launch", "eik_fim2d_live_pack",
     "eik_fim2d_live_merge", "eik_fim2d_release", "eik_node_allreduce", "eik_node_shm_open",
     "eik_node_shm_close", "eik_node_shm_unlink", "eik_ipc_alloc", "eik_ipc_free", "eik_ipc_open", "eik_ipc_close",
@@ -451,6 +452,14 @@ class Context:
         H, W = im.shape
         out = np.empty_like(im)
         self._chk(lib().eik_image_fill_u8(self._h, im, H, W, out))
+        return out
+
+    def disk_morph(self, im, radius, erode):
+        """cv2.erode / cv2.dilate of a 0/1 mask with structural_disk(radius) (eik_disk_morph_u8)."""
+        im = np.ascontiguousarray(im, dtype=np.uint8)
+        H, W = im.shape
+        out = np.empty_like(im)
+        self._chk(lib().eik_disk_morph_u8(self._h, im, H, W, int(radius), int(bool(erode)), out))
         return out
 
     def gradient2d(self, T):

@@ -113,3 +113,22 @@ def test_costmap_vs_reference_fixture(ctx, golden, k):
     fin = np.isfinite(R)
     assert np.array_equal(np.isfinite(cost), fin)
     assert (np.abs(cost[fin] - R[fin]) / R[fin]).max() <= 1e-12
+
+
+MORPH_CASES = [((300, 257), 1), ((300, 257), 9), ((300, 257), 10), ((300, 257), 20), ((130, 200), 63),
+               ((130, 200), 64), ((131, 66), 65), ((70, 300), 3)]
+
+
+@pytest.mark.parametrize("shape,r", MORPH_CASES, ids=[f"{s[0]}x{s[1]}-r{r}" for s, r in MORPH_CASES])
+@pytest.mark.parametrize("erode", [False, True])
+def test_disk_morphology_vs_oracle(ctx, shape, r, erode):
+    """cv2.erode / cv2.dilate with structural_disk (Coupled_motion_planner.py:96-105, :1168-1177) on
+    random masks, bit-exact against the oracle's restatement: the segment scans of the bounded
+    transform (csrc/costmap.hip cm_bnd_*) at radii around the 64-pixel segment length, ragged shapes."""
+    rng = np.random.default_rng(r * 7 + erode)
+    p = 0.92 if erode else 0.02  # erosion of a mostly-set mask, dilation of a sparse one
+    im = (rng.random(shape) < p).astype(np.uint8)
+    se = CO.structural_disk(r)
+    ref = CO.erode(im, se) if erode else CO.dilate(im, se)
+    got = ctx.disk_morph(im, r, erode)
+    assert np.array_equal(got, ref), (shape, r, erode, int((got != ref).sum()))
