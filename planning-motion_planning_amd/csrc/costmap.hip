@@ -457,18 +457,28 @@ __device__ __forceinline__ void ccl_union(int* p, int a, int b, int scope) {
     }
 }
 
+// Each pixel starts linked to the first pixel of its horizontal run (a wave holds two 32-pixel tile
+// rows: run starts from one ballot), so only vertical neighbours are unioned, and of those only the
+// first column of each stretch where two runs touch (the pixels to its left already joined them).
 __global__ __launch_bounds__(256) void cm_ccl_local_kernel(const unsigned char* __restrict__ m, int64_t H, int64_t W,
                                                            int* __restrict__ lroot, int* __restrict__ parent) {
+    static_assert(kCcl == 32, "a wave holds two tile rows");
     __shared__ int lp[kCcl * kCcl];
     const unsigned char v = m[0];
     const int64_t y0 = (int64_t)blockIdx.y * kCcl, x0 = (int64_t)blockIdx.x * kCcl;
+    const int lane = threadIdx.x & 63;
     bool s[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int q = threadIdx.x + 256 * k;
         const int64_t gy = y0 + q / kCcl, gx = x0 + q % kCcl;
         s[k] = gy < H && gx < W && m[gy * W + gx] == v;
-        lp[q] = s[k] ? q : -1;
+        const unsigned long long sm = __ballot(s[k]);
+        // a run starts where the pixel is set and its left neighbour (same row) is not
+        const unsigned long long starts = sm & ~((sm << 1) & ~0x0000000100000001ull);
+        const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+        const int rs = 63 - __clzll(starts & upto);  // the run's first lane (same row: col 0 starts a run)
+        lp[q] = s[k] ? q - (lane - rs) : -1;
     }
     __syncthreads();
 #pragma unroll
@@ -476,8 +486,9 @@ __global__ __launch_bounds__(256) void cm_ccl_local_kernel(const unsigned char* 
         const int q = threadIdx.x + 256 * k;
         if (!s[k]) continue;
         const int lx = q % kCcl, ly = q / kCcl;
-        if (lx + 1 < kCcl && ccl_ld(lp, q + 1, 0) >= 0) ccl_union(lp, q, q + 1, 0);  // -1 never changes
-        if (ly + 1 < kCcl && ccl_ld(lp, q + kCcl, 0) >= 0) ccl_union(lp, q, q + kCcl, 0);
+        if (ly + 1 >= kCcl || ccl_ld(lp, q + kCcl, 0) < 0) continue;
+        if (lx > 0 && ccl_ld(lp, q - 1, 0) >= 0 && ccl_ld(lp, q + kCcl - 1, 0) >= 0) continue;  // joined on the left
+        ccl_union(lp, q, q + kCcl, 0);  // (-1 entries never change: pixels not set)
     }
     __syncthreads();
 #pragma unroll
