@@ -277,11 +277,114 @@ __global__ __launch_bounds__(256) void cm_edt_rows_lds_kernel(const int* __restr
     }
 }
 
+// The EDT of :1194 feeds only od = dil * (1 - dist / max(dist)) (:1196): dist matters exactly where
+// dil is set -- within r of an obstacle, i.e. D <= r^2 (dil = the disk dilation of the same mask,
+// :1192) -- plus its maximum.  Exact scans of every kEdtSample-th pixel in both directions give Ds
+// and a lower bound Mlb = max Ds of max D; a pixel lies within 15 rows and columns of the sample
+// it is mapped to, so d <= sqrt(Ds) + 15 sqrt(2) (d is 1-Lipschitz).  Where that bound is <= Mlb the pixel cannot exceed the
+// maximum: its outward scan stops at k = r (exact if D <= r^2, the dil pixels; else it stores a
+// value <= Mlb, outside dil, where od is 0 either way).  Every other pixel is scanned in full.  Every
+// D <= r^2 and the maximum stay exact, so dist, its maximum and od are bit-identical to the full
+// transform's.
+constexpr int kEdtSample = 16;
+__global__ void cm_edt_sample_kernel(const int* __restrict__ g, int64_t H, int64_t W, unsigned* __restrict__ mlb,
+                                     int* __restrict__ ds) {
+    const int64_t ny = (H + kEdtSample - 1) / kEdtSample, nx = (W + kEdtSample - 1) / kEdtSample;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long best = 0;
+    if (t < ny * nx) {
+        const int64_t y = (t / nx) * kEdtSample, x = (t - (t / nx) * nx) * kEdtSample;
+        const int* row = g + y * W;
+        long long b = row[x] >= kFar ? (long long)1 << 62 : (long long)row[x] * row[x];
+        for (long long k = 1; k * k < b && (x - k >= 0 || x + k < W); ++k) {
+            if (x - k >= 0 && row[x - k] < kFar) { const long long v = k * k + (long long)row[x - k] * row[x - k]; b = v < b ? v : b; }
+            if (x + k < W && row[x + k] < kFar) { const long long v = k * k + (long long)row[x + k] * row[x + k]; b = v < b ? v : b; }
+        }
+        best = b > INT32_MAX ? INT32_MAX : (unsigned long long)b;
+        ds[t] = (int)best;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long v = __shfl_xor(best, o);
+        best = v > best ? v : best;
+    }
+    if ((threadIdx.x & 63) == 0 && best) atomicMax(mlb, (unsigned)best);
+}
+
+__global__ __launch_bounds__(256) void cm_edt_rows_ramp_kernel(const int* __restrict__ g, int64_t H, int64_t W, int r,
+                                                               const unsigned* __restrict__ mlb,
+                                                               const int* __restrict__ ds, int* __restrict__ D) {
+    __shared__ int gs[kEdtRowMax];
+    const int64_t y = blockIdx.x;
+    const int w = (int)W;
+    const long long lb = (long long)*mlb;
+    const int64_t ny = (H + kEdtSample - 1) / kEdtSample, nx = (W + kEdtSample - 1) / kEdtSample;
+    const int64_t sy = (y + kEdtSample / 2) / kEdtSample < ny ? (y + kEdtSample / 2) / kEdtSample : ny - 1;
+    for (int x = threadIdx.x; x < w; x += blockDim.x) gs[x] = g[y * W + x];
+    __syncthreads();
+    for (int x = threadIdx.x; x < w; x += blockDim.x) {
+        const int64_t sx = (x + kEdtSample / 2) / kEdtSample < nx ? (x + kEdtSample / 2) / kEdtSample : nx - 1;
+        // >= d(x): the sample is within 15 rows and 15 columns (8 + 8 inside, up to 15 at the clamped
+        // last row / column of samples)
+        const double ub = __builtin_sqrt((double)ds[sy * nx + sx]) + 21.22;
+        const bool full = ub * ub > (double)lb;
+        long long best = gs[x] >= kFar ? (long long)1 << 62 : (long long)gs[x] * gs[x];
+        for (int k = 1; (long long)k * k < best && (k <= r || full) && (x - k >= 0 || x + k < w); ++k) {
+            const long long k2 = (long long)k * k;
+            if (x - k >= 0 && gs[x - k] < kFar) {
+                const long long v = k2 + (long long)gs[x - k] * gs[x - k];
+                best = v < best ? v : best;
+            }
+            if (x + k < w && gs[x + k] < kFar) {
+                const long long v = k2 + (long long)gs[x + k] * gs[x + k];
+                best = v < best ? v : best;
+            }
+        }
+        // a capped scan that found nothing within r: outside dil; store a value <= Mlb <= max D
+        if (!full && best > (long long)r * r && best > lb) best = lb;
+        D[y * W + x] = best > INT32_MAX ? INT32_MAX : (int)best;
+    }
+}
+
 struct FeatEq {  // feat = (m[i] == val)
     const unsigned char* m;
     unsigned char val;
     __device__ bool operator()(int64_t i) const { return m[i] == val; }
 };
+
+static hipError_t cm_edt_cols(const unsigned char* m, unsigned char val, int64_t H, int64_t W, int* g, int* vbuf,
+                              hipStream_t st);
+
+// :1194's transform as the ramp uses it (see cm_edt_sample_kernel); r = the dil radius of :1192
+hipError_t cm_edt_ramp(const unsigned char* m, int64_t H, int64_t W, int r, int* g, int* D, int* vbuf, hipStream_t st) {
+    if (W > kEdtRowMax) return cm_edt(m, 1, H, W, g, D, vbuf, st);
+    hipError_t e = cm_edt_cols(m, 1, H, W, g, vbuf, st);
+    if (e != hipSuccess) return e;
+    unsigned* mlb = reinterpret_cast<unsigned*>(vbuf);  // (the column pass's scratch is free again)
+    e = hipMemsetAsync(mlb, 0, sizeof(unsigned), st);
+    if (e != hipSuccess) return e;
+    const int64_t ns = ((H + kEdtSample - 1) / kEdtSample) * ((W + kEdtSample - 1) / kEdtSample);
+    int* ds = vbuf + 1;  // ns <= n - 1 exact sample values (H, W >= 2)
+    hipLaunchKernelGGL(cm_edt_sample_kernel, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, st, g, H, W, mlb, ds);
+    hipLaunchKernelGGL(cm_edt_rows_ramp_kernel, dim3((unsigned)H), dim3(256), 0, st, g, H, W, r, mlb, ds, D);
+    return hipGetLastError();
+}
+
+static hipError_t cm_edt_cols(const unsigned char* m, unsigned char val, int64_t H, int64_t W, int* g, int* vbuf,
+                              hipStream_t st) {
+    const int64_t nseg = (H + kSeg - 1) / kSeg;
+    if (2 * nseg * W <= H * W) {
+        int* first = vbuf;
+        int* last = vbuf + nseg * W;
+        const dim3 grid((unsigned)((W + 255) / 256), (unsigned)nseg);
+        hipLaunchKernelGGL(cm_seg_summary_kernel<FeatEq>, grid, dim3(256), 0, st, FeatEq{m, val}, H, W, first, last);
+        hipLaunchKernelGGL(cm_seg_carry_kernel, dim3((unsigned)((W + 255) / 256)), dim3(256), 0, st, nseg, W, first, last);
+        hipLaunchKernelGGL(cm_seg_fill_kernel<FeatEq>, grid, dim3(256), 0, st, FeatEq{m, val}, H, W, first, last, g);
+    } else {
+        hipLaunchKernelGGL(cm_edt_cols_kernel<FeatEq>, dim3((unsigned)((W + 63) / 64)), dim3(64), 0, st,
+                           FeatEq{m, val}, H, W, g);
+    }
+    return hipGetLastError();
+}
 
 hipError_t cm_edt(const unsigned char* m, unsigned char val, int64_t H, int64_t W, int* g, int* D, int* vbuf,
                   hipStream_t st) {

@@ -171,6 +171,8 @@ hipError_t cm_normals(const double* Z, int64_t H, int64_t W, double size, unsign
                       unsigned char* obst, double* Nx, double* Ny, double* Nz, hipStream_t st);
 hipError_t cm_morph(const unsigned char* A, int64_t H, int64_t W, int r, bool erode, unsigned char* out, int* g, int* D,
                     int* vbuf, hipStream_t st);
+// :1194's transform as od (:1196) uses it: exact where D <= r^2 (r = :1192's dil radius) and at its maximum
+hipError_t cm_edt_ramp(const unsigned char* m, int64_t H, int64_t W, int r, int* g, int* D, int* vbuf, hipStream_t st);
 hipError_t cm_edt(const unsigned char* m, unsigned char val, int64_t H, int64_t W, int* g, int* D, int* vbuf,
                   hipStream_t st);
 hipError_t cm_fill_cost(const unsigned char* m, int64_t n, float* c, hipStream_t st);

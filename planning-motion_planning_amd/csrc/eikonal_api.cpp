@@ -1722,7 +1722,7 @@ int eik_costmap_dev(eik_ctx* c, const double* d_Z, int64_t H, int64_t W, double 
     HIPCHK(c, cm_morph(tmp, H, W, r2, true, obst, g, D, vbuf, st));  // :1177
     HIPCHK(c, cm_border(obst, H, W, 1, st));                         // :1180-1184
     HIPCHK(c, cm_morph(obst, H, W, r3, false, dil, g, D, vbuf, st)); // :1192
-    HIPCHK(c, cm_edt(obst, 1, H, W, g, D, vbuf, st));                // :1194 (distance to obstacles)
+    HIPCHK(c, cm_edt_ramp(obst, H, W, r3, g, D, vbuf, st));          // :1194 (distance to obstacles, as :1196 uses it)
     HIPCHK(c, cm_cost(obst, dil, D, H, W, res, p.high, p.gradient, work, tmpd, d_cost, red, st));  // :1187-1216
     return EIK_OK;
 }
