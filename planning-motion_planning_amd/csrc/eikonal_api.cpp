@@ -23,6 +23,10 @@
 
 using namespace eik;
 
+int rover_assemble(const double* pathS, int64_t nS, const double* pathG, int64_t nG, const double* Z, int64_t H,
+                   int64_t W, const eik_rover_query* q, double* path_xyz, double* heading, int64_t cap, int64_t* n_out,
+                   double zmin_known);  // rover.cpp
+
 namespace {
 
 thread_local std::string g_create_err;
@@ -1712,6 +1716,10 @@ int eik_costmap_dev(eik_ctx* c, const double* d_Z, int64_t H, int64_t W, double 
     const int r2 = (int)std::nearbyint((p.diagonal / 2) / res);     // :1172-1173
     const int r3 = (int)std::nearbyint(p.expansion / res);          // :1190-1191
     HIPCHK(c, cm_normals(d_Z, H, W, size, red, p.slope_max, obst, nullptr, nullptr, nullptr, st));  // :1104-1160
+    // min(Z)'s key (red is reused below) for the rover path's z lookup (:1101, :1246): misc word 5
+    HIPCHK(c, c->misc.ensure(64));
+    HIPCHK(c, hipMemcpyAsync((unsigned long long*)c->misc.p + 5, red, sizeof(unsigned long long),
+                             hipMemcpyDeviceToDevice, st));
     int rc = cm_fill(c, obst, H, W, fcost, fT, st);                 // :1163-1164
     if (rc) return rc;
     HIPCHK(c, cm_morph(obst, H, W, r1, true, tmp, g, D, vbuf, st));  // :1168
@@ -1824,9 +1832,22 @@ int eik_rover_path_f64(eik_ctx* c, const double* Z, int64_t H, int64_t W, const 
     double* dZ = (double*)c->T2.p;
     double* dcost = (double*)c->cost.p;
     double* dT = (double*)c->T.p;
+    // EIK_ROVER_PHASES=1 (diagnostics): synchronise after each phase and print its wall time
+    static const bool phases = getenv("EIK_ROVER_PHASES") != nullptr;
+    auto tp = std::chrono::steady_clock::now();
+    auto phase = [&](const char* name) {
+        if (!phases) return;
+        (void)hipStreamSynchronize(st);
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[rover] %-10s %8.3f ms\n", name, std::chrono::duration<double, std::milli>(now - tp).count());
+        tp = now;
+    };
+    phase("setup");
     HIPCHK(c, host_to_dev(c, dZ, Z, sizeof(double) * n, st));
+    phase("dem_h2d");
     int rc = eik_costmap_dev(c, dZ, H, W, res, q->size, params, dcost, nullptr, st);  // :1101-1216
     if (rc) return rc;
+    phase("costmap");
     // biComputeTmap(cMap.T, goal = sample node, start = rover node)   :1222; both fronts, one batch
     HIPCHK(c, hipMemcpyAsync(dcost + n, dcost, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
     if (cost_out) HIPCHK(c, dev_to_host(c, cost_out, dcost, sizeof(double) * n, st));
@@ -1836,6 +1857,7 @@ int eik_rover_path_f64(eik_ctx* c, const double* Z, int64_t H, int64_t W, const 
     unsigned long long best = 0;
     rc = solve_fronts(c, f, dcost, dT, g, H, W, &best);  // :114-162
     if (rc) return rc;
+    phase("fronts");
     if (best == ~0ull) return set_err(c, EIK_ERR_UNREACHABLE, "the rover cannot reach the sample");
     const int64_t node = (int64_t)(best & ((1ull << 29) - 1));
     const double jn[2] = {(double)(node % W), (double)(node / W)};
@@ -1861,10 +1883,13 @@ int eik_rover_path_f64(eik_ctx* c, const double* Z, int64_t H, int64_t W, const 
     if (rc) return rc;
     HIPCHK(c, hipEventRecord(c->ev_join, c->stream2));
     HIPCHK(c, hipStreamWaitEvent(st, c->ev_join, 0));
+    phase("walks");
     int64_t hn[2];
     int hs[2];
+    unsigned long long zkey = 0;
     HIPCHK(c, hipMemcpyAsync(hn, dn, sizeof hn, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipMemcpyAsync(hs, dst, sizeof hs, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(&zkey, (unsigned long long*)c->misc.p + 5, sizeof zkey, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));
     if (hs[0] == EIK_PATH_ERROR || hs[1] == EIK_PATH_ERROR)
         return set_err(c, EIK_ERR_ARG, "getPathGDM failed (the reference raises): NaN point or out of range");
@@ -1872,7 +1897,13 @@ int eik_rover_path_f64(eik_ctx* c, const double* Z, int64_t H, int64_t W, const 
     HIPCHK(c, hipMemcpyAsync(pg.data(), dP, sizeof(double) * 2 * hn[0], hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipMemcpyAsync(ps.data(), dP + 2 * pcap, sizeof(double) * 2 * hn[1], hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));
-    rc = eik_rover_assemble(ps.data(), hn[1], pg.data(), hn[0], Z, H, W, q, path_xyz, heading, cap, n_out);
+    phase("paths_d2h");
+    // the cost builder's min(Z), from its order-preserving key (costmap.hip dkey)
+    const unsigned long long zb = (zkey >> 63) ? (zkey & ~(1ull << 63)) : ~zkey;
+    double zmin;
+    memcpy(&zmin, &zb, sizeof zmin);
+    rc = rover_assemble(ps.data(), hn[1], pg.data(), hn[0], Z, H, W, q, path_xyz, heading, cap, n_out, zmin);
+    phase("assemble");
     if (rc) return set_err(c, rc, *n_out > cap ? "path buffer too small (%ld rows needed)" : "waypoint outside the DEM",
                            (long)*n_out);
     return EIK_OK;

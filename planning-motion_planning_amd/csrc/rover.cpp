@@ -9,9 +9,11 @@
 
 #include "../../include/eikonal.h"
 
-extern "C" int eik_rover_assemble(const double* pathS, int64_t nS, const double* pathG, int64_t nG, const double* Z,
-                                  int64_t H, int64_t W, const eik_rover_query* q, double* path_xyz, double* heading,
-                                  int64_t cap, int64_t* n_out) {
+// zmin_known: min(Z) when the caller has it (eik_rover_path_f64: the cost builder's device minimum,
+// exact), else NaN -- a host pass over the whole DEM (7 ms of planner step 1 at 4096^2, one core)
+int rover_assemble(const double* pathS, int64_t nS, const double* pathG, int64_t nG, const double* Z, int64_t H,
+                   int64_t W, const eik_rover_query* q, double* path_xyz, double* heading, int64_t cap, int64_t* n_out,
+                   double zmin_known) {
 #pragma clang fp contract(off)  // numpy's elementwise arithmetic: no fused multiply-adds
     if (!pathS || !pathG || !Z || !q || !path_xyz || !heading || !n_out || nS < 1 || nG < 1 || H < 1 || W < 1 ||
         !(q->resolution > 0))
@@ -46,8 +48,11 @@ extern "C" int eik_rover_assemble(const double* pathS, int64_t nS, const double*
     *n_out = n;
     if (n > cap) return EIK_ERR_ARG;
     // z = zp + Zs[uint32(round(y / res)), uint32(round(x / res))], Zs = Z - min(Z)   :1101, :1246
-    double zmin = std::numeric_limits<double>::infinity();
-    for (int64_t i = 0; i < H * W; ++i) zmin = std::min(zmin, Z[i]);  // np.min (no NaN in a DEM)
+    double zmin = zmin_known;
+    if (std::isnan(zmin)) {
+        zmin = std::numeric_limits<double>::infinity();
+        for (int64_t i = 0; i < H * W; ++i) zmin = std::min(zmin, Z[i]);  // np.min (no NaN in a DEM)
+    }
     for (int64_t k = 0; k < n; ++k) {
         const size_t i = keep[k];
         const double fy = std::nearbyint(py[i] / res), fx = std::nearbyint(px[i] / res);  // half to even
@@ -62,4 +67,11 @@ extern "C" int eik_rover_assemble(const double* pathS, int64_t nS, const double*
     for (int64_t k = 1; k < n; ++k)
         heading[k] = std::atan2(path_xyz[3 * k + 1] - path_xyz[3 * (k - 1) + 1], path_xyz[3 * k] - path_xyz[3 * (k - 1)]);
     return EIK_OK;
+}
+
+extern "C" int eik_rover_assemble(const double* pathS, int64_t nS, const double* pathG, int64_t nG, const double* Z,
+                                  int64_t H, int64_t W, const eik_rover_query* q, double* path_xyz, double* heading,
+                                  int64_t cap, int64_t* n_out) {
+    return rover_assemble(pathS, nS, pathG, nG, Z, H, W, q, path_xyz, heading, cap, n_out,
+                          std::numeric_limits<double>::quiet_NaN());
 }
