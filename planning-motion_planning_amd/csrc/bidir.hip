@@ -18,8 +18,9 @@
 //   2. select: per field the smallest value bucket holding >= K0+1 cells (coarse scan, then a
 //              1024-bin histogram inside that coarse bin) -> the member set {bucket(T) <=
 //              threshold}, a prefix of the field's pop order that holds every cell of rank <= K0
-//   3. rank:   compact the members in node order (stable select), radix-sort them by T (stable,
-//              so ties stay in node order) -> their exact ranks; non-members keep rank UINT_MAX
+//   3. rank:   compact the members in node order (stable select), radix-sort them by T rounded to
+//              float (stable: ties stay in node order), then put each run of equal floats in (T,
+//              node) order -> their exact ranks; non-members keep rank UINT_MAX
 //   4. join:   min over cells of max(rankG, rankS) as before.
 // A non-member has rank > K0 >= k*, so it can be neither the join nor a closed cell of a partial
 // field, and the members' ranks equal their ranks in the whole field (every cell below a member
@@ -265,14 +266,40 @@ __global__ void join_scale_kernel(const double* __restrict__ TG, const double* _
     sel->scale = double(kCoarse) / (4.0 * (M > 0.0 ? M : 1.0));
 }
 
-// 3. keys of the compacted members (node order) for the stable sort
+// 3. keys of the compacted members (node order) for the stable sort: T rounded to float (monotone,
+//    so the float order is the double order wherever the floats differ), 32-bit keys -- half the
+//    radix passes of the doubles' bits; join_fixup_kernel then orders the runs of equal floats
 __global__ void join_gather_kernel(const double* __restrict__ T, const unsigned* __restrict__ list, int64_t m,
-                                   unsigned long long* __restrict__ keys, unsigned* __restrict__ idx) {
+                                   unsigned* __restrict__ keys, unsigned* __restrict__ idx) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= m) return;
     const unsigned i = list[j];
-    keys[j] = (unsigned long long)__double_as_longlong(T[i]);
+    keys[j] = __float_as_uint((float)T[i]);  // T >= 0: the float bits order as unsigned
     idx[j] = i;
+}
+
+// After the stable sort by float key (ties in node order): each run of equal float keys is put in
+// (T, node) order -- insertion sort by its first thread.  Runs are short (cells whose T agree to
+// float precision); runs of exactly equal T are already in node order, so they cost one pass.
+__global__ void join_fixup_kernel(const double* __restrict__ T, const unsigned* __restrict__ key, int64_t m,
+                                  unsigned* __restrict__ idx) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j + 1 >= m || key[j + 1] != key[j] || (j > 0 && key[j - 1] == key[j])) return;  // run starts only
+    int64_t e = j + 2;
+    while (e < m && key[e] == key[j]) ++e;
+    for (int64_t a = j + 1; a < e; ++a) {
+        const unsigned ia = idx[a];
+        const double ta = T[ia];
+        int64_t b = a - 1;
+        while (b >= j) {
+            const unsigned ib = idx[b];
+            const double tb = T[ib];
+            if (tb < ta || (tb == ta && ib < ia)) break;
+            idx[b + 1] = ib;
+            --b;
+        }
+        idx[b + 1] = ia;
+    }
 }
 
 // rank[sorted_idx[k]] = k for the members; every other cell keeps UINT_MAX (memset)
@@ -322,11 +349,14 @@ struct JoinLayout {
 
 size_t cub_scratch(int64_t n) {
     size_t sort_b = 0, sel_b = 0;
+    size_t sort32_b = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort32_b, (unsigned*)nullptr, (unsigned*)nullptr,
+                                             (unsigned*)nullptr, (unsigned*)nullptr, (int)n, 0, 32, (hipStream_t)0);
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort_b, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
                                              (unsigned*)nullptr, (unsigned*)nullptr, (int)n, 0, 64, (hipStream_t)0);
     (void)hipcub::DeviceSelect::If(nullptr, sel_b, hipcub::CountingInputIterator<unsigned>(0u), (unsigned*)nullptr,
                                    (unsigned*)nullptr, n, JoinMember{nullptr, nullptr, 0}, (hipStream_t)0);
-    return (std::max(sort_b, sel_b) + 255) & ~size_t(255);
+    return (std::max(std::max(sort_b, sort32_b), sel_b) + 255) & ~size_t(255);
 }
 
 // k_in | k_out (n u64) | i_in | i_out | rg | rs (n u32) | cub scratch | JoinSel
@@ -389,15 +419,19 @@ hipError_t bidir_join(const double* d_TG, const double* d_TS, int64_t n, void* d
         const int64_t m = hm[f];
         if (m > 0) {
             const unsigned g = (unsigned)((m + 255) / 256);
-            hipLaunchKernelGGL(join_gather_kernel, dim3(g), dim3(256), 0, st, T[f], lists[f], m, L.k_in, L.i_in);
+            hipLaunchKernelGGL(join_gather_kernel, dim3(g), dim3(256), 0, st, T[f], lists[f], m,
+                               reinterpret_cast<unsigned*>(L.k_in), L.i_in);
         }
         e = hipMemsetAsync(rank[f], 0xFF, sizeof(unsigned) * (size_t)n, st);
         if (e != hipSuccess) return e;
         if (m > 0) {
             size_t b = L.cub_bytes;
-            e = hipcub::DeviceRadixSort::SortPairs(L.cub_tmp, b, L.k_in, L.k_out, L.i_in, L.i_out, (int)m, 0, 64, st);
+            unsigned* k32_in = reinterpret_cast<unsigned*>(L.k_in);
+            unsigned* k32_out = reinterpret_cast<unsigned*>(L.k_out);
+            e = hipcub::DeviceRadixSort::SortPairs(L.cub_tmp, b, k32_in, k32_out, L.i_in, L.i_out, (int)m, 0, 32, st);
             if (e != hipSuccess) return e;
             const unsigned g = (unsigned)((m + 255) / 256);
+            hipLaunchKernelGGL(join_fixup_kernel, dim3(g), dim3(256), 0, st, T[f], k32_out, m, L.i_out);
             hipLaunchKernelGGL(scatter_rank_kernel, dim3(g), dim3(256), 0, st, L.i_out, m, rank[f]);
         }
     }

@@ -100,6 +100,11 @@ def make(case, rng):
         H, W = 200, 220
         TG = cone(H, W, 50, 60, rng, 0.2)
         TS = TG.copy()
+    elif case == "float_ties":  # distinct doubles that round to one float: the sort's run fix-up
+        H, W = 200, 220
+        TG = np.floor(cone(H, W, 150, 120, rng)) + 1e-9 * rng.random((H, W))
+        TS = np.floor(cone(H, W, 30, 40, rng)) + 1e-9 * rng.random((H, W))
+        TG[120, 150] = TS[40, 30] = 0.0
     elif case == "large":
         H, W = 2048, 1536
         TG, TS = cone(H, W, 1400, 1800, rng, 0.4, 1.3), cone(H, W, 100, 200, rng, 0.4)
@@ -111,7 +116,7 @@ def make(case, rng):
     return TG, TS
 
 
-CASES = ["smooth", "obstacles", "ties", "manhattan", "lopsided", "corridor", "same_source", "large"]
+CASES = ["smooth", "obstacles", "ties", "manhattan", "lopsided", "corridor", "same_source", "float_ties", "large"]
 
 
 @pytest.mark.parametrize("case", CASES)
