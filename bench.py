@@ -338,12 +338,13 @@ def ms_to_path(cost, ctx, fim, dev, stream, goal, edt, start=(256, 256), reps=3)
     res = {}
     if f64:  # the drop-in computes in float64 (FastMarching.py:93-95)
         tot, lens = [], []
-        for _ in range(reps):
+        for rep in range(reps + 2):  # two untimed calls first: the pinned result pool's first blocks
             t0 = time.perf_counter()
             Th = ctx.tmap2d(host_cost, goal)
             path, st = ctx.path2d(Th, start, goal)
-            tot.append((time.perf_counter() - t0) * 1e3)
-            lens.append(len(path))
+            if rep >= 2:
+                tot.append((time.perf_counter() - t0) * 1e3)
+                lens.append(len(path))
         res.update({"ms_to_path": round(float(np.median(tot)), 3),
                     "ms_to_path_route": "drop-in: eik_tmap2d_f64 + eik_path2d_f64 on host arrays (pinned ring)"})
     tot, devs = [], []
