@@ -381,12 +381,8 @@ JoinLayout layout(void* work, int64_t n) {
 
 // d_TG/d_TS: n doubles (full fields); d_work: bidir_join_work_bytes(n).  One host synchronisation
 // (the member counts size the sorts).  members (optional, host): the two member-set sizes.
-hipError_t bidir_join(const double* d_TG, const double* d_TS, int64_t n, void* d_work, size_t work_bytes,
-                      unsigned long long* d_best, hipStream_t st, int64_t* members) {
-    if (n >= (1ll << 29)) return hipErrorInvalidValue;
-    const JoinLayout L = layout(d_work, n);
-    if (L.total > work_bytes) return hipErrorOutOfMemory;
-    JoinSel* sel = L.sel;
+// steps 1-2 of the join: the bound K0 and each field's member threshold bucket, in sel
+static hipError_t join_bound(const double* d_TG, const double* d_TS, int64_t n, JoinSel* sel, hipStream_t st) {
     hipError_t e = hipMemsetAsync(sel, 0, sizeof(JoinSel), st);
     if (e == hipSuccess) e = hipMemsetAsync(&sel->n0, 0xFF, sizeof(sel->n0), st);
     if (e != hipSuccess) return e;
@@ -397,6 +393,17 @@ hipError_t bidir_join(const double* d_TG, const double* d_TS, int64_t n, void* d
     hipLaunchKernelGGL(join_coarse_scan_kernel, dim3(1), dim3(64), 0, st, sel);
     hipLaunchKernelGGL(join_fine_kernel, dim3(pgrid), dim3(256), 0, st, d_TG, d_TS, n, sel);
     hipLaunchKernelGGL(join_fine_scan_kernel, dim3(1), dim3(64), 0, st, sel);
+    return hipGetLastError();
+}
+
+hipError_t bidir_join(const double* d_TG, const double* d_TS, int64_t n, void* d_work, size_t work_bytes,
+                      unsigned long long* d_best, hipStream_t st, int64_t* members) {
+    if (n >= (1ll << 29)) return hipErrorInvalidValue;
+    const JoinLayout L = layout(d_work, n);
+    if (L.total > work_bytes) return hipErrorOutOfMemory;
+    JoinSel* sel = L.sel;
+    hipError_t e = join_bound(d_TG, d_TS, n, sel, st);
+    if (e != hipSuccess) return e;
     // stable compaction of the members: G into i_in, S into rs (free until its ranks are scattered)
     const double* T[2] = {d_TG, d_TS};
     unsigned* lists[2] = {L.i_in, L.rs};
@@ -518,28 +525,6 @@ __global__ __launch_bounds__(256) void coarse_cost_kernel(const double* __restri
     if ((threadIdx.x & 63) == 0 && b) atomicMax(&chk->maxcost_bits, b);
 }
 
-// T at rank k* in each field (k* <= every member count, so both cells exist)
-__global__ void join_tk_kernel(const unsigned* __restrict__ rg, const unsigned* __restrict__ rs,
-                               const double* __restrict__ TG, const double* __restrict__ TS, int64_t n,
-                               const unsigned long long* __restrict__ best, FrontsCheck* __restrict__ chk) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const unsigned long long b = *best;
-    if (i >= n || b == ~0ull) return;
-    const unsigned k = (unsigned)(b >> 30);
-    if (rg[i] == k) chk->tk[0] = TG[i];
-    if (rs[i] == k) chk->tk[1] = TS[i];
-}
-
-// caps from the coarse meeting: F x (coarse T at rank k*) x margin + the largest finite cost;
-// +inf (no cap) when the coarse fronts never met
-__global__ void fronts_caps_kernel(const unsigned long long* __restrict__ best_c, double F, double margin,
-                                   FrontsCheck* __restrict__ chk) {
-    const int f = threadIdx.x;
-    if (f >= 2) return;
-    const double mc = __longlong_as_double((long long)chk->maxcost_bits);
-    chk->caps[f] = *best_c == ~0ull ? Real<double>::inf() : F * chk->tk[f] * margin + mc;
-}
-
 // the capped fields: T above the map's cap -> +inf (an upper bound, not the converged value), and
 // the kept (finite) cells per map
 __global__ __launch_bounds__(256) void cap_clean_kernel(double* __restrict__ T, int64_t n, FrontsCheck* __restrict__ chk) {
@@ -579,13 +564,28 @@ hipError_t fronts_coarse_cost(const double* d_cost, int64_t H, int64_t W, int F,
     return hipGetLastError();
 }
 
-// after bidir_join on the coarse fields (same work buffer): the caps
-hipError_t fronts_caps(const double* d_TG, const double* d_TS, int64_t n, const void* d_work,
-                       const unsigned long long* d_best, double F, double margin, FrontsCheck* chk, hipStream_t st) {
-    const JoinLayout L = layout(const_cast<void*>(d_work), n);
-    hipLaunchKernelGGL(join_tk_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, L.rg, L.rs, d_TG, d_TS, n,
-                       d_best, chk);
-    hipLaunchKernelGGL(fronts_caps_kernel, dim3(1), dim3(64), 0, st, d_best, F, margin, chk);
+// caps from the coarse fields' join bound alone (no ranks: no sort, no host synchronisation): the
+// upper edge of each field's member threshold bucket is >= its T at rank K0 >= k*
+__global__ void fronts_caps_bound_kernel(const JoinSel* __restrict__ sel, double F, double margin,
+                                         FrontsCheck* __restrict__ chk) {
+    const int f = threadIdx.x;
+    if (f >= 2) return;
+    const double mc = __longlong_as_double((long long)chk->maxcost_bits);
+    const int cb = sel->cb[f];
+    double cap = Real<double>::inf();  // fronts never met, or the threshold in the open bucket
+    if (sel->n0 != ~0ull && cb >= 0 && cb < kCoarse - 1)
+        cap = F * ((double(cb) + double(sel->fb[f] + 1) / double(kFine)) / sel->scale) * margin + mc;
+    chk->caps[f] = cap;
+    chk->best_c = sel->n0;
+}
+
+hipError_t fronts_estimate(const double* d_TG, const double* d_TS, int64_t n, void* d_work, double F, double margin,
+                           FrontsCheck* chk, hipStream_t st) {
+    if (n >= (1ll << 29)) return hipErrorInvalidValue;
+    const JoinLayout L = layout(d_work, n);
+    hipError_t e = join_bound(d_TG, d_TS, n, L.sel, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(fronts_caps_bound_kernel, dim3(1), dim3(64), 0, st, L.sel, F, margin, chk);
     return hipGetLastError();
 }
 

@@ -226,17 +226,16 @@ hipError_t bidir_partial(double* d_TG, double* d_TS, int64_t H, int64_t W, const
 // the capped fronts' device block (eikonal_api.cpp solve_fronts)
 struct FrontsCheck {
     double caps[2];                   // per front: activation cap of the full-resolution solve
-    double tk[2];                     // coarse fields: T at the meeting rank
     unsigned long long maxcost_bits;  // largest finite cost of the raster (double bits)
     unsigned kept[2];                 // cells at or below the cap per front
     unsigned viol;                    // a band cell was cut off by the cap
     unsigned pad;
-    unsigned long long best_c;        // the coarse join
+    unsigned long long best_c;        // the coarse fields' seed (~0: they never meet)
 };
 hipError_t fronts_coarse_cost(const double* d_cost, int64_t H, int64_t W, int F, double* d_out, int64_t Hc, int64_t Wc,
                               FrontsCheck* chk, hipStream_t st);
-hipError_t fronts_caps(const double* d_TG, const double* d_TS, int64_t n, const void* d_work,
-                       const unsigned long long* d_best, double F, double margin, FrontsCheck* chk, hipStream_t st);
+hipError_t fronts_estimate(const double* d_TG, const double* d_TS, int64_t n, void* d_work, double F, double margin,
+                           FrontsCheck* chk, hipStream_t st);
 hipError_t fronts_clean(double* d_T, int64_t n, FrontsCheck* chk, hipStream_t st);
 
 }  // namespace eik

@@ -1029,8 +1029,8 @@ static int join_and_partial(eik_ctx* c, double* dT, int64_t n, int64_t H, int64_
 }
 
 // Capped fronts: rasters of at least kFrontsCapCells cells, F x F coarse blocks with F =
-// max(4, ceil(max(H, W) / 512)), cap = F x (coarse T at the meeting rank) x margin (kFrontsMargin,
-// EIK_OPT_FRONTS_CAP) + the largest finite cost
+// max(4, ceil(max(H, W) / 512)), cap = F x (coarse T at the join bound's rank K0, bidir.hip
+// fronts_estimate) x margin (kFrontsMargin, EIK_OPT_FRONTS_CAP) + the largest finite cost
 constexpr int64_t kFrontsCapCells = 1 << 20;
 
 // biComputeTmap's two fronts (FastMarching.py:114-162) as one B = 2 batch -- map 0 from the goal
@@ -1070,8 +1070,7 @@ static int solve_fronts(eik_ctx* c, eik_fim2d* f, double* dcost, double* dT, con
         int rc = eik_fim2d_solve(fc, ccost, cT, gc, st);
         c->last = keep;
         if (rc) return rc;
-        HIPCHK(c, bidir_join(cT, cT + nc, nc, c->work.p, c->work.bytes, &chk->best_c, st));
-        HIPCHK(c, fronts_caps(cT, cT + nc, nc, c->work.p, &chk->best_c, (double)F, c->fronts_cap, chk, st));
+        HIPCHK(c, fronts_estimate(cT, cT + nc, nc, c->work.p, (double)F, c->fronts_cap, chk, st));
         f->a.tcap = chk->caps;
         rc = eik_fim2d_solve(f, dcost, dT, g, st);
         f->a.tcap = nullptr;
