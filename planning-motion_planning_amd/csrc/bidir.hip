@@ -14,7 +14,9 @@
 // raster.  It bounds k* first and ranks only the cells under the bound:
 //   1. seed:   n0 = argmin over cells of max(TG, TS) (both finite) -> k* <= K0 = max(rankG(n0),
 //              rankS(n0)), both ranks counted exactly in one pass beside a 256-bin coarse
-//              histogram of each field over [0, 4 max(TG(n0), TS(n0))) (+ one overflow bin)
+//              histogram of each field over [0, 4 max(TG(n0), TS(n0))) (+ one overflow bin);
+//              then n1 = argmin of the larger of the two histogram rank estimates, whose exact
+//              ranks give K1; the bound is min(K0, K1)
 //   2. select: per field the smallest value bucket holding >= K0+1 cells (coarse scan, then a
 //              1024-bin histogram inside that coarse bin) -> the member set {bucket(T) <=
 //              threshold}, a prefix of the field's pop order that holds every cell of rank <= K0
@@ -48,6 +50,9 @@ struct JoinSel {
     int fb[2];              // threshold fine bucket inside cb
     unsigned need[2];       // members still needed inside cb (K0 + 1 - cells of lower coarse buckets)
     unsigned m[2];          // member count per field (select output)
+    unsigned long long n1;  // rank-aware seed: (estimated max rank) << 29 | node; ~0: none
+    unsigned r1[2];         // exact ranks of n1
+    unsigned pre[2][kCoarse];  // cells below each coarse bucket
     unsigned hc[2][kCoarse];
     unsigned hf[2][kFine];
 };
@@ -181,6 +186,81 @@ __global__ __launch_bounds__(256) void join_count_kernel(const double* __restric
 }
 
 // 2a. per field the first coarse bucket whose running count reaches K0 + 1 (one thread per field)
+// 1c. a rank-aware seed: the value-space n0 can sit far from the meeting when the fronts grow at
+//     different rates (a front in a corner or a corridor).  Each field's rank is estimated from its
+//     coarse histogram (cells below the bucket + the bucket's share by linear position), and n1 =
+//     argmin of the larger estimate; its exact ranks then give a second bound K1 (usually far
+//     tighter), and the join keeps min(K0, K1).
+__global__ void join_prefix_kernel(JoinSel* __restrict__ sel) {
+    const int f = threadIdx.x;
+    if (f >= 2) return;
+    unsigned cum = 0;
+    for (int b = 0; b < kCoarse; ++b) {
+        sel->pre[f][b] = cum;
+        cum += sel->hc[f][b];
+    }
+}
+
+__device__ __forceinline__ unsigned rank_estimate(const JoinSel* sel, int f, double t) {
+    const double q = t * sel->scale;
+    const int b = coarse_of(t, sel->scale);
+    const double frac = b == kCoarse - 1 ? 1.0 : (q - double(b) < 0.0 ? 0.0 : q - double(b));
+    return sel->pre[f][b] + (unsigned)(frac * double(sel->hc[f][b]));
+}
+
+__global__ __launch_bounds__(256) void join_seed2_kernel(const double* __restrict__ TG, const double* __restrict__ TS,
+                                                         int64_t n, JoinSel* __restrict__ sel) {
+    __shared__ unsigned long long wmin[4];
+    unsigned long long v = ~0ull;
+    if (sel->n0 != ~0ull) {
+        const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+            const double a = TG[i], b = TS[i];
+            if (fin(a) && fin(b)) {
+                const unsigned ea = rank_estimate(sel, 0, a), eb = rank_estimate(sel, 1, b);
+                const unsigned long long c = ((unsigned long long)(ea > eb ? ea : eb) << 29) | (unsigned long long)i;
+                v = c < v ? c : v;
+            }
+        }
+    }
+    v = wave_min(v);
+    if ((threadIdx.x & 63) == 0) wmin[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long m = wmin[0];
+        for (int w = 1; w < 4; ++w) m = wmin[w] < m ? wmin[w] : m;
+        if (m != ~0ull) atomicMin(&sel->n1, m);
+    }
+}
+
+// exact ranks of n1 (as join_count_kernel's of n0, without the histograms)
+__global__ __launch_bounds__(256) void join_count2_kernel(const double* __restrict__ TG, const double* __restrict__ TS,
+                                                          int64_t n, JoinSel* __restrict__ sel) {
+    __shared__ unsigned wsum[2][4];
+    const unsigned long long p = sel->n1;
+    if (p == ~0ull) return;
+    const int64_t node = (int64_t)(p & ((1ull << 29) - 1));
+    const double g0 = TG[node], s0 = TS[node];
+    unsigned cg = 0, cs = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const double a = TG[i], b = TS[i];
+        cg += (a < g0 || (a == g0 && i < node)) ? 1u : 0u;
+        cs += (b < s0 || (b == s0 && i < node)) ? 1u : 0u;
+    }
+    cg = wave_sum(cg);
+    cs = wave_sum(cs);
+    if ((threadIdx.x & 63) == 0) {
+        wsum[0][threadIdx.x >> 6] = cg;
+        wsum[1][threadIdx.x >> 6] = cs;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        const unsigned t = wsum[threadIdx.x][0] + wsum[threadIdx.x][1] + wsum[threadIdx.x][2] + wsum[threadIdx.x][3];
+        if (t) atomicAdd(&sel->r1[threadIdx.x], t);
+    }
+}
+
 __global__ void join_coarse_scan_kernel(JoinSel* __restrict__ sel) {
     const int f = threadIdx.x;
     if (f >= 2) return;
@@ -188,7 +268,11 @@ __global__ void join_coarse_scan_kernel(JoinSel* __restrict__ sel) {
         sel->cb[f] = -1;
         return;
     }
-    const unsigned k0 = sel->r0[0] > sel->r0[1] ? sel->r0[0] : sel->r0[1];
+    unsigned k0 = sel->r0[0] > sel->r0[1] ? sel->r0[0] : sel->r0[1];
+    if (sel->n1 != ~0ull) {
+        const unsigned k1 = sel->r1[0] > sel->r1[1] ? sel->r1[0] : sel->r1[1];
+        k0 = k1 < k0 ? k1 : k0;
+    }
     unsigned cum = 0;
     int c = kCoarse - 1;
     for (int b = 0; b < kCoarse; ++b) {
@@ -385,11 +469,15 @@ JoinLayout layout(void* work, int64_t n) {
 static hipError_t join_bound(const double* d_TG, const double* d_TS, int64_t n, JoinSel* sel, hipStream_t st) {
     hipError_t e = hipMemsetAsync(sel, 0, sizeof(JoinSel), st);
     if (e == hipSuccess) e = hipMemsetAsync(&sel->n0, 0xFF, sizeof(sel->n0), st);
+    if (e == hipSuccess) e = hipMemsetAsync(&sel->n1, 0xFF, sizeof(sel->n1), st);
     if (e != hipSuccess) return e;
     const unsigned pgrid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(kPassBlocks, (n + 255) / 256));
     hipLaunchKernelGGL(join_seed_kernel, dim3(pgrid), dim3(256), 0, st, d_TG, d_TS, n, sel);
     hipLaunchKernelGGL(join_scale_kernel, dim3(1), dim3(1), 0, st, d_TG, d_TS, sel);
     hipLaunchKernelGGL(join_count_kernel, dim3(pgrid), dim3(256), 0, st, d_TG, d_TS, n, sel);
+    hipLaunchKernelGGL(join_prefix_kernel, dim3(1), dim3(64), 0, st, sel);
+    hipLaunchKernelGGL(join_seed2_kernel, dim3(pgrid), dim3(256), 0, st, d_TG, d_TS, n, sel);
+    hipLaunchKernelGGL(join_count2_kernel, dim3(pgrid), dim3(256), 0, st, d_TG, d_TS, n, sel);
     hipLaunchKernelGGL(join_coarse_scan_kernel, dim3(1), dim3(64), 0, st, sel);
     hipLaunchKernelGGL(join_fine_kernel, dim3(pgrid), dim3(256), 0, st, d_TG, d_TS, n, sel);
     hipLaunchKernelGGL(join_fine_scan_kernel, dim3(1), dim3(64), 0, st, sel);
