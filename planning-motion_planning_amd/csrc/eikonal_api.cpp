@@ -1048,7 +1048,10 @@ static int solve_fronts(eik_ctx* c, eik_fim2d* f, double* dcost, double* dT, con
     HIPCHK(c, c->work.ensure(bidir_join_work_bytes(n)));
     const bool capped = c->fronts_cap > 0 && n >= kFrontsCapCells && std::min(H, W) >= 256;
     if (capped) {
-        const int64_t F = std::max<int64_t>(4, (std::max(H, W) + 511) / 512);
+        // coarse side 512 (EIK_FRONTS_COARSE, diagnostics): 256 / 1024 were slower at 4096^2
+        // (profiles/r04t_fronts_coarse_side.log: looser caps / a longer coarse chain)
+        static const int64_t cside = getenv("EIK_FRONTS_COARSE") ? std::max(64, atoi(getenv("EIK_FRONTS_COARSE"))) : 512;
+        const int64_t F = std::max<int64_t>(4, (std::max(H, W) + cside - 1) / cside);
         const int64_t Hc = (H + F - 1) / F, Wc = (W + F - 1) / F, nc = Hc * Wc;
         const size_t cb = sizeof(double) * 2 * nc;
         HIPCHK(c, c->fronts.ensure(2 * cb + 256));
