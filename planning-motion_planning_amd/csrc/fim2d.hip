@@ -48,7 +48,8 @@ __device__ __forceinline__ R stage_cost(R c) {
 }
 
 // EIK_EDGE_FIRST (see the write-back in process_tile): measured and OFF -- C2 2-7 % slower in fp64
-// and fp32 (profiles/r03l_edge_first_ab.log): the drain before the activations is latency, not the
+// and fp32 (profiles/r03l_edge_first_ab.log), and C3 / C4 3-8 % slower (round 4,
+// profiles/r04u_edge_first_throughput_ab.log): the drain before the activations is latency, not the
 // number of stores, and the extra per-visit barrier and edge-column stores cost more than it saves.
 #ifndef EIK_EDGE_FIRST
 #define EIK_EDGE_FIRST 0
