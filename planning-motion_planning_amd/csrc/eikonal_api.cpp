@@ -1011,8 +1011,9 @@ int eik_tmap2d_batch_f32(eik_ctx* c, const float* cost, int64_t B, int64_t H, in
 }
 
 // nodeJoin + partial fields from the two device-resident full fields dT[0:n] (goal front) and
-// dT[n:2n] (start front), in place; *best = the packed join (~0: the fronts never meet).  Ends
-// with the stream synchronised on *best.
+// dT[n:2n] (start front), in place; *best = the packed join (~0: the fronts never meet).  d_cost
+// (the fronts' raster): band cells by the band relaxation (bidir.hip), else at their full-field
+// values; d_chk: the capped fronts' check.  Ends with the stream synchronised on *best.
 static int join_and_partial(eik_ctx* c, double* dT, int64_t n, int64_t H, int64_t W, unsigned long long* best,
                             int64_t members[2], const double* d_cost = nullptr, FrontsCheck* d_chk = nullptr,
                             FrontsCheck* h_chk = nullptr) {
@@ -1096,7 +1097,7 @@ static int solve_fronts(eik_ctx* c, eik_fim2d* f, double* dcost, double* dT, con
     int rc = eik_fim2d_solve(f, dcost, dT, g, st);
     if (rc) return rc;
     int64_t mem[2] = {0, 0};
-    rc = join_and_partial(c, dT, n, H, W, best, mem);
+    rc = join_and_partial(c, dT, n, H, W, best, mem, dcost);
     if (!capped) {
         c->fronts_info[4] = mem[0];
         c->fronts_info[5] = mem[1];
