@@ -141,8 +141,9 @@ int eik_bidir_join_f64(eik_ctx* ctx, const double* TG, const double* TS, int64_t
 
 /* How the last biComputeTmap / rover path formed its fronts: out[0] 1 = capped fronts, out[1] 1 =
  * the capped result was replaced by the full solve, out[2..3] cells kept under the caps (goal,
- * start front), out[4..5] cells the join ranked per front. */
-int eik_fronts_info(const eik_ctx* ctx, int64_t out[6]);
+ * start front), out[4..5] cells the join ranked per front, out[6..7] band cells relaxed per front,
+ * out[8..9] the band relaxation's sweeps per front. */
+int eik_fronts_info(const eik_ctx* ctx, int64_t out[10]);
 
 /* B independent maps (goal sweep / terrain Monte-Carlo): cost, T: B*H*W; goals: B x (x, y). */
 int eik_tmap2d_batch_f32(eik_ctx* ctx, const float* cost, int64_t B, int64_t H, int64_t W, const int64_t* goals,

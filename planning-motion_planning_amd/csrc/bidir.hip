@@ -51,6 +51,7 @@ struct JoinSel {
     unsigned need[2];       // members still needed inside cb (K0 + 1 - cells of lower coarse buckets)
     unsigned m[2];          // member count per field (select output)
     unsigned nb[2];         // band cells listed for the band relaxation (bidir_partial with a cost)
+    unsigned sweeps[2];     // the band relaxation's sweeps
     unsigned long long n1;  // rank-aware seed: (estimated max rank) << 29 | node; ~0: none
     unsigned r1[2];         // exact ranks of n1
     unsigned pre[2][kCoarse];  // cells below each coarse bucket
@@ -572,45 +573,45 @@ __global__ void bidir_partial_kernel(double* __restrict__ T, const unsigned* __r
         return;
     }
     if (viol && !fin(T[i]) && fin(cost[i])) atomicOr(viol, 1u);
-    if (blist && fin(cost[i])) {  // relaxed from +inf by bidir_band_kernel
-        T[i] = Real<double>::inf();
+    if (blist && fin(cost[i])) {
+        // relaxed by bidir_band_kernel from the update over its closed neighbours alone (an upper
+        // bound of the fixed point, already equal to it where the upwind neighbours are closed);
+        // closed cells are never written here, so their values are final
+        const double inf = Real<double>::inf();
+        auto cv = [&](bool in, int64_t j) { return in && rank[j] <= k ? T[j] : inf; };
+        const double l = cv(x > 0, i - 1), r = cv(x + 1 < W, i + 1), u = cv(y > 0, i - W), d = cv(y + 1 < H, i + W);
+        T[i] = godunov2(l < r ? l : r, u < d ? u : d, cost[i]);
         blist[atomicAdd(bcount, 1u)] = (unsigned)i;
     }
 }
 
-// The band relaxation: one workgroup per field, Gauss-Seidel sweeps over its band list until no
-// cell decreases (monotone from +inf: the fixed point does not depend on the order).  Loads bypass
-// the CU's L1 (agent scope), and every sweep ends with a fence and a barrier, so a sweep that
-// changes nothing saw every update of the one before.
-constexpr int kBandThreads = 1024, kBandMaxSweeps = 1 << 16;
-__global__ __launch_bounds__(kBandThreads) void bidir_band_kernel(double* __restrict__ TG, double* __restrict__ TS,
-                                                                  const double* __restrict__ cost, int64_t H, int64_t W,
-                                                                  const unsigned* __restrict__ listG,
-                                                                  const unsigned* __restrict__ listS,
-                                                                  const JoinSel* __restrict__ sel) {
-    __shared__ int changed;
-    double* T = blockIdx.x == 0 ? TG : TS;
-    const unsigned* list = blockIdx.x == 0 ? listG : listS;
-    const unsigned cnt = sel->nb[blockIdx.x];
-    auto ld = [&](int64_t j) { return __hip_atomic_load(T + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-    for (int sweep = 0; sweep < kBandMaxSweeps; ++sweep) {
-        if (threadIdx.x == 0) changed = 0;
-        __syncthreads();
-        for (unsigned j = threadIdx.x; j < cnt; j += blockDim.x) {
-            const int64_t i = list[j];
-            const int64_t y = i / W, x = i - y * W;
-            const double l = x > 0 ? ld(i - 1) : Real<double>::inf(), r = x + 1 < W ? ld(i + 1) : Real<double>::inf();
-            const double u = y > 0 ? ld(i - W) : Real<double>::inf(), d = y + 1 < H ? ld(i + W) : Real<double>::inf();
-            const double w = godunov2(l < r ? l : r, u < d ? u : d, cost[i]);  // getEikonal's branches
-            if (w < ld(i)) {
-                __hip_atomic_store(T + i, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                changed = 1;
-            }
-        }
-        __threadfence();
-        __syncthreads();
-        if (!changed) break;
-        __syncthreads();
+// The band relaxation: sweeps over both fronts' band lists, one launch per sweep across the GPU,
+// each cell updated in place (monotone from an upper bound: the fixed point does not depend on the
+// order) until a sweep decreases nothing beyond rounding.  Sweep s records a change in flags[s];
+// sweep s + 1 returns at once when sweep s changed nothing, so batches of sweeps are queued without
+// waiting and the host reads the flags once per batch.
+constexpr int kBandBatch = 16, kBandMaxBatches = 4096;
+__global__ void bidir_band_sweep_kernel(double* __restrict__ TG, double* __restrict__ TS, const double* __restrict__ cost,
+                                        int64_t H, int64_t W, const unsigned* __restrict__ listG,
+                                        const unsigned* __restrict__ listS, const JoinSel* __restrict__ sel,
+                                        unsigned* __restrict__ flags, int s) {
+    if (s > 0 && flags[s - 1] == 0u) return;  // converged
+    const unsigned nG = sel->nb[0], nS = sel->nb[1];
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= (int64_t)nG + nS) return;
+    double* T = j < nG ? TG : TS;
+    const int64_t i = j < nG ? listG[j] : listS[j - nG];
+    const int64_t y = i / W, x = i - y * W;
+    const double inf = Real<double>::inf();
+    const double l = x > 0 ? T[i - 1] : inf, r = x + 1 < W ? T[i + 1] : inf;
+    const double u = y > 0 ? T[i - W] : inf, d = y + 1 < H ? T[i + W] : inf;
+    const double w = godunov2(l < r ? l : r, u < d ? u : d, cost[i]);  // getEikonal's branches
+    const double t = T[i];
+    if (w < t) {
+        T[i] = w;
+        // another sweep only for a decrease beyond rounding: cells that feed each other can
+        // otherwise trade last-ulp decreases for many sweeps
+        if (w < t * (1.0 - 0x1p-40)) flags[s] = 1u;
     }
 }
 
@@ -630,8 +631,36 @@ hipError_t bidir_partial(double* d_TG, double* d_TS, int64_t H, int64_t W, const
                        &L.sel->nb[0]);
     hipLaunchKernelGGL(bidir_partial_kernel, dim3(grid), dim3(256), 0, st, d_TS, L.rs, H, W, d_best, d_cost, d_viol, ls,
                        &L.sel->nb[1]);
-    if (d_cost)
-        hipLaunchKernelGGL(bidir_band_kernel, dim3(2), dim3(kBandThreads), 0, st, d_TG, d_TS, d_cost, H, W, lg, ls, L.sel);
+    if (d_cost) {
+        unsigned hnb[2] = {0, 0};  // the band sizes size the sweep launches
+        hipError_t e = hipMemcpyAsync(hnb, L.sel->nb, sizeof hnb, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return e;
+        const int64_t cnt = (int64_t)hnb[0] + hnb[1];
+        if (cnt > 0) {
+            unsigned* flags = L.i_in;  // free after the join
+            const unsigned g = (unsigned)((cnt + 255) / 256);
+            unsigned sweeps = 0;
+            for (int batch = 0; batch < kBandMaxBatches; ++batch) {
+                e = hipMemsetAsync(flags, 0, sizeof(unsigned) * kBandBatch, st);
+                if (e != hipSuccess) return e;
+                for (int q = 0; q < kBandBatch; ++q)
+                    hipLaunchKernelGGL(bidir_band_sweep_kernel, dim3(g), dim3(256), 0, st, d_TG, d_TS, d_cost, H, W, lg, ls,
+                                       L.sel, flags, q);
+                unsigned hf[kBandBatch];
+                e = hipMemcpyAsync(hf, flags, sizeof hf, hipMemcpyDeviceToHost, st);
+                if (e == hipSuccess) e = hipStreamSynchronize(st);
+                if (e != hipSuccess) return e;
+                int last = 0;
+                while (last < kBandBatch && hf[last]) ++last;  // sweeps that changed something
+                sweeps += (unsigned)(last < kBandBatch ? last + 1 : kBandBatch);
+                if (last < kBandBatch) break;
+            }
+            const unsigned sw[2] = {sweeps, sweeps};
+            e = hipMemcpy(L.sel->sweeps, sw, sizeof sw, hipMemcpyHostToDevice);  // (the stream is idle here)
+            if (e != hipSuccess) return e;
+        }
+    }
     return hipGetLastError();
 }
 
@@ -747,5 +776,14 @@ hipError_t fronts_clean(double* d_T, int64_t n, FrontsCheck* chk, hipStream_t st
 }
 
 size_t bidir_join_work_bytes(int64_t n) { return layout(nullptr, n).total; }
+
+// the band relaxation's band cells and sweeps per front (after bidir_partial with a cost)
+hipError_t bidir_band_stats(const void* d_work, int64_t n, unsigned out[4], hipStream_t st) {
+    const JoinLayout L = layout(const_cast<void*>(d_work), n);
+    hipError_t e = hipMemcpyAsync(out, L.sel->nb, 2 * sizeof(unsigned), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(out + 2, L.sel->sweeps, 2 * sizeof(unsigned), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    return e;
+}
 
 }  // namespace eik

@@ -218,6 +218,7 @@ hipError_t arm_tunnel(const ArmArgs& a, hipStream_t st);
 hipError_t bidir_join(const double* d_TG, const double* d_TS, int64_t n, void* d_work, size_t work_bytes,
                       unsigned long long* d_best, hipStream_t st, int64_t* members = nullptr);
 size_t bidir_join_work_bytes(int64_t n);
+hipError_t bidir_band_stats(const void* d_work, int64_t n, unsigned out[4], hipStream_t st);
 // after bidir_join on the same work buffer: the two fields -> biComputeTmap's partial fields;
 // d_cost / d_viol (optional): flag a band cell of finite cost left +inf (capped fronts)
 hipError_t bidir_partial(double* d_TG, double* d_TS, int64_t H, int64_t W, const void* d_work,

@@ -151,7 +151,8 @@ struct eik_ctx {
     eik_fim2d* cached_fronts = nullptr;  // coarse B = 2 solver of the capped bidirectional fronts
     double fronts_cap = 1.25;          // EIK_OPT_FRONTS_CAP: cap margin (0: full fronts)
     DevBuf fronts;                     // capped fronts: coarse cost (2 maps) | coarse T (2 maps) | FrontsCheck
-    int64_t fronts_info[6] = {};       // eik_fronts_info: capped, fallback, kept G / S, members G / S
+    int64_t fronts_info[10] = {};      // eik_fronts_info: capped, fallback, kept G / S, members G / S,
+                                       // band cells G / S, band relaxation sweeps G / S
     DevBuf cm_u8, cm_i32, cm_f32, cm_f64;  // cost-builder scratch
     DevBuf arm;                            // end-effector volume scratch (arm.hip)
     int resident_l[2][5] = {};  // co-resident workgroups of fim2dl_persist_kernel<R, nl> (f32, f64)
@@ -1023,6 +1024,11 @@ static int join_and_partial(eik_ctx* c, double* dT, int64_t n, int64_t H, int64_
     HIPCHK(c, bidir_join(dT, dT + n, n, c->work.p, c->work.bytes, (unsigned long long*)c->misc.p, st, members));
     HIPCHK(c, bidir_partial(dT, dT + n, H, W, c->work.p, (const unsigned long long*)c->misc.p, st, d_cost,
                             d_chk ? &d_chk->viol : nullptr));
+    if (d_cost) {
+        unsigned bs[4] = {0, 0, 0, 0};
+        HIPCHK(c, bidir_band_stats(c->work.p, n, bs, st));
+        for (int q = 0; q < 4; ++q) c->fronts_info[6 + q] = bs[q];
+    }
     HIPCHK(c, hipMemcpyAsync(best, c->misc.p, sizeof *best, hipMemcpyDeviceToHost, st));
     if (d_chk) HIPCHK(c, hipMemcpyAsync(h_chk, d_chk, sizeof *h_chk, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));
@@ -1045,7 +1051,7 @@ static int solve_fronts(eik_ctx* c, eik_fim2d* f, double* dcost, double* dT, con
                         unsigned long long* best) {
     hipStream_t st = c->stream;
     const int64_t n = H * W;
-    for (int64_t& v : c->fronts_info) v = 0;
+    for (int64_t& v : c->fronts_info) v = 0;  // (join_and_partial fills the band entries)
     HIPCHK(c, c->work.ensure(bidir_join_work_bytes(n)));
     const bool capped = c->fronts_cap > 0 && n >= kFrontsCapCells && std::min(H, W) >= 256;
     if (capped) {
@@ -1105,9 +1111,9 @@ static int solve_fronts(eik_ctx* c, eik_fim2d* f, double* dcost, double* dT, con
     return rc;
 }
 
-int eik_fronts_info(const eik_ctx* c, int64_t out[6]) {
+int eik_fronts_info(const eik_ctx* c, int64_t out[10]) {
     if (!c || !out) return EIK_ERR_ARG;
-    for (int i = 0; i < 6; ++i) out[i] = c->fronts_info[i];
+    for (int i = 0; i < 10; ++i) out[i] = c->fronts_info[i];
     return EIK_OK;
 }
 

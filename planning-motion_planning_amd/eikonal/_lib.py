@@ -320,10 +320,10 @@ class Context:
 
     def fronts_info(self):
         """How the last tmap2d_bidir / rover_path formed its fronts (eik_fronts_info)."""
-        out = np.zeros(6, np.int64)
+        out = np.zeros(10, np.int64)
         self._chk(lib().eik_fronts_info(self._h, out))
         return {"capped": bool(out[0]), "fallback": bool(out[1]), "kept": out[2:4].tolist(),
-                "members": out[4:6].tolist()}
+                "members": out[4:6].tolist(), "band": out[6:8].tolist(), "band_sweeps": out[8:10].tolist()}
 
     def path2d(self, T, init, end, tau=0.5):
         T = np.ascontiguousarray(T, dtype=np.float64)
