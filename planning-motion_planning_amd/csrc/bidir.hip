@@ -16,18 +16,18 @@
 //              rankS(n0)), both ranks counted exactly in one pass beside a 256-bin coarse
 //              histogram of each field over [0, 4 max(TG(n0), TS(n0))) (+ one overflow bin);
 //              then n1 = argmin of the larger of the two histogram rank estimates, whose exact
-//              ranks give K1; the bound is min(K0, K1)
-//   2. select: per field the smallest value bucket holding >= K0+1 cells (coarse scan, then a
+//              ranks give K1; the bound is K = min(K0, K1)
+//   2. select: per field the smallest value bucket holding >= K+1 cells (coarse scan, then a
 //              1024-bin histogram inside that coarse bin) -> the member set {bucket(T) <=
-//              threshold}, a prefix of the field's pop order that holds every cell of rank <= K0
+//              threshold}, a prefix of the field's pop order that holds every cell of rank <= K
 //   3. rank:   compact the members in node order (stable select), radix-sort them by T rounded to
 //              float (stable: ties stay in node order), then put each run of equal floats in (T,
 //              node) order -> their exact ranks; non-members keep rank UINT_MAX
 //   4. join:   min over cells of max(rankG, rankS) as before.
-// A non-member has rank > K0 >= k*, so it can be neither the join nor a closed cell of a partial
+// A non-member has rank > K >= k*, so it can be neither the join nor a closed cell of a partial
 // field, and the members' ranks equal their ranks in the whole field (every cell below a member
 // in pop order is a member).  The bucket function is monotone in T, so the member set is a prefix.
-// The sort then covers ~K0 cells instead of H*W (the cells the fronts popped, plus one bucket).
+// The sort then covers ~K cells instead of H*W (the cells the fronts popped, plus one bucket).
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
