@@ -657,7 +657,7 @@ hipError_t bidir_partial(double* d_TG, double* d_TS, int64_t H, int64_t W, const
                 if (last < kBandBatch) break;
             }
             const unsigned sw[2] = {sweeps, sweeps};
-            e = hipMemcpy(L.sel->sweeps, sw, sizeof sw, hipMemcpyHostToDevice);  // (the stream is idle here)
+            e = hipMemcpyAsync(L.sel->sweeps, sw, sizeof sw, hipMemcpyHostToDevice, st);  // (pageable: staged now)
             if (e != hipSuccess) return e;
         }
     }
