@@ -13,7 +13,7 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke rc=$?"; exit 1; }
 fi
 timeout -k 10 600 python bench.py --dtype $D > $O/bench_$R.json 2> $O/bench_$R.err || { echo "bench rc=$?"; tail -n 20 $O/bench_$R.err; exit 1; }
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_$R -o prof -- python bench.py --dtype $D --steps 10 --warmup 2 --no-cpu-baseline --extras C5 --extra-steps 3 > $O/prof_$R.out 2> $O/prof_$R.err || { echo "prof rc=$?"; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_$R -o prof -- python bench.py --dtype $D --steps 40 --warmup 3 --no-cpu-baseline --extras C5 --extra-steps 3 > $O/prof_$R.out 2> $O/prof_$R.err || { echo "prof rc=$?"; exit 1; }
 find /tmp/prof_$R -name "*kernel_stats.csv" -exec cp {} $O/${R}_kernel_stats.csv \;
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d /tmp/pmc_fetch_$R -o f -- python bench.py --dtype $D --steps 3 --warmup 1 --no-cpu-baseline --no-path --no-timing --no-extra > $O/pmc_fetch.out 2> $O/pmc_fetch.err || { echo "pmc fetch rc=$?"; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d /tmp/pmc_write_$R -o w -- python bench.py --dtype $D --steps 3 --warmup 1 --no-cpu-baseline --no-path --no-timing --no-extra > $O/pmc_write.out 2> $O/pmc_write.err || { echo "pmc write rc=$?"; exit 1; }
