@@ -39,9 +39,11 @@ from eikonal import _lib as L  # noqa: E402
 METRIC = "Eikonal Gcells/s + ms-to-path, 4k² & 16k² costmap at 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 # per element byte: cost read + T read + T write + halo read per full visit; T write + halo
-# re-read per in-place pass (x 4 for fp32, x 8 for fp64)
+# re-read per in-place pass (x 4 for fp32, x 8 for fp64); a tile's first visit reads no T (its T is
+# still +inf: eik_stats.fresh_visits, fim2d.hip kFreshSkip)
 CELLS_PER_VISIT = 3 * 64 * 64 + 4 * 64
 CELLS_PER_PASS = 64 * 64 + 4 * 64
+CELLS_T_READ = 64 * 64
 WIDE_TILES = 16384  # fp32 maps of >= this many tiles run the 4-waves-per-SIMD kernel (csrc kWideTiles)
 
 
@@ -168,7 +170,7 @@ def main():
         """K steps between barrier + synchronize; returns (max-over-ranks seconds, visits, passes,
         sweep_ms, launches)."""
         ctx.set_option(L.OPT_TIMING, 1 if instrument else 0)
-        visits, passes, sweep_ms, iters = 0, 0, 0.0, 0
+        visits, passes, fresh, sweep_ms, iters = 0, 0, 0, 0.0, 0
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -179,6 +181,7 @@ def main():
                 s = fim.stats()
                 visits += s["tile_visits"]
                 passes += s["inplace_passes"]
+                fresh += s["fresh_visits"]
                 sweep_ms += s["sweep_ms"]
                 iters += s["iterations"]
         torch.cuda.synchronize()
@@ -190,12 +193,12 @@ def main():
             tt = torch.tensor([el], dtype=torch.float64)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=ctrl)
             el = tt.item()
-        return el, visits, passes, sweep_ms, iters
+        return el, visits, passes, fresh, sweep_ms, iters
 
     # 1) the measurement: no per-launch instrumentation inside the timed region
-    el, _, _, _, _ = timed(False)
+    el, _, _, _, _, _ = timed(False)
     # 2) the same K steps again with a hipEvent pair around every sweep launch (roofline)
-    el_i, visits, passes, sweep_ms, iters = (0.0, 0, 0, 0.0, 0) if args.no_timing else timed(True)
+    el_i, visits, passes, fresh, sweep_ms, iters = (0.0, 0, 0, 0, 0.0, 0) if args.no_timing else timed(True)
 
     if world > 1:  # the halo transport delivered every final edge (a wrong field cannot pass)
         dd_ok = dd.halo_consistent(blk, T, ghost, group=ctrl)
@@ -210,7 +213,7 @@ def main():
 
     # roofline of the dominant kernel (rank-local: this rank's launches and its event time)
     launches = iters
-    alg_bytes = esz * (visits * CELLS_PER_VISIT + passes * CELLS_PER_PASS)
+    alg_bytes = esz * (visits * CELLS_PER_VISIT - fresh * CELLS_T_READ + passes * CELLS_PER_PASS)
     achieved = (alg_bytes / (sweep_ms * 1e-3) / 1e9) if sweep_ms > 0 else None
     traffic = None
     wide = not f64 and ((blk.h + 63) // 64) * ((blk.w + 63) // 64) >= WIDE_TILES
@@ -239,6 +242,7 @@ def main():
         "launches_per_solve": round(launches / args.steps, 1),
         "tile_visits_per_solve": round(visits / args.steps, 1),
         "inplace_passes_per_solve": round(passes / args.steps, 1),
+        "fresh_visits_per_solve": round(fresh / args.steps, 1),
     }
 
     out = {
@@ -509,7 +513,8 @@ def bench_c2(ctx, dev, stream, cost, goal, steps, dtype):
     st = fim.stats()
     ctx.set_option(L.OPT_TIMING, 0)
     esz = 8 if f64 else 4
-    alg = esz * (st["tile_visits"] * CELLS_PER_VISIT + st["inplace_passes"] * CELLS_PER_PASS)
+    alg = esz * (st["tile_visits"] * CELLS_PER_VISIT - st["fresh_visits"] * CELLS_T_READ
+                 + st["inplace_passes"] * CELLS_PER_PASS)
     fim.close()
     del c, T
     torch.cuda.empty_cache()

@@ -62,6 +62,8 @@ typedef struct {
     double bytes_alg;     /* algorithmic bytes of the sweep launches (tile_visits x bytes/visit) */
     int64_t inplace_passes; /* persistent mode: extra in-place passes of busy tiles (halo refresh
                                + sweep + write-back of the tile already in LDS)                 */
+    int64_t fresh_visits; /* persistent mode: tile visits (among tile_visits) that read no T --
+                             the tile's first visit, T still +inf (bytes_alg counts them so)    */
 } eik_stats;
 
 /* options (eik_set_option) */

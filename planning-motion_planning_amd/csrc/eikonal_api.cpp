@@ -424,7 +424,7 @@ static int fim2d_create_rows(eik_ctx* c, int64_t B, int64_t H, int64_t W, int dt
         (e = f->edge.ensure(sizeof(unsigned) * 4)) != hipSuccess || (e = f->goals.ensure(sizeof(int64_t) * 2 * B)) != hipSuccess ||
         (e = f->ecol.ensure((dtype == EIK_F64 ? 8 : 4) * 2 * kTile * (size_t)tiles)) != hipSuccess ||
         (e = hipHostMalloc((void**)&f->h_counts, sizeof(int) * 64)) != hipSuccess ||
-        (e = hipHostMalloc((void**)&f->h_visits, 2 * sizeof(unsigned long long))) != hipSuccess ||
+        (e = hipHostMalloc((void**)&f->h_visits, 3 * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipHostMalloc((void**)&f->h_goals, sizeof(int64_t) * 2 * B)) != hipSuccess ||
         (e = hipEventCreate(&f->ev_start)) != hipSuccess || (e = hipEventCreate(&f->ev_stop)) != hipSuccess) {
         eik_fim2d_destroy(f);
@@ -673,11 +673,11 @@ static int finish_solve(eik_fim2d* f, int64_t* active) {
     HIPCHK(c, hipEventRecord(f->ev_stop, f->stream));
     const bool persist = f->a.mode == kModePersistent;  // h_q (queued after the launch) holds the counters
     if (!persist)
-        HIPCHK(c, hipMemcpyAsync(f->h_visits, (void*)f->a.visits, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+        HIPCHK(c, hipMemcpyAsync(f->h_visits, (void*)f->a.visits, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                                  f->stream));
     HIPCHK(c, wait_stream(f->stream));
     ++f->host_syncs;
-    if (persist) memcpy(f->h_visits, (const char*)f->h_q + kVisitsOff, 2 * sizeof(unsigned long long));
+    if (persist) memcpy(f->h_visits, (const char*)f->h_q + kVisitsOff, 3 * sizeof(unsigned long long));
     if (c->timing) drain_timing(f);
     float ms = 0.f;
     (void)hipEventElapsedTime(&ms, f->ev_start, f->ev_stop);
@@ -916,7 +916,7 @@ int eik_fim2d_stats(eik_fim2d* f, eik_stats* out) {
     if (!f || !out) return EIK_ERR_ARG;
     if (f->started) {
         eik_ctx* c = f->ctx;
-        HIPCHK(c, hipMemcpyAsync(f->h_visits, (void*)f->a.visits, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+        HIPCHK(c, hipMemcpyAsync(f->h_visits, (void*)f->a.visits, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                                  f->stream));
         HIPCHK(c, hipStreamSynchronize(f->stream));
     }
@@ -931,7 +931,9 @@ static void fill_stats(const eik_fim2d* f, eik_stats* out) {
     out->host_syncs = f->host_syncs;
     out->solve_ms = f->solve_ms;
     out->sweep_ms = f->sweep_ms;
-    out->bytes_alg = (double)out->tile_visits * bytes_per_visit(f->f64) +
+    out->fresh_visits = (int64_t)f->h_visits[2];
+    out->bytes_alg = (double)out->tile_visits * bytes_per_visit(f->f64) -
+                     (double)out->fresh_visits * kTile * kTile * (f->f64 ? 8 : 4) +
                      (double)out->inplace_passes * bytes_per_pass(f->f64) +
                      (double)f->B * f->H * f->W * (f->f64 ? 8 : 4);
 }
@@ -1284,12 +1286,12 @@ static int solve_layered(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, i
     const int grid = std::min(c->grid > 0 ? c->grid : 4 * c->cu_count, res);
     a.fresh_first = c->fresh_first;
     HIPCHK(c, hipEventRecord(f->ev_start, st));
-    HIPCHK(c, hipMemsetAsync((void*)f->a.visits, 0, 2 * sizeof(unsigned long long), st));
+    HIPCHK(c, hipMemsetAsync((void*)f->a.visits, 0, 3 * sizeof(unsigned long long), st));
     HIPCHK(c, fim2dl_init(a, f64, goal[0], goal[1], goal[2], st));
     HIPCHK(c, fim2dl_persist(a, nl, f64, grid, st));
     HIPCHK(c, hipEventRecord(f->ev_stop, st));
     HIPCHK(c, hipMemcpyAsync(f->h_q, f->qctl.p, kQueueCtlBytes, hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipMemcpyAsync(f->h_visits, (void*)f->a.visits, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(f->h_visits, (void*)f->a.visits, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));
     const unsigned err = f->h_q[192 / 4];
     if (err & 1u)
@@ -1303,6 +1305,7 @@ static int solve_layered(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, i
     c->last.iterations = 1;
     c->last.tile_visits = (int64_t)f->h_visits[0];
     c->last.inplace_passes = (int64_t)f->h_visits[1];
+    c->last.fresh_visits = 0;  // the layered kernel always reads T
     c->last.host_syncs = 1;
     c->last.solve_ms = ms;
     // per visit: cost + T read and T write of the tile's nl layers plus the halo ring; per in-place

@@ -102,6 +102,16 @@ constexpr int kActStep = EIK_ACT_STEP;
 template <typename R>
 constexpr bool kEcol = sizeof(R) == 8 ? EIK_ECOL_F64 : EIK_ECOL_F32;
 
+// EIK_FRESH_SKIP: a persistent visit of a tile no visit has written yet (its grab's exchange
+// returns the state without kVisited) stages only the cost: its T is the init kernel's +inf.
+// Every writer of a full tile's T outside a visit is the init kernel or the seed kernel, and the
+// seed kernel queues its tile as visited.  (Cut tiles, whose ghost cells come from load_T, always
+// read T.)
+#ifndef EIK_FRESH_SKIP
+#define EIK_FRESH_SKIP 1
+#endif
+constexpr bool kFreshSkip = EIK_FRESH_SKIP;
+
 // ------------------------------------------------------------------------- quadrant sweep
 // A tile cell in LDS: arrival time and cost side by side, so one ds_read_b64 (fp32) fetches both.
 template <typename R>
@@ -267,6 +277,7 @@ struct TileLds {
     unsigned key[5];    // min new value entering: self, N, S, W, E (f32 bits; ordered mode)
     int defer, tile, last;
     unsigned dirs;      // quadrant sweeps of this visit (bit w: wave w's direction)
+    unsigned fresh;     // persistent mode: the tile's first visit (kFreshSkip)
 };
 
 // ---------------------------------------------------------------------------- tile body
@@ -361,7 +372,27 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
         }
         Ts[h] = make_cell<R>(hv, INF, hcol);
     };
-    if (full) {
+    if (full && COH && kFreshSkip && __builtin_amdgcn_readfirstlane(L.fresh)) {
+        // a tile's first visit: T is still the init kernel's +inf (the seed kernel marks the goal
+        // tile visited), so only the cost is read
+        R cr[16];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t gy = y0 + (tid >> 4) + 16 * k;
+            if constexpr (sizeof(R) == 4) {
+                const float4 c4 = *reinterpret_cast<const float4*>(&cost[gy * a.W + x0 + cx]);
+                cr[4 * k] = c4.x; cr[4 * k + 1] = c4.y; cr[4 * k + 2] = c4.z; cr[4 * k + 3] = c4.w;
+            } else {
+                const double2 c0 = *reinterpret_cast<const double2*>(&cost[gy * a.W + x0 + cx]);
+                const double2 c1 = *reinterpret_cast<const double2*>(&cost[gy * a.W + x0 + cx + 2]);
+                cr[4 * k] = c0.x; cr[4 * k + 1] = c0.y; cr[4 * k + 2] = c1.x; cr[4 * k + 3] = c1.y;
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) told[4 * k + e] = INF;
+        }
+        store_tile(cr, load_halo());
+        if (tid == 0) atomicAdd(a.visits + 2, 1ull);  // eik_stats::fresh_visits (the byte model)
+    } else if (full) {
         R cr[16];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -785,6 +816,7 @@ __global__ __launch_bounds__(kThreads, WPS) void fim2d_persist_kernel(Fim2dArgs 
             const int t = qgrab(a, trig);
             L.tile = t;
             L.dirs = sweep_dirs(trig);
+            L.fresh = !(trig & kVisited);
             if (t >= 0) EIK_VISIT(t, trig, L.dirs);
         }
         __syncthreads();
@@ -811,9 +843,9 @@ __global__ void fim2d_init_kernel(R* __restrict__ T, int64_t n, unsigned* __rest
         if (qctl) qctl[t] = 0u;
         if (t < 4) {
             if (counts) counts[t] = 0u;
-            if (visits) visits[t] = 0u;
             if (edge) edge[t] = 0u;
         }
+        if (t < 6 && visits) visits[t] = 0u;  // full visits, in-place passes, fresh visits (u64 each)
     }
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) T[i] = Real<R>::inf();
     if (ecol)
@@ -844,7 +876,7 @@ __global__ void fim2d_seed_kernel(Fim2dArgs a, const int64_t* __restrict__ goals
     if (kEcol<R> && a.ecol && (gx % kTile == 0 || gx % kTile == kTile - 1))  // the edge columns' copy
         static_cast<R*>(a.ecol)[((int64_t)tile * 2 + (gx % kTile == 0 ? 0 : 1)) * kTile + gy % kTile] = R(0);
     if (a.mode == kModePersistent) {
-        qpush(a, tile, kSelf);
+        qpush(a, tile, kSelf | kVisited);  // visited: its T is not all +inf (kFreshSkip)
         return;
     }
     a.mark[tile] = 1;  // enqueued for iteration 0

@@ -48,7 +48,8 @@ class ArmVolume(C.Structure):
 
 class EikStats(C.Structure):
     _fields_ = [("iterations", i64), ("tile_visits", i64), ("host_syncs", i64), ("solve_ms", C.c_double),
-                ("sweep_ms", C.c_double), ("bytes_alg", C.c_double), ("inplace_passes", i64)]
+                ("sweep_ms", C.c_double), ("bytes_alg", C.c_double), ("inplace_passes", i64),
+                ("fresh_visits", i64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -216,6 +216,29 @@ def test_stats_count_visits(ctx):
     assert s["tile_visits"] >= 64 and s["iterations"] >= 1 and s["solve_ms"] > 0
 
 
+@pytest.mark.parametrize("shape,f64", [((512, 512), False), ((512, 512), True), ((300, 500), True)])
+def test_fresh_visits_read_no_T(ctx, shape, f64):
+    """A persistent visit of a full tile nobody has written yet stages only the cost (fim2d.hip
+    kFreshSkip): on a uniform raster every full tile but the goal's is first visited that way,
+    exactly once, and the byte model leaves out their T reads.  (List mode always reads T.)"""
+    from eikonal import _lib as L
+    H, W = shape
+    dt = np.float64 if f64 else np.float32
+    c = np.ones(shape, dt)
+    goal = [256, 256]
+    T = ctx.tmap2d(c, goal, dtype=dt)
+    s = ctx.stats()
+    persistent = s["iterations"] == 1
+    full = (H // 64) * (W // 64)
+    goal_full = goal[1] // 64 < H // 64 and goal[0] // 64 < W // 64
+    assert s["fresh_visits"] == ((full - goal_full) if persistent else 0)
+    esz = 8 if f64 else 4
+    alg = esz * (s["tile_visits"] * (3 * 4096 + 256) - s["fresh_visits"] * 4096 + s["inplace_passes"] * (4096 + 256)
+                 + H * W)
+    assert s["bytes_alg"] == alg
+    check_field(T, oracle_field(c, goal), goal, f64)
+
+
 @pytest.mark.parametrize("passes", [1, 2, 8, 16])
 def test_pass_cap_option(passes):
     """EIK_OPT_PASSES (in-place passes per persistent visit) changes the schedule, not the field:
