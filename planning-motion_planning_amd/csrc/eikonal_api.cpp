@@ -1305,14 +1305,15 @@ static int solve_layered(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, i
     c->last.iterations = 1;
     c->last.tile_visits = (int64_t)f->h_visits[0];
     c->last.inplace_passes = (int64_t)f->h_visits[1];
-    c->last.fresh_visits = 0;  // the layered kernel always reads T
+    c->last.fresh_visits = (int64_t)f->h_visits[2];
     c->last.host_syncs = 1;
     c->last.solve_ms = ms;
-    // per visit: cost + T read and T write of the tile's nl layers plus the halo ring; per in-place
-    // pass: T write + halo
+    // per visit: cost + T read and T write of the tile's nl layers plus the halo ring (a first
+    // visit reads no T); per in-place pass: T write + halo
     const double esz = f64 ? 8.0 : 4.0;
     c->last.bytes_alg = esz * nl *
-                        ((double)c->last.tile_visits * (3.0 * kTile * th + 2.0 * (kTile + th)) +
+                        ((double)c->last.tile_visits * (3.0 * kTile * th + 2.0 * (kTile + th)) -
+                         (double)c->last.fresh_visits * kTile * th +
                          (double)c->last.inplace_passes * (1.0 * kTile * th + 2.0 * (kTile + th))) +
                         esz * H * W * L;
     return EIK_OK;

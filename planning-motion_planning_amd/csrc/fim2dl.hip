@@ -50,6 +50,13 @@ template <> struct LCell<double> {
 #endif
 template <typename R> constexpr int kRowsOf = sizeof(R) == 4 ? kTile : EIK_L64_ROWS;
 
+// EIK_FRESH_SKIP_L: a full tile's first visit stages only the cost -- its T layers are still the init
+// kernel's +inf (the seed kernel queues the goal's tile as visited), as fim2d.hip's kFreshSkip
+#ifndef EIK_FRESH_SKIP_L
+#define EIK_FRESH_SKIP_L 1
+#endif
+constexpr bool kFreshSkipL = EIK_FRESH_SKIP_L;
+
 template <typename R, int TH>
 struct TileLdsL {
     LCell<R> Tbuf[(TH + 2 + 2 * kGuard) * kLds];  // tile + halo ring ((TH+2) x 66 at offset kGuard * kLds), guard
@@ -59,6 +66,7 @@ struct TileLdsL {
     unsigned key[5];
     int tile;
     unsigned dirs;
+    unsigned fresh;  // the tile's first visit (kFreshSkipL)
 };
 // A sweep's 4-step group spans rows [-(kAhead - 1), TH + 1 + kAhead - 1]: every row it reads (T
 // and cost alike) is inside the guard rows of both arrays, and a guard row's +inf cost keeps its T
@@ -312,7 +320,20 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
         if constexpr (sizeof(R) == 8) return (c >= R(0) && c < 0x1p-500) ? R(0x1p-500) : c;  // NaN stays NaN
         else return c;
     };
-    if (y0 + TH <= a.H && x0 + kTile <= a.W) {  // full tile: no per-cell range test
+    if (COH && kFreshSkipL && y0 + TH <= a.H && x0 + kTile <= a.W && __builtin_amdgcn_readfirstlane(L.fresh)) {
+        R cc[NJ][NL];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int64_t gi = ((y0 + wave + 4 * j) * a.W + x0 + lane) * ls + a.z0;
+#pragma unroll
+            for (int z = 0; z < NL; ++z) {
+                told[j][z] = INF;
+                cc[j][z] = scost(cost[gi + z]);
+            }
+        }
+        store_tile(cc, load_halo());
+        if (tid == 0) atomicAdd(a.visits + 2, 1ull);  // eik_stats::fresh_visits
+    } else if (y0 + TH <= a.H && x0 + kTile <= a.W) {  // full tile: no per-cell range test
         R cc[NJ][NL];
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
@@ -444,6 +465,7 @@ __global__ __launch_bounds__(kThreads) void fim2dl_persist_kernel(Fim2dArgs a) {
             const int t = qgrab(a, trig);
             L.tile = t;
             L.dirs = sweep_dirs(trig);
+            L.fresh = !(trig & kVisited);
         }
         __syncthreads();
         tile = __builtin_amdgcn_readfirstlane(L.tile);
@@ -467,7 +489,7 @@ template <typename R>
 __global__ void fim2dl_seed_kernel(Fim2dArgs a, int64_t gx, int64_t gy, int64_t gz, int th) {
     static_cast<R*>(a.T)[(gy * a.W + gx) * a.ls + gz] = R(0);
     __threadfence();
-    qpush(a, (int)(gy / th) * a.ntx + (int)(gx / kTile), kSelf);
+    qpush(a, (int)(gy / th) * a.ntx + (int)(gx / kTile), kSelf | kVisited);  // T not all +inf
 }
 
 __global__ void fim2dl_rewind_kernel(Fim2dArgs a) { *a.qhead = *a.qtail; }
