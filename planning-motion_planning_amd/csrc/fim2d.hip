@@ -104,8 +104,10 @@ constexpr bool kEcol = sizeof(R) == 8 ? EIK_ECOL_F64 : EIK_ECOL_F32;
 
 // EIK_FRESH_SKIP: a persistent visit of a tile no visit has written yet (its grab's exchange
 // returns the state without kVisited) stages only the cost: its T is the init kernel's +inf.
-// Every writer of a full tile's T outside a visit is the init kernel or the seed kernel, and the
-// seed kernel queues its tile as visited.  (Cut tiles, whose ghost cells come from load_T, always
+// Between a solve's init and its end, the only writers of a full tile's T outside a visit are the
+// init kernel and the seed kernel, and the seed kernel queues its tile as visited (the kernels that
+// rewrite T afterwards -- bidir.hip's partial fields and cap clean-up -- run after the solve, and
+// the next solve starts with the init).  (Cut tiles, whose ghost cells come from load_T, always
 // read T.)
 #ifndef EIK_FRESH_SKIP
 #define EIK_FRESH_SKIP 1
