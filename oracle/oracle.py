@@ -11,7 +11,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liboracle.so")
+# ORACLE_LIB: tools/san.sh points it at the ASan/UBSan build (`make -C oracle san`)
+LIB_PATH = os.environ.get("ORACLE_LIB", os.path.join(HERE, "liboracle.so"))
 
 OK, ERR_ARG, ERR_NOMEM = 0, -1, -2
 REF_STOPITERATION, REF_UNBOUND, REF_VALUEERROR, REF_INDEXERROR = 2, 3, 4, 5

@@ -83,11 +83,33 @@ def _share_hip_runtime():
             C.CDLL(p, mode=C.RTLD_GLOBAL)
 
 
+# Sanitizer runs only (tools/san.sh): EIKONAL_HOST_LIB names an ASan/UBSan build of the
+# host-only sources (dem_io.cpp, rover.cpp, node_sync.cpp: `make -C csrc san`), and lib() then binds
+# just their entry points from it -- no HIP runtime in the process, nothing of the GPU path.
+HOST_LIB = os.environ.get("EIKONAL_HOST_LIB")
+
+
+def _bind_host(L):
+    P = C.POINTER
+    L.eik_load_dem_txt.argtypes = [C.c_char_p, vp, i64, P(i64), P(i64), C.c_int]
+    L.eik_io_last_error.restype = C.c_char_p
+    L.eik_node_allreduce.argtypes = [vp, C.c_int, C.c_int, C.c_uint64, i64, P(i64), C.c_double]
+    L.eik_node_shm_open.argtypes = [C.c_char_p, i64, C.c_int, P(vp)]
+    L.eik_node_shm_close.argtypes = [vp, i64]
+    L.eik_node_shm_unlink.argtypes = [C.c_char_p]
+    L.eik_rover_assemble.argtypes = [_f64p, i64, _f64p, i64, _f64p, i64, i64, P(RoverQuery), _f64p, _f64p, i64,
+                                     P(i64)]
+
+
 def lib():
     """Load libeikonal.so; raise (never fall back) when it is absent."""
     global _lib
     with _lock:
         if _lib is not None:
+            return _lib
+        if HOST_LIB:
+            _lib = C.CDLL(HOST_LIB)
+            _bind_host(_lib)
             return _lib
         if not os.path.exists(LIB_PATH):
             raise EikError(EIK_ERR_NODEVICE, f"{LIB_PATH} not built (run __graft_entry__.build())")
@@ -265,6 +287,7 @@ class Context:
         if getattr(self, "_h", None):
             lib().eik_destroy(self._h)
             self._h = None
+            release_pinned()  # the recycled result blocks (bounded, and freed here)
 
     def __del__(self):
         try:
@@ -556,8 +579,22 @@ class Fim2d:
 # is gone, then the block goes back to the pool (hipHostMalloc of 128 MiB costs milliseconds).
 PINNED_MIN_BYTES = 16 << 20  # below this the ABI copies directly anyway
 _pin_lock = threading.Lock()
-_pin_free = {}  # nbytes -> [ptr, ...]
-_PIN_POOL_MAX = 8  # free blocks kept per size
+_pin_free = {}  # nbytes -> [ptr, ...], oldest first
+_PIN_POOL_BYTES = 512 << 20  # free blocks kept, all sizes together (e.g. four 4096^2 float64 fields)
+
+
+def _pool_bytes():
+    return sum(n * len(v) for n, v in _pin_free.items())
+
+
+def release_pinned():
+    """Give every recycled page-locked block back to the runtime (blocks still held by live
+    arrays return to the pool when their arrays go; Context.close() calls this)."""
+    with _pin_lock:
+        ptrs = [p for v in _pin_free.values() for p in v]
+        _pin_free.clear()
+    for p in ptrs:
+        lib().eik_host_free(p)
 
 
 class _PinnedBlock:
@@ -575,12 +612,20 @@ class _PinnedBlock:
 
     def __del__(self):
         try:
+            evict = []
             with _pin_lock:
-                free = _pin_free.setdefault(self.nbytes, [])
-                if len(free) < _PIN_POOL_MAX:
-                    free.append(self.ptr)
-                    return
-            lib().eik_host_free(self.ptr)
+                if self.nbytes > _PIN_POOL_BYTES:
+                    evict.append(self.ptr)
+                else:
+                    _pin_free.setdefault(self.nbytes, []).append(self.ptr)
+                    # over the byte budget: free the oldest blocks of the other sizes first
+                    while _pool_bytes() > _PIN_POOL_BYTES:
+                        n = next((k for k, v in _pin_free.items() if v and k != self.nbytes), self.nbytes)
+                        evict.append(_pin_free[n].pop(0))
+                        if not _pin_free[n]:
+                            del _pin_free[n]
+            for p in evict:
+                lib().eik_host_free(p)
         except Exception:
             pass
 
