@@ -52,6 +52,7 @@ struct JoinSel {
     unsigned m[2];          // member count per field (select output)
     unsigned nb[2];         // band cells listed for the band relaxation (bidir_partial with a cost)
     unsigned sweeps[2];     // the band relaxation's sweeps
+    unsigned longrun[2];    // a run of equal float keys longer than kFixupRun: sort that field by 64-bit keys
     unsigned long long n1;  // rank-aware seed: (estimated max rank) << 29 | node; ~0: none
     unsigned r1[2];         // exact ranks of n1
     unsigned pre[2][kCoarse];  // cells below each coarse bucket
@@ -366,13 +367,21 @@ __global__ void join_gather_kernel(const double* __restrict__ T, const unsigned*
 
 // After the stable sort by float key (ties in node order): each run of equal float keys is put in
 // (T, node) order -- insertion sort by its first thread.  Runs are short (cells whose T agree to
-// float precision); runs of exactly equal T are already in node order, so they cost one pass.
+// float precision); runs of exactly equal T are already in node order, so they cost one pass.  A
+// run longer than kFixupRun (e.g. a zero-cost region, whose distinct T of ~2^-500 all round to the
+// float 0) is left alone and flags the field (longrun): bidir_join then sorts that field again by
+// the doubles' 64-bit patterns, so no run costs a quadratic insertion sort on one thread.
+constexpr int64_t kFixupRun = 1024;
 __global__ void join_fixup_kernel(const double* __restrict__ T, const unsigned* __restrict__ key, int64_t m,
-                                  unsigned* __restrict__ idx) {
+                                  unsigned* __restrict__ idx, unsigned* __restrict__ longrun) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j + 1 >= m || key[j + 1] != key[j] || (j > 0 && key[j - 1] == key[j])) return;  // run starts only
     int64_t e = j + 2;
-    while (e < m && key[e] == key[j]) ++e;
+    while (e < m && key[e] == key[j] && e - j <= kFixupRun) ++e;
+    if (e - j > kFixupRun) {
+        atomicOr(longrun, 1u);
+        return;
+    }
     for (int64_t a = j + 1; a < e; ++a) {
         const unsigned ia = idx[a];
         const double ta = T[ia];
@@ -386,6 +395,16 @@ __global__ void join_fixup_kernel(const double* __restrict__ T, const unsigned* 
         }
         idx[b + 1] = ia;
     }
+}
+
+// the fallback's keys: the doubles' bit patterns (T >= 0: they order as unsigned), exact
+__global__ void join_gather64_kernel(const double* __restrict__ T, const unsigned* __restrict__ list, int64_t m,
+                                     unsigned long long* __restrict__ keys, unsigned* __restrict__ idx) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    const unsigned i = list[j];
+    keys[j] = (unsigned long long)__double_as_longlong(T[i]);
+    idx[j] = i;
 }
 
 // rank[sorted_idx[k]] = k for the members; every other cell keeps UINT_MAX (memset)
@@ -528,9 +547,32 @@ hipError_t bidir_join(const double* d_TG, const double* d_TS, int64_t n, void* d
             e = hipcub::DeviceRadixSort::SortPairs(L.cub_tmp, b, k32_in, k32_out, L.i_in, L.i_out, (int)m, 0, 32, st);
             if (e != hipSuccess) return e;
             const unsigned g = (unsigned)((m + 255) / 256);
-            hipLaunchKernelGGL(join_fixup_kernel, dim3(g), dim3(256), 0, st, T[f], k32_out, m, L.i_out);
+            hipLaunchKernelGGL(join_fixup_kernel, dim3(g), dim3(256), 0, st, T[f], k32_out, m, L.i_out,
+                               &sel->longrun[f]);
             hipLaunchKernelGGL(scatter_rank_kernel, dim3(g), dim3(256), 0, st, L.i_out, m, rank[f]);
         }
+    }
+    // a field with a run of equal float keys too long for the fix-up: its members again (the select
+    // is stable and deterministic: the same list), sorted by the 64-bit patterns, ranks re-scattered
+    unsigned lr[2] = {0, 0};
+    e = hipMemcpyAsync(lr, sel->longrun, sizeof lr, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return e;
+    for (int f = 0; f < 2; ++f) {
+        const int64_t m = hm[f];
+        if (!lr[f] || m <= 0) continue;
+        size_t b = L.cub_bytes;
+        e = hipcub::DeviceSelect::If(L.cub_tmp, b, hipcub::CountingInputIterator<unsigned>(0u), L.i_in, &sel->m[f], n,
+                                     JoinMember{T[f], sel, f}, st);
+        if (e != hipSuccess) return e;
+        const unsigned g = (unsigned)((m + 255) / 256);
+        hipLaunchKernelGGL(join_gather64_kernel, dim3(g), dim3(256), 0, st, T[f], L.i_in, m, L.k_in, L.i_in);
+        b = L.cub_bytes;
+        e = hipcub::DeviceRadixSort::SortPairs(L.cub_tmp, b, L.k_in, L.k_out, L.i_in, L.i_out, (int)m, 0, 64, st);
+        if (e != hipSuccess) return e;
+        e = hipMemsetAsync(rank[f], 0xFF, sizeof(unsigned) * (size_t)n, st);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(scatter_rank_kernel, dim3(g), dim3(256), 0, st, L.i_out, m, rank[f]);
     }
     e = hipMemsetAsync(d_best, 0xFF, sizeof(unsigned long long), st);
     if (e != hipSuccess) return e;
@@ -572,7 +614,9 @@ __global__ void bidir_partial_kernel(double* __restrict__ T, const unsigned* __r
         T[i] = Real<double>::inf();
         return;
     }
-    if (viol && !fin(T[i]) && fin(cost[i])) atomicOr(viol, 1u);
+    // (with a band list the value is recomputed from the closed cells below, so a cut-off value
+    // does not survive and needs no fallback: the check is for the full-field band values only)
+    if (viol && !blist && !fin(T[i]) && fin(cost[i])) atomicOr(viol, 1u);
     if (blist && fin(cost[i])) {
         // relaxed by bidir_band_kernel from the update over its closed neighbours alone (an upper
         // bound of the fixed point, already equal to it where the upwind neighbours are closed);
@@ -641,7 +685,11 @@ hipError_t bidir_partial(double* d_TG, double* d_TS, int64_t H, int64_t W, const
             unsigned* flags = L.i_in;  // free after the join
             const unsigned g = (unsigned)((cnt + 255) / 256);
             unsigned sweeps = 0;
-            for (int batch = 0; batch < kBandMaxBatches; ++batch) {
+            bool converged = false;
+            // a sweep in place finalises every cell whose dependency chain through the band is no
+            // longer than the sweeps so far, and no chain is longer than the band: cnt sweeps suffice
+            const int64_t max_batches = std::min<int64_t>(kBandMaxBatches, cnt / kBandBatch + 2);
+            for (int64_t batch = 0; batch < max_batches; ++batch) {
                 e = hipMemsetAsync(flags, 0, sizeof(unsigned) * kBandBatch, st);
                 if (e != hipSuccess) return e;
                 for (int q = 0; q < kBandBatch; ++q)
@@ -654,11 +702,17 @@ hipError_t bidir_partial(double* d_TG, double* d_TS, int64_t H, int64_t W, const
                 int last = 0;
                 while (last < kBandBatch && hf[last]) ++last;  // sweeps that changed something
                 sweeps += (unsigned)(last < kBandBatch ? last + 1 : kBandBatch);
-                if (last < kBandBatch) break;
+                if (last < kBandBatch) {
+                    converged = true;
+                    break;
+                }
             }
             const unsigned sw[2] = {sweeps, sweeps};
             e = hipMemcpyAsync(L.sel->sweeps, sw, sizeof sw, hipMemcpyHostToDevice, st);  // (pageable: staged now)
             if (e != hipSuccess) return e;
+            // not settled within the bound (never on valid input): the caller reports it as
+            // EIK_ERR_NOCONVERGE instead of returning unrelaxed band values
+            if (!converged) return hipErrorNotReady;
         }
     }
     return hipGetLastError();

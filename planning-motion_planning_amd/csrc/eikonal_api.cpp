@@ -229,8 +229,11 @@ static int bytes_per_pass(bool f64) { return (f64 ? 8 : 4) * (kTile * kTile + 4 
 // threads overlapped with the DMA of the other chunk.  A pageable hipMemcpyAsync of a FRESH host
 // buffer (every numpy array the drop-in receives or returns) ran at ~8 GB/s: 16 ms per 128 MiB,
 // 3 ms only once the runtime had seen the buffer; staged: ~4 ms either way (tools/h2d_probe.cpp).
-// host_to_dev returns once the source has been read (the DMA of the last chunk may still run on
-// st); dev_to_host returns with the data in dst (it waits for st's earlier work).
+// Staged (pageable) buffers: host_to_dev returns once the source has been read (the DMA of the last
+// chunk may still run on st); dev_to_host returns with the data in dst (it waits for st's earlier
+// work).  A buffer wholly inside a pinned block (eik_host_alloc) goes as ONE hipMemcpyAsync on st
+// and both return at once: the source must stay unchanged, and dst is valid, only after st is
+// synchronised -- every caller synchronises st before it returns to its own caller.
 constexpr size_t kStageChunk = 8ull << 20;
 // pinned host blocks handed out by eik_host_alloc: a copy wholly inside one goes as one DMA
 static std::mutex g_pin_mu;
@@ -1024,8 +1027,13 @@ static int join_and_partial(eik_ctx* c, double* dT, int64_t n, int64_t H, int64_
     HIPCHK(c, c->work.ensure(bidir_join_work_bytes(n)));
     HIPCHK(c, c->misc.ensure(64));
     HIPCHK(c, bidir_join(dT, dT + n, n, c->work.p, c->work.bytes, (unsigned long long*)c->misc.p, st, members));
-    HIPCHK(c, bidir_partial(dT, dT + n, H, W, c->work.p, (const unsigned long long*)c->misc.p, st, d_cost,
-                            d_chk ? &d_chk->viol : nullptr));
+    {
+        const hipError_t e = bidir_partial(dT, dT + n, H, W, c->work.p, (const unsigned long long*)c->misc.p, st, d_cost,
+                                           d_chk ? &d_chk->viol : nullptr);
+        if (e == hipErrorNotReady)
+            return set_err(c, EIK_ERR_NOCONVERGE, "biComputeTmap: the band relaxation of the partial fields did not settle");
+        HIPCHK(c, e);
+    }
     if (d_cost) {
         unsigned bs[4] = {0, 0, 0, 0};
         HIPCHK(c, bidir_band_stats(c->work.p, n, bs, st));

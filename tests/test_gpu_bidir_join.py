@@ -105,6 +105,16 @@ def make(case, rng):
         TG = np.floor(cone(H, W, 150, 120, rng)) + 1e-9 * rng.random((H, W))
         TS = np.floor(cone(H, W, 30, 40, rng)) + 1e-9 * rng.random((H, W))
         TG[120, 150] = TS[40, 30] = 0.0
+    elif case == "zero_cost_patch":  # a zero-cost region around the goal -- ~1e5 distinct
+        # T of ~2^-500 (the fp64 solver's staged cost floor) all round to the float 0, one run of
+        # equal 32-bit keys in no node order: the fix-up hands the field to the 64-bit sort
+        H, W = 400, 400
+        TG = cone(H, W, 200, 200, rng, 0.3) + 1.0
+        yy, xx = np.mgrid[0:H, 0:W]
+        patch = (np.abs(xx - 200) < 160) & (np.abs(yy - 200) < 160)
+        TG[patch] = 2.0 ** -500 * (1.0 + cone(H, W, 200, 200, rng, 0.9)[patch])
+        TG[200, 200] = 0.0
+        TS = cone(H, W, 8, 12, rng, 0.3)
     elif case == "large":
         H, W = 2048, 1536
         TG, TS = cone(H, W, 1400, 1800, rng, 0.4, 1.3), cone(H, W, 100, 200, rng, 0.4)
@@ -116,7 +126,8 @@ def make(case, rng):
     return TG, TS
 
 
-CASES = ["smooth", "obstacles", "ties", "manhattan", "lopsided", "corridor", "same_source", "float_ties", "large"]
+CASES = ["smooth", "obstacles", "ties", "manhattan", "lopsided", "corridor", "same_source", "float_ties",
+         "zero_cost_patch", "large"]
 
 
 @pytest.mark.parametrize("case", CASES)
