@@ -67,6 +67,22 @@ __device__ __forceinline__ R stage_cost(R c) {
 #endif
 constexpr int kActStep = EIK_ACT_STEP;
 
+// EIK_EARLY_AND (persistent in-place passes): the consumption of the activations that reached the
+// busy tile (the state word's atomicAnd, a.sched bit 0) is issued by wave 0 at sweep step
+// EIK_AND_STEP instead of after the sweep, so its result is in when the sweep ends, and every wave
+// issues its halo reload right after the sweep's barrier -- the reload's round trip then overlaps
+// the write-back and its drain instead of following them.  (Still correct: the reload is issued
+// after the atomicAnd returned, so it sees every edge whose activation it consumed; an activation
+// arriving later stays pending for the next boundary.)
+#ifndef EIK_EARLY_AND
+#define EIK_EARLY_AND 0
+#endif
+#ifndef EIK_AND_STEP
+#define EIK_AND_STEP 96
+#endif
+constexpr bool kEarlyAnd = EIK_EARLY_AND;
+constexpr int kAndStep = EIK_AND_STEP;
+
 // (EIK_LAZY_CLAIM, round 4: a grabbed tile claimed -- PENDING -> BUSY -- at its first pass boundary
 // instead of before its staging, taking the grab's exchange round trip off the front's hop; the
 // first boundary then has to reload the halo to tell new activations from the served ones.
@@ -101,6 +117,23 @@ constexpr int kActStep = EIK_ACT_STEP;
 #endif
 template <typename R>
 constexpr bool kEcol = sizeof(R) == 8 ? EIK_ECOL_F64 : EIK_ECOL_F32;
+
+// EIK_WB_ONCE (persistent mode, full tiles, precisions with kEcol): a pass stores only what other
+// workgroups read while the tile is busy -- its first and last rows (the N / S neighbours' halos)
+// and the edge-column copies (the W / E halos, Fim2dArgs::ecol) -- and drains those before its
+// activations; the interior rows are stored once, when the visit ends, and drained before the
+// finish (the tile's next visit stages them).  "Changed in this pass" of an interior cell, which
+// no longer follows from the stored copy, comes from a 64-bit sum of the bit patterns of the
+// thread's 16 cells: T only decreases, so the sum changes exactly when a cell does (mod 2^64: a
+// decrease is below 2^64).  EIK_OPT_TOL > 0 then applies to the tracked cells only (an exact
+// test on the others: more passes at worst, the same fixed point).
+#ifndef EIK_WB_ONCE
+#define EIK_WB_ONCE 0
+#endif
+template <typename R>
+constexpr bool kWbOnce = EIK_WB_ONCE && kEcol<R>;
+__device__ __forceinline__ unsigned bits_of(float v) { return __float_as_uint(v); }
+__device__ __forceinline__ unsigned long long bits_of(double v) { return (unsigned long long)__double_as_longlong(v); }
 
 // EIK_FRESH_SKIP: a persistent visit of a tile no visit has written yet (its grab's exchange
 // returns the state without kVisited) stages only the cost: its T is the init kernel's +inf.
@@ -436,6 +469,15 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
         }
     }
     if (lane < 4) cell_c(Ts, (lane >> 1) * (kLds - 1) * kLds + (lane & 1) * (kLds - 1), (lane & 1) * (kLds - 1)) = INF;  // corners
+    // EIK_WB_ONCE: this visit stores interior rows at its end only (once), the row chunks still to
+    // store (dirty, bit k), and the bit-pattern sum of the thread's cells after the last pass
+    const bool once = COH && kWbOnce<R> && full;
+    unsigned dirty = 0u;
+    unsigned long long ssum = 0ull;
+    if (once) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) ssum += (unsigned long long)bits_of(told[i]);
+    }
     __syncthreads();
     EIK_PROBE(1);
 
@@ -454,10 +496,15 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
         if (act_tile >= 0) qpush_complete(a, act_tile, act_old);
         act_tile = -1;
     };
+    // EIK_EARLY_AND: this visit consumes activations inside the sweep (uniform)
+    const bool early = COH && kEarlyAnd && (a.sched & 1) && a.max_rounds == 1;
     for (int pass = 0;; ++pass) {
-        // in-sweep duties, by group step: wave 0's split activation (EIK_ACT_SPLIT)
+        unsigned pend_early = 0;
+        // in-sweep duties, by group step: wave 0's split activation (EIK_ACT_SPLIT) and, with
+        // EIK_EARLY_AND, its consumption of the activations that reached the tile
         auto hook = [&](int st) {
             if (EIK_ACT_SPLIT && wave == 0 && st == kActStep) act_complete();
+            if (early && tid == 0 && st == kAndStep) pend_early = atomicAnd(&a.qstate[tile], kBusy | kVisited);
         };
         // ---- sweep rounds (quadrant directions concurrently, one per wave; `dirs` selects them)
         const bool sweep = (dirs >> wave) & 1u;
@@ -471,6 +518,7 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
             } else {  // a wave without a sweep this pass still does its duties, in step order
                 for (int st = 0; st < 2 * kTile; st += kAhead) hook(st);
             }
+            if (early && tid == 0) L.pend = pend_early;  // (waits for the atomicAnd: issued 32 steps ago)
             __syncthreads();
         } else {
             for (int round = 0;; ++round) {
@@ -494,7 +542,11 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
         // before the halo reload) -- an in-place pass then serves them instead of a re-queued
         // visit.  Issued now, awaited with the write-back's drain.
         unsigned pend_old = 0;
-        if (COH && (a.sched & 1) && tid == 0) pend_old = atomicAnd(&a.qstate[tile], kBusy | kVisited);
+        if (COH && (a.sched & 1) && tid == 0 && !early) pend_old = atomicAnd(&a.qstate[tile], kBusy | kVisited);
+        // EIK_EARLY_AND: the consumption is done -- the next pass's halo now, beside the write-back
+        // (a visit that ends here discards it)
+        R hv_early = INF;
+        if (early) hv_early = load_halo();
         // ---- write back changed cells, collect side flags (and entering values, ordered mode).
         // EIK_EDGE_FIRST (persistent mode, full tiles): only the tile's edge cells -- the values a
         // neighbour's halo reads -- are stored and drained before the activations; the interior
@@ -505,18 +557,25 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
         unsigned fl = 0;
         unsigned defer_rows = 0;
         R kmin_self = INF, kmin[4] = {INF, INF, INF, INF};
+        unsigned long long nsum = 0ull;  // EIK_WB_ONCE: this pass's bit-pattern sum
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int ry = (tid >> 4) + 16 * k;
             const int64_t gy = y0 + ry;
+            // EIK_WB_ONCE: an interior row keeps its stored copy (told) at the visit's start,
+            // except for its edge-column cells, whose copies (ecol) are stored every pass
+            const bool once_row = once && ry != 0 && ry != kTile - 1;
             R nv[4];
             bool any = false;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 nv[e] = cell_t(Ts, (ry + 1) * kLds + cx + e + 1, cx + e + 1);
                 any |= nv[e] < told[4 * k + e];
+                if (once) nsum += (unsigned long long)bits_of(nv[e]);
+                // cells whose told follows every pass (all but a once-row's inner cells)
+                const bool trk = !once_row || (e == 0 && cx == 0) || (e == 3 && cx == kTile - 4);
                 // (a ghost cell inside a cut tile is lowered by the halo reload, never by a sweep)
-                if (nv[e] < told[4 * k + e] * keep && (full || (gy < a.H && x0 + cx + e < a.W))) {
+                if (trk && nv[e] < told[4 * k + e] * keep && (full || (gy < a.H && x0 + cx + e < a.W))) {
                     fl |= 128u;  // changed in this visit
                     kmin_self = umin(kmin_self, nv[e]);
                     // A neighbour can only improve if this edge value undercuts the neighbour's
@@ -534,7 +593,9 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
                 }
             }
             if (any) {
-                if (COH && EIK_EDGE_FIRST && full && ry != 0 && ry != kTile - 1) {
+                if (once_row) {
+                    defer_rows |= 1u << k;  // stored when the visit ends (dirty)
+                } else if (COH && EIK_EDGE_FIRST && full && ry != 0 && ry != kTile - 1) {
                     if (cx == 0 && nv[0] < told[4 * k]) T.st(gy * a.W + x0, nv[0]);
                     if (cx == kTile - 4 && nv[3] < told[4 * k + 3]) T.st(gy * a.W + x0 + kTile - 1, nv[3]);
                     defer_rows |= 1u << k;
@@ -554,8 +615,15 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
             }
             if (COH) {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) told[4 * k + e] = nv[e];  // what memory holds now
+                for (int e = 0; e < 4; ++e)  // what memory holds now (a once-row: its ecol cells)
+                    if (!once_row || (e == 0 && cx == 0) || (e == 3 && cx == kTile - 4)) told[4 * k + e] = nv[e];
             }
+        }
+        if (once) {
+            if (nsum != ssum) fl |= 128u;  // some cell of this thread decreased in this pass
+            ssum = nsum;
+            dirty |= defer_rows;
+            defer_rows = 0u;
         }
         if (fl) atomicOr(&L.flags, fl);
         if (a.delta < INF) {
@@ -565,7 +633,7 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
                 if (kmin[q] < INF) atomicMin(&L.key[q + 1], __float_as_uint((float)kmin[q]));
         }
         if (tid == 0) L.last = a.max_rounds == 1 ? -1 : (int)last_changed;  // -1: see flags bit 7
-        if (COH && (a.sched & 1) && tid == 0) L.pend = pend_old;
+        if (COH && (a.sched & 1) && tid == 0 && !early) L.pend = pend_old;
         if constexpr (COH) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
         __syncthreads();
         EIK_PROBE(7);
@@ -585,12 +653,33 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
             const unsigned pend = L.pend & (kPending | kFromN | kFromS | kFromW | kFromE);
             const bool self = (f & 128u) != 0u;
             if ((!self && !pend) || pass + 1 >= a.max_passes || a.max_rounds != 1) {
+                if (once) {
+                    // EIK_WB_ONCE: the last pass's edges have drained, so its neighbour activations
+                    // go now, ahead of the interior stores and their drain (activate_after then only
+                    // re-queues the tile itself: the bits cleared here are not read before it)
+                    activate_neighbours(a, tile, f | L.flags_acc, L.key, 0, 0u);  // lanes 0..4
+                    if (tid == 0) {
+                        L.flags = f & ~0x6fu;
+                        L.flags_acc = 0u;
+                    }
+                    asm volatile("" ::: "memory");
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        if (dirty & (1u << k)) {
+                            const int ry = (tid >> 4) + 16 * k;
+                            R v[4];
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) v[e] = cell_t(Ts, (ry + 1) * kLds + cx + e + 1, cx + e + 1);
+                            T.st4((y0 + ry) * a.W + x0 + cx, v);
+                        }
+                    }
+                }
                 store_deferred();  // drained by the persistent loop before the finish
                 break;
             }
             // the halo reload is issued first and the budget charge goes to wave 1, so wave 0's
             // activation atomics are the only round trips the next pass waits for
-            const R hv = load_halo();
+            const R hv = early ? hv_early : load_halo();
             if (tid == 64) charge_inplace_pass(a);  // in-place passes: stats and the visit budget
             // a.sched bit 1: after the first pass, neighbour activations wait for the visit's end
             // (one activation with the converged edges instead of one per pass)
@@ -792,7 +881,7 @@ __global__ __launch_bounds__(kThreads, WPS) void fim2d_persist_kernel(Fim2dArgs 
     int tile = -1;
     unsigned nvis = 0;  // wave 0 lane 0: visits not yet added to the global counter
     for (;;) {
-        if (EIK_EDGE_FIRST && tile >= 0) {  // uniform: every wave's deferred interior stores
+        if ((EIK_EDGE_FIRST || kWbOnce<R>) && tile >= 0) {  // uniform: every wave's deferred interior stores
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // complete before the finish
             __syncthreads();
         }

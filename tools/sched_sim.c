@@ -9,7 +9,8 @@
  * activation is the smallest improved edge value), 2 buckets of width delta (then FIFO), 3 the first
  * activation of a never-visited tile (the front) ahead of the FIFO, 4 as 2 but a queued tile keeps the
  * bucket of the activation that queued it (no re-push on a lower key; a released tile that still
- * changes is re-queued with the smallest value it changed to -- the GPU's bucket queue).
+ * changes is re-queued with the smallest value it changed to -- the GPU's bucket queue), 5 FIFO with
+ * displacement at push (DISP slots from the head; the displaced entry moves to the tail).
  *   gcc -O3 -march=native -o /tmp/sched_sim tools/sched_sim.c -lm
  *   /tmp/sched_sim cost.f32 N policy passes K
  */
@@ -26,6 +27,11 @@ static long seq = 0;
 static int oneside = 0;  /* 1: each quadrant sweep reads only its upstream neighbours */
 static int skipdir = 0;  /* 1: an in-place pass skips the one direction that alone changed the tile last pass */
 static int wrap = 0;     /* 1: the skewed sweep's idle tail steps run its rows again (lane l: rows 0..62-l) */
+static int earlyx = 0;   /* 1: a quadrant sweep runs by anti-diagonal steps and stops at the first step past the
+                          * last step of a dirty cell (changed in the tile's previous pass, or fed by a halo cell
+                          * that changed) at which no cell changed (EARLYX; counts steps per pass = max over dirs) */
+static long steps_run = 0, steps_full = 0;
+static int disp = 8;     /* policy 5: slots scanned from the head at a push (DISP) */
 static float *cost, *T, *key_of;
 static unsigned char *pend, *held;
 
@@ -65,12 +71,29 @@ static void activate(int t, float k) {
     if (policy == 1) hpush(key_of[t], t);
     else if (policy == 2 || policy == 4) hpush(floor(key_of[t] / delta) * 1e9 + (double)(seq++), t);  /* bucket, then FIFO */
     else if (policy == 3 && !visited[t]) ffifo[(fft++) % fcap] = t;
+    else if (policy == 6 && visited[t] && fh < ft) {
+        /* refinement first (the GPU's qslot_put_front with the test inverted): a visited tile's
+         * activation takes the next-to-be-taken slot when a backlog exists, its entry to the tail */
+        int u = fifo[fh % fcap]; fifo[fh % fcap] = t; fifo[(ft++) % fcap] = u;
+    }
+    else if (policy == 5) {
+        /* FIFO with displacement at push (the GPU's slot CAS): among the next DISP queued entries, the
+         * one with the largest key above k gives its slot to t and goes to the tail */
+        size_t best = (size_t)-1; float bk = k;
+        for (size_t i = fh; i < ft && i < fh + (size_t)disp; ++i) {
+            int u = fifo[i % fcap];
+            float ku = (pend[u] && !held[u]) ? key_of[u] : -1.f;  /* stale entries are not displaced */
+            if (ku > bk) { bk = ku; best = i; }
+        }
+        if (best != (size_t)-1) { int u = fifo[best % fcap]; fifo[best % fcap] = t; fifo[(ft++) % fcap] = u; }
+        else fifo[(ft++) % fcap] = t;
+    }
     else fifo[(ft++) % fcap] = t;
 }
 static int take(void) {
     if (policy == 3)
         while (ffh != fft) { int t = ffifo[(ffh++) % fcap]; if (pend[t] && !held[t]) return t; }
-    if (policy && policy != 3) {
+    if (policy && policy != 3 && policy != 5 && policy != 6) {
         while (hn) {
             HE e = hpop();
             if (pend[e.t] && !held[e.t] &&
@@ -82,7 +105,7 @@ static int take(void) {
     return -1;
 }
 
-typedef struct { int t, p, last; float kmin; float L[TS + 2][TS + 2], C[TS + 2][TS + 2]; } Work;
+typedef struct { int t, p, last; float kmin; float L[TS + 2][TS + 2], C[TS + 2][TS + 2]; unsigned char D[TS][TS]; } Work;
 
 int main(int argc, char** argv) {
     const char* cf = argv[1]; N = atoi(argv[2]); policy = atoi(argv[3]);
@@ -91,6 +114,8 @@ int main(int argc, char** argv) {
     if (getenv("ONESIDE")) oneside = 1;
     if (getenv("SKIPDIR")) skipdir = 1;
     if (getenv("WRAP")) wrap = 1;
+    if (getenv("EARLYX")) earlyx = 1;
+    if (getenv("DISP")) disp = atoi(getenv("DISP"));
     long dsweeps = 0;  /* quadrant sweeps run */
     NT = N / TS;
     const int nt = NT * NT;
@@ -117,6 +142,7 @@ int main(int argc, char** argv) {
                 if (t < 0) continue;
                 held[t] = 1; pend[t] = 0; key_of[t] = INFINITY; ++visits; visited[t] = 1;
                 W[k].t = t; W[k].p = 0; W[k].last = -1;
+                memset(W[k].D, 1, sizeof W[k].D);  /* a (re)staged tile: nothing known, every cell dirty */
                 int ty = t / NT, tx = t % NT, y0 = ty * TS, x0 = tx * TS;
                 for (int y = -1; y <= TS; ++y)
                     for (int x = -1; x <= TS; ++x) {
@@ -129,8 +155,18 @@ int main(int argc, char** argv) {
                 int t = W[k].t, y0 = (t / NT) * TS, x0 = (t % NT) * TS;
                 if (pend[t]) W[k].last = -1;  /* activated meanwhile: every direction */
                 pend[t] = 0; key_of[t] = INFINITY;
-                for (int x = -1; x <= TS; ++x) { W[k].L[0][x + 1] = at(y0 - 1, x0 + x); W[k].L[TS + 1][x + 1] = at(y0 + TS, x0 + x); }
-                for (int y = 0; y < TS; ++y) { W[k].L[y + 1][0] = at(y0 + y, x0 - 1); W[k].L[y + 1][TS + 1] = at(y0 + y, x0 + TS); }
+                for (int x = -1; x <= TS; ++x) {
+                    float n = at(y0 - 1, x0 + x), so = at(y0 + TS, x0 + x);
+                    if (x >= 0 && x < TS && n < W[k].L[0][x + 1]) W[k].D[0][x] = 1;  /* fed by a changed halo cell */
+                    if (x >= 0 && x < TS && so < W[k].L[TS + 1][x + 1]) W[k].D[TS - 1][x] = 1;
+                    W[k].L[0][x + 1] = n; W[k].L[TS + 1][x + 1] = so;
+                }
+                for (int y = 0; y < TS; ++y) {
+                    float w = at(y0 + y, x0 - 1), e = at(y0 + y, x0 + TS);
+                    if (w < W[k].L[y + 1][0]) W[k].D[y][0] = 1;
+                    if (e < W[k].L[y + 1][TS + 1]) W[k].D[y][TS - 1] = 1;
+                    W[k].L[y + 1][0] = w; W[k].L[y + 1][TS + 1] = e;
+                }
             }
             ++busy;
         }
@@ -143,6 +179,37 @@ int main(int argc, char** argv) {
             ++npass; ++W[k].p;
             float (*L)[TS + 2] = W[k].L, (*C)[TS + 2] = W[k].C;
             int ch = 0, chd[4] = {0, 0, 0, 0};
+            if (earlyx) {
+                static unsigned char nd[TS][TS];
+                memset(nd, 0, sizeof nd);
+                int pass_steps = 0;
+                for (int d = 0; d < 4; ++d) {
+                    int sx = (d & 1) ? -1 : 1, sy = (d & 2) ? -1 : 1, smax = -1;
+                    for (int yy = 0; yy < TS; ++yy) for (int xx = 0; xx < TS; ++xx) {
+                        int y = sy > 0 ? yy : TS - 1 - yy, x = sx > 0 ? xx : TS - 1 - xx;
+                        if (W[k].D[y][x] && xx + yy > smax) smax = xx + yy;
+                    }
+                    int s = 0;
+                    for (; s < 2 * TS - 1; ++s) {
+                        int any = 0;
+                        for (int xx = 0; xx < TS; ++xx) {
+                            int yy = s - xx;
+                            if (yy < 0 || yy >= TS) continue;
+                            int y = (sy > 0 ? yy : TS - 1 - yy) + 1, x = (sx > 0 ? xx : TS - 1 - xx) + 1;
+                            float w = god(L[y][x - sx], L[y - sy][x], C[y][x]);
+                            if (w < L[y][x]) { L[y][x] = w; ch = 1; chd[d] = 1; any = 1; nd[y - 1][x - 1] = 1; }
+                        }
+                        if (s > smax && !any) { ++s; break; }
+                    }
+                    if (s > pass_steps) pass_steps = s;
+                    ++dsweeps;
+                }
+                steps_run += pass_steps; steps_full += 2 * TS - 1;
+                memcpy(W[k].D, nd, sizeof nd);
+                changed[k] = ch;
+                W[k].last = -1;
+                continue;
+            }
             for (int d = 0; d < 4; ++d) {
                 if (skipdir && W[k].last == d) continue;
                 ++dsweeps;
@@ -211,5 +278,6 @@ int main(int argc, char** argv) {
     for (size_t i = 0; i < (size_t)N * N; ++i) if (isfinite(T[i])) { s += T[i]; ++fin; }
     printf("policy %d passes %d K %d: rounds %ld visits %ld passes %ld (%.2f/tile) sweeps %ld avg busy %.0f checksum %.6e finite %ld\n", policy,
            maxp, K, rounds, visits, npass, (double)npass / nt, dsweeps, (double)busy_sum / rounds, s, fin);
+    if (earlyx) printf("EARLYX: pass steps run %ld of %ld (%.3f)\n", steps_run, steps_full, (double)steps_run / steps_full);
     return 0;
 }
