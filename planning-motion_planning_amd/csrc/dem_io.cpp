@@ -6,6 +6,7 @@
 // bit-identical).  Host code: no GPU, no context.
 #include <charconv>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -42,7 +43,16 @@ int parse_line(const char* b, const char* e, double* out, int64_t want, int64_t*
         if (s < t && *s == '+') ++s;  // from_chars does not take a leading '+'
         double v = 0;
         const auto r = std::from_chars(s, t, v);
-        if (r.ec != std::errc() || r.ptr != t) return EIK_ERR_ARG;
+        if (r.ec == std::errc::result_out_of_range && r.ptr == t) {
+            // Python's float() gives +-inf on overflow and 0 / a subnormal on underflow, where
+            // from_chars reports the range error: glibc's strtod (correctly rounded too) does that
+            const std::string tok(s, t);
+            char* end = nullptr;
+            v = strtod(tok.c_str(), &end);
+            if (end != tok.c_str() + tok.size()) return EIK_ERR_ARG;
+        } else if (r.ec != std::errc() || r.ptr != t) {
+            return EIK_ERR_ARG;
+        }
         if (out && n < want) out[n] = v;
         ++n;
         if (q == e) break;
