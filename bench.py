@@ -277,6 +277,24 @@ def main():
                                            else "RCCL batch_isend_irecv + all_reduce")
         out["config"]["dd_halo_consistent"] = dd_ok
         out["config"].update(dd_check)
+        # every rank's work per solve (the decomposition's total against the single-domain solve's)
+        if not args.no_timing:
+            mine = torch.tensor([visits, passes, fresh, blk.h * blk.w], dtype=torch.float64) / \
+                torch.tensor([args.steps, args.steps, args.steps, 1], dtype=torch.float64)
+            allr = [torch.zeros_like(mine) for _ in range(world)]
+            dist.all_gather(allr, mine, group=ctrl)
+            pr = torch.stack(allr)
+            sd_v = dd_check.get("single_domain_tile_visits")
+            sd_p = dd_check.get("single_domain_inplace_passes")
+            out["config"]["dd_per_rank"] = {
+                "tile_visits": [round(v, 1) for v in pr[:, 0].tolist()],
+                "inplace_passes": [round(v, 1) for v in pr[:, 1].tolist()],
+                "fresh_visits": [round(v, 1) for v in pr[:, 2].tolist()],
+                "total_tile_visits": round(float(pr[:, 0].sum()), 1),
+                "total_inplace_passes": round(float(pr[:, 1].sum()), 1),
+                "visits_vs_single_domain": round(float(pr[:, 0].sum()) / sd_v, 3) if sd_v else None,
+                "passes_vs_single_domain": (round(float(pr[:, 0].sum() + pr[:, 1].sum()) / (sd_v + sd_p), 3)
+                                            if sd_v else None)}
         rr = dd_rounds[-args.steps:]
         out["config"]["dd_rounds_per_solve"] = round(sum(rr) / max(len(rr), 1), 1)
         out["config"]["dd_us_per_round"] = round(ms_per_step * 1e3 / max(sum(rr) / max(len(rr), 1), 1), 1)
@@ -407,6 +425,7 @@ def dd_field_check(args, ctx, dev, stream, blk, cost, T, H, W, seed, goal_g, tdt
     f1 = eikonal.Fim2d(ctx, 1, H, W, edt)
     f1.solve(full_c.data_ptr(), full_T.data_ptr(), [goal_g], stream.cuda_stream)
     torch.cuda.synchronize()
+    s1 = f1.stats()  # the single-domain solve's work: the reference for the decomposition's total
     f1.close()
     ref = full_T[blk.y0:blk.y1, blk.x0:blk.x1].contiguous()
     del full_c, full_T
@@ -425,7 +444,7 @@ def dd_field_check(args, ctx, dev, stream, blk, cost, T, H, W, seed, goal_g, tdt
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
         return t.item()
 
-    out = {}
+    out = {"single_domain_tile_visits": int(s1["tile_visits"]), "single_domain_inplace_passes": int(s1["inplace_passes"])}
     e = worst(err_of(T))
     out["dd_field_ok"] = bool(e <= tol)
     out["dd_field_max_rel"] = e
@@ -467,6 +486,48 @@ def c3_goal(cost_b, b, N):
             return gx, gy
 
 
+def solver_roofline(ctx, fim, solve, edt, kname, pmc_name, reps=3):
+    """Roofline of one persistent solver launch (one launch per solve) on the throughput-bound
+    configs: the launch's hipEvent time on the solver's stream (EIK_OPT_TIMING) and eik_stats'
+    visits / first visits / in-place passes over `reps` solves, on the byte model of the C2 line
+    (cost + T read + T write + halo per visit, no T read on a first visit, T write +
+    halo per in-place pass).  traffic: the committed PMC pair of this config (profiles/pmc_name,
+    tools/one_config.py under rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, tools/pmc_traffic.py)."""
+    esz = 8 if edt == L.EIK_F64 else 4
+    ctx.set_option(L.OPT_TIMING, 1)
+    ms, alg, vis, pas, fr = [], [], [], [], []
+    try:
+        for _ in range(reps):
+            solve()
+            st = fim.stats()
+            ms.append(st["sweep_ms"])
+            vis.append(st["tile_visits"])
+            pas.append(st["inplace_passes"])
+            fr.append(st["fresh_visits"])
+            alg.append(esz * (st["tile_visits"] * CELLS_PER_VISIT - st["fresh_visits"] * CELLS_T_READ
+                              + st["inplace_passes"] * CELLS_PER_PASS))
+    finally:
+        ctx.set_option(L.OPT_TIMING, 0)
+    ms_k, alg_k = float(np.mean(ms)), float(np.mean(alg))
+    ach = alg_k / (ms_k * 1e-3) / 1e9 if ms_k > 0 else None
+    traffic = None
+    pf = os.path.join(ROOT, "profiles", pmc_name)
+    if os.path.exists(pf):
+        try:
+            pm = json.load(open(pf))
+            if kname.split("<")[0] in pm.get("kernel", "") and pm.get("dtype") == ("f64" if esz == 8 else "f32"):
+                traffic = pm.get("bytes_per_launch")
+        except Exception:
+            traffic = None
+    return {"bound": "hbm", "kernel": kname, "achieved": round(ach, 2) if ach else None, "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None, "traffic": traffic,
+            "traffic_source": f"profiles/{pmc_name}" if traffic else None,
+            "alg_bytes_per_launch": round(alg_k), "avg_launch_us": round(ms_k * 1e3, 2),
+            "tile_visits_per_solve": round(float(np.mean(vis)), 1),
+            "inplace_passes_per_solve": round(float(np.mean(pas)), 1),
+            "fresh_visits_per_solve": round(float(np.mean(fr)), 1)}
+
+
 def bench_batch(ctx, dev, stream, steps, tdt, edt, B=128, N=1024, rank=0, world=1, group=None):
     """configs[2]: 128 maps of 1024^2 (terrain seeds 1000..1127, one goal per map), ONE batched
     persistent solve (tiles of all maps share the device FIFO).  A step = the whole batch.  With
@@ -483,12 +544,17 @@ def bench_batch(ctx, dev, stream, steps, tdt, edt, B=128, N=1024, rank=0, world=
     fim = eikonal.Fim2d(ctx, nb, N, N, edt)
     if world > 1:
         dist.barrier()
-    sec = timed_loop(lambda: fim.solve(cost.data_ptr(), T.data_ptr(), goals, stream.cuda_stream), steps)
+    solve = lambda: fim.solve(cost.data_ptr(), T.data_ptr(), goals, stream.cuda_stream)  # noqa: E731
+    sec = timed_loop(solve, steps)
     if world > 1:
         tt = torch.tensor([sec], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=group)
         sec = tt.item()
     st = fim.stats()
+    f64 = edt == L.EIK_F64
+    roof = None if world > 1 else solver_roofline(
+        ctx, fim, solve, edt, f"fim2d_persist_kernel<{'double' if f64 else 'float'}, 1>",
+        f"pmc_traffic_c3{'' if f64 else '_f32'}.json")
     reach = float(torch.isfinite(T).float().mean())
     fim.close()
     del cost, T
@@ -498,7 +564,7 @@ def bench_batch(ctx, dev, stream, steps, tdt, edt, B=128, N=1024, rank=0, world=
             "dtype": "f64" if edt == L.EIK_F64 else "f32",
             "value": round(B * N * N / sec / 1e9, 4), "unit": "Gcells/s", "ms_per_step": round(sec * 1e3, 4),
             "steps": steps, "tile_visits_per_solve": st["tile_visits"], "inplace_passes_per_solve": st["inplace_passes"],
-            "reached_fraction": round(reach, 4)}
+            "reached_fraction": round(reach, 4), **({"roofline": roof} if roof else {})}
 
 
 def bench_c2(ctx, dev, stream, cost, goal, steps, dtype):
@@ -534,8 +600,14 @@ def bench_c4(ctx, dev, stream, steps, tdt, edt, N=16384):
     T = torch.empty_like(cost)
     fim = eikonal.Fim2d(ctx, 1, N, N, edt)
     goal = (N // 2, N // 2)
-    sec = timed_loop(lambda: fim.solve(cost.data_ptr(), T.data_ptr(), [goal], stream.cuda_stream), steps)
+    solve = lambda: fim.solve(cost.data_ptr(), T.data_ptr(), [goal], stream.cuda_stream)  # noqa: E731
+    sec = timed_loop(solve, steps)
     st = fim.stats()
+    f64 = edt == L.EIK_F64
+    wide = not f64 and (N // 64) * (N // 64) >= WIDE_TILES
+    roof = solver_roofline(ctx, fim, solve, edt,
+                           f"fim2d_persist_kernel<{'double' if f64 else 'float'}, {4 if wide else 1}>",
+                           f"pmc_traffic_c4{'' if f64 else '_f32'}.json", reps=2)
     reach = float(torch.isfinite(T).float().mean())
     fim.close()
     del cost, T
@@ -543,7 +615,7 @@ def bench_c4(ctx, dev, stream, steps, tdt, edt, N=16384):
     return {"workload": f"configs[3] at 1 GPU: {N}x{N} DEM-derived raster (seed 7), single goal at the centre, 1x1",
             "dtype": "f64" if edt == L.EIK_F64 else "f32", "value": round(N * N / sec / 1e9, 4), "unit": "Gcells/s", "ms_per_step": round(sec * 1e3, 4),
             "steps": steps, "tile_visits_per_solve": st["tile_visits"], "inplace_passes_per_solve": st["inplace_passes"],
-            "reached_fraction": round(reach, 4)}
+            "reached_fraction": round(reach, 4), "roofline": roof}
 
 
 def bench_arm(ctx, steps, half=30, m=40, K=16, res=0.05):

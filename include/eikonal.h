@@ -97,11 +97,20 @@ typedef enum {
                                 division free of range handling inside their safe domain; 1 = the
                                 same loop with the compiler's sqrt / division; 0 = the loop in
                                 the reference's statement order.  Same path bits in all three.  */
-    EIK_OPT_FRONTS_CAP = 13  /* biComputeTmap / rover path, rasters >= 2^20 cells: 1 (default) solves
+    EIK_OPT_FRONTS_CAP = 13, /* biComputeTmap / rover path, rasters >= 2^20 cells: 1 (default) solves
                                 each front only up to a cap on T estimated from a coarse copy of
                                 the raster (x 1.25) and falls back to the full solve when the
                                 capped fields cannot be shown to give the full fields' join; a
                                 value v > 1: the same with margin v; 0 = full fronts            */
+    EIK_OPT_LIVE_PACK = 14,  /* live domain decomposition (eik_fim2d_live_pack): 0 (default) = the
+                                halo agent stores every edge cell each round; 1 = only the cells
+                                of tiles that are neither pending nor busy (converged edges), so a
+                                neighbour is not re-activated by every intermediate refinement
+                                (a round whose snapshot had no tile pending or busy packs all)   */
+    EIK_OPT_PRIO = 15        /* 2D persistent solves of one or two maps: v > 0 serves waiting tiles
+                                lowest entering T first, in 64 bands of width v x 64 x the geometric
+                                mean of the finite costs (fim_engine.hpp "priority bands");
+                                0 = the FIFO                                                      */
 } eik_option;
 
 typedef enum { EIK_MODE_LIST = 0, EIK_MODE_PERSISTENT = 1 } eik_mode;

@@ -53,6 +53,13 @@ struct Fim2dArgs {
     // *qhold != 0
     unsigned* qhold;       // nullptr: end when no tile is pending or busy
     struct LiveBox* live;  // pinned host mailbox of the halo agent (live launches only)
+    int live_pack;         // EIK_OPT_LIVE_PACK: 1 = the agent packs only cells of idle tiles
+    // priority bands (EIK_OPT_PRIO, fim_engine.hpp): pending tiles wait in kBands FIFOs by entering T
+    // (band = T / pdelta, the last band open-ended) and are taken lowest band first; nullptr bctl: off
+    unsigned* bslot;            // [kBands][bmask + 1]: tile + 1, 0 = empty
+    unsigned bmask;
+    unsigned long long* bctl;   // band b: head at bctl[16 b], tail at bctl[16 b + 8] (own 64-B lines)
+    const float* pdelta;        // band width in units of T (device word: prio_delta_kernel sets it per solve)
 };
 
 // Host <-> halo-agent mailbox (pinned, coherent host memory).  The host writes cmd, then seq
@@ -74,6 +81,7 @@ constexpr int kModeList = 0, kModePersistent = 1;
 // @kVisitsOff, on a 128-B line of their own (sharing the error word's line -- polled by every
 // grab -- with the in-place passes' atomics cost C2 ~20 %)
 constexpr size_t kQueueCtlBytes = 384;
+constexpr int kBands = 64;  // priority bands (EIK_OPT_PRIO): one band per lane of the grabbing wave
 constexpr size_t kVisitsOff = 256;
 
 // T = inf, queue / list / visit / edge words cleared, goals seeded
@@ -83,6 +91,7 @@ hipError_t fim2d_sweep(const Fim2dArgs& a, bool f64, int grid, hipStream_t st);
 constexpr int64_t kWideTiles = 16384;
 hipError_t fim2d_persist(const Fim2dArgs& a, bool f64, int grid, hipStream_t st, bool wide = false, bool rewind = true);
 hipError_t fim2d_qrewind(const Fim2dArgs& a, hipStream_t st);
+hipError_t fim2d_prio_delta(const void* cost, bool f64, int64_t n, float mult, float* out, hipStream_t st);
 int fim2d_persist_resident(bool f64, int cus, bool wide = false);
 hipError_t fim2d_merge_ghost(const Fim2dArgs& a, bool f64, int side, const void* recv, int64_t len, hipStream_t st);
 hipError_t fim2d_pack_edges(const Fim2dArgs& a, bool f64, void* n, void* s, void* w, void* e, hipStream_t st);

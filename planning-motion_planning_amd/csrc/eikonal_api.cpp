@@ -140,6 +140,8 @@ struct eik_ctx {
     int passes = 0;              // EIK_OPT_PASSES: in-place passes per persistent visit (0: adaptive)
     bool fresh_first = false;    // EIK_OPT_FRESH_FIRST: fresh tiles jump a backlogged FIFO
     int sched = 1;               // EIK_OPT_SCHED: in-place scheduling of persistent visits
+    int live_pack = 0;           // EIK_OPT_LIVE_PACK: the halo agent packs only idle tiles' edges
+    double prio = 0.0;           // EIK_OPT_PRIO: band width of the priority bands in T (0: plain FIFO)
     int path_loop = 2;           // EIK_OPT_PATH_LOOP: 2D walker loop form (profiles/r02i_path_walker.log)
     int timing = 0;
     int grid = 0;
@@ -181,6 +183,7 @@ struct eik_fim2d {
     DevBuf lists, counts, mark, edge, goals, key;
     DevBuf ecol;                         // every tile's two edge columns (Fim2dArgs::ecol)
     DevBuf qctl, qslot, qstate;          // persistent-mode FIFO
+    DevBuf bslot, bctl;                  // priority bands (EIK_OPT_PRIO)
     int* h_counts = nullptr;             // pinned
     unsigned* h_q = nullptr;             // pinned copy of qctl
     unsigned long long* h_visits = nullptr;
@@ -372,6 +375,8 @@ int eik_set_option(eik_ctx* c, int opt, double v) {
         case EIK_OPT_PASSES: c->passes = std::max(0, std::min(64, (int)v)); break;
         case EIK_OPT_FRESH_FIRST: c->fresh_first = v != 0; break;
         case EIK_OPT_SCHED: c->sched = std::max(0, std::min(3, (int)v)); break;
+        case EIK_OPT_LIVE_PACK: c->live_pack = v != 0; break;
+        case EIK_OPT_PRIO: c->prio = v > 0 ? v : 0.0; break;
         case EIK_OPT_PATH_LOOP: c->path_loop = std::max(0, std::min(2, (int)v)); break;
         case EIK_OPT_FRONTS_CAP: c->fronts_cap = v <= 0 ? 0.0 : v == 1 ? kFrontsMargin : std::max(1.0, v); break;
         default: return set_err(c, EIK_ERR_ARG, "unknown option %d", opt);
@@ -474,6 +479,13 @@ void eik_fim2d_destroy(eik_fim2d* f) {
     delete f;
 }
 
+// the queue counters of the last persistent launch (EIK_QDEBUG builds; zeros otherwise)
+extern "C" int eik_fim2d_qcount(const eik_fim2d* f, uint64_t out[8]) {
+    if (!f || !out) return EIK_ERR_ARG;
+    memcpy(out, (const char*)f->h_q + kVisitsOff + 24, 8 * sizeof(uint64_t));
+    return EIK_OK;
+}
+
 int eik_fim2d_set_ghosts(eik_fim2d* f, void* n, void* s, void* w, void* e) {
     if (!f) return EIK_ERR_ARG;
     if (f->B != 1) return set_err(f->ctx, EIK_ERR_ARG, "ghost strips need B == 1");
@@ -525,6 +537,25 @@ int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
     // (the previous solve on this solver synchronised before returning: h_goals is free)
     memcpy(f->h_goals, goals, sizeof(int64_t) * 2 * f->B);
     HIPCHK(c, hipMemcpyAsync(f->goals.p, f->h_goals, sizeof(int64_t) * 2 * f->B, hipMemcpyHostToDevice, f->stream));
+    // priority bands (persistent mode): kBands rings of twice the tiles each (a pending tile has at
+    // most one live entry per band it was pushed to plus stale ones, dropped when taken), cleared
+    // with the queue before the seed kernel pushes the goal's tile
+    f->a.bctl = nullptr;
+    // (one map or a few: a batch of independent maps keeps the FIFO -- their keys do not compare)
+    if (c->prio > 0 && f->a.mode == kModePersistent && f->B <= 2) {
+        uint64_t bc = 1024;
+        while (bc < 2 * (uint64_t)f->a.capacity) bc <<= 1;
+        HIPCHK(c, f->bslot.ensure(sizeof(unsigned) * kBands * bc));
+        HIPCHK(c, f->bctl.ensure(128 * kBands + 128));  // + the band width's word
+        HIPCHK(c, hipMemsetAsync(f->bslot.p, 0, sizeof(unsigned) * kBands * bc, f->stream));
+        HIPCHK(c, hipMemsetAsync(f->bctl.p, 0, 128 * kBands, f->stream));
+        f->a.bslot = (unsigned*)f->bslot.p;
+        f->a.bmask = (unsigned)(bc - 1);
+        f->a.bctl = (unsigned long long*)f->bctl.p;
+        float* pd = (float*)((char*)f->bctl.p + 128 * kBands);
+        HIPCHK(c, fim2d_prio_delta(d_cost, f->f64, f->H * f->W, (float)c->prio, pd, f->stream));
+        f->a.pdelta = pd;
+    }
     HIPCHK(c, fim2d_init(f->a, f->f64, (int)f->B, (const int64_t*)f->goals.p, (unsigned*)f->edge.p, f->stream));
     f->started = true;
     f->need_rewind = false;  // the init cleared the queue words
@@ -589,6 +620,7 @@ int eik_fim2d_iterate(eik_fim2d* f, int64_t max_iters, int64_t* active) {
         const int g = std::min(grid, f->persist_grid);
         f->a.fresh_first = c->fresh_first;
         f->a.sched = c->sched;
+        f->a.live_pack = c->live_pack;
         // eik_fim2d_solve launches without the queue rewind (the next solve's init clears the
         // queue); a later merge_ghost / iterate on the same solve issues it first (need_rewind)
         HIPCHK(c, rewind_if_needed(f));

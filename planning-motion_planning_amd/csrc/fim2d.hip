@@ -67,22 +67,6 @@ __device__ __forceinline__ R stage_cost(R c) {
 #endif
 constexpr int kActStep = EIK_ACT_STEP;
 
-// EIK_EARLY_AND (persistent in-place passes): the consumption of the activations that reached the
-// busy tile (the state word's atomicAnd, a.sched bit 0) is issued by wave 0 at sweep step
-// EIK_AND_STEP instead of after the sweep, so its result is in when the sweep ends, and every wave
-// issues its halo reload right after the sweep's barrier -- the reload's round trip then overlaps
-// the write-back and its drain instead of following them.  (Still correct: the reload is issued
-// after the atomicAnd returned, so it sees every edge whose activation it consumed; an activation
-// arriving later stays pending for the next boundary.)
-#ifndef EIK_EARLY_AND
-#define EIK_EARLY_AND 0
-#endif
-#ifndef EIK_AND_STEP
-#define EIK_AND_STEP 96
-#endif
-constexpr bool kEarlyAnd = EIK_EARLY_AND;
-constexpr int kAndStep = EIK_AND_STEP;
-
 // (EIK_LAZY_CLAIM, round 4: a grabbed tile claimed -- PENDING -> BUSY -- at its first pass boundary
 // instead of before its staging, taking the grab's exchange round trip off the front's hop; the
 // first boundary then has to reload the halo to tell new activations from the served ones.
@@ -102,6 +86,17 @@ constexpr int kAndStep = EIK_AND_STEP;
 // (profiles/r04c_async_wb_ab.log).  The drain is the front's hop either way -- a neighbour may be
 // activated only once the edge it reads has landed.)
 
+// (Round 5, measured on one box against this schedule and removed -- code in commit f3e04a5:
+//  * EIK_WB_ONCE: a pass stored only the first / last rows and the edge-column copies, the interior
+//    rows once when the visit ended (a 64-bit sum of the cells' bit patterns told a pass that changed
+//    them).  PMC writes would fall ~8x, but C2 fp64 2.39-2.41 -> 2.52-2.58 ms, C3 -6 %, C4 -8 %
+//    (profiles/r05a_wb_once_ab.log): the per-pass drain is latency, not bytes, and the interior's
+//    drain moved onto the visit's finish.
+//  * EIK_EARLY_AND: the activation consumption issued by wave 0 at sweep step 96 (or 64) so that the
+//    halo reload could overlap the write-back's drain.  C2 fp64 2.38-2.41 -> 2.85-2.91 ms, visits
+//    +20 %, in-place passes +19 % (profiles/r05b_early_and_ab.log): activations arriving in the
+//    sweep's last steps were no longer served in place and came back as full visits.)
+
 // EIK_ECOL_F64 / _F32 (kEcol): the W / E halo columns of a visit come from Fim2dArgs::ecol, a copy of every tile's two
 // edge columns stored beside T by the write-back (and the init / seed kernels), instead of from T:
 // a column of T spans 64 rows, i.e. 64 lines of 64-128 B for 256-512 B of data (the fp64 solve's
@@ -117,23 +112,6 @@ constexpr int kAndStep = EIK_AND_STEP;
 #endif
 template <typename R>
 constexpr bool kEcol = sizeof(R) == 8 ? EIK_ECOL_F64 : EIK_ECOL_F32;
-
-// EIK_WB_ONCE (persistent mode, full tiles, precisions with kEcol): a pass stores only what other
-// workgroups read while the tile is busy -- its first and last rows (the N / S neighbours' halos)
-// and the edge-column copies (the W / E halos, Fim2dArgs::ecol) -- and drains those before its
-// activations; the interior rows are stored once, when the visit ends, and drained before the
-// finish (the tile's next visit stages them).  "Changed in this pass" of an interior cell, which
-// no longer follows from the stored copy, comes from a 64-bit sum of the bit patterns of the
-// thread's 16 cells: T only decreases, so the sum changes exactly when a cell does (mod 2^64: a
-// decrease is below 2^64).  EIK_OPT_TOL > 0 then applies to the tracked cells only (an exact
-// test on the others: more passes at worst, the same fixed point).
-#ifndef EIK_WB_ONCE
-#define EIK_WB_ONCE 0
-#endif
-template <typename R>
-constexpr bool kWbOnce = EIK_WB_ONCE && kEcol<R>;
-__device__ __forceinline__ unsigned bits_of(float v) { return __float_as_uint(v); }
-__device__ __forceinline__ unsigned long long bits_of(double v) { return (unsigned long long)__double_as_longlong(v); }
 
 // EIK_FRESH_SKIP: a persistent visit of a tile no visit has written yet (its grab's exchange
 // returns the state without kVisited) stages only the cost: its T is the init kernel's +inf.
@@ -469,15 +447,6 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
         }
     }
     if (lane < 4) cell_c(Ts, (lane >> 1) * (kLds - 1) * kLds + (lane & 1) * (kLds - 1), (lane & 1) * (kLds - 1)) = INF;  // corners
-    // EIK_WB_ONCE: this visit stores interior rows at its end only (once), the row chunks still to
-    // store (dirty, bit k), and the bit-pattern sum of the thread's cells after the last pass
-    const bool once = COH && kWbOnce<R> && full;
-    unsigned dirty = 0u;
-    unsigned long long ssum = 0ull;
-    if (once) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) ssum += (unsigned long long)bits_of(told[i]);
-    }
     __syncthreads();
     EIK_PROBE(1);
 
@@ -491,20 +460,16 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
     unsigned dirs = L.dirs;
     // EIK_ACT_SPLIT: this lane's activation issued at the last pass boundary (-1: none)
     int act_tile = -1;
-    unsigned act_old = 0u;
+    unsigned act_old = 0u, act_kold = 0x7f800000u;
+    float act_k = 0.f;  // priority mode: the activation's key and the neighbour's key before it
     auto act_complete = [&]() {
-        if (act_tile >= 0) qpush_complete(a, act_tile, act_old);
+        if (act_tile >= 0) qpush_complete(a, act_tile, act_old, act_k, act_kold);
         act_tile = -1;
     };
-    // EIK_EARLY_AND: this visit consumes activations inside the sweep (uniform)
-    const bool early = COH && kEarlyAnd && (a.sched & 1) && a.max_rounds == 1;
     for (int pass = 0;; ++pass) {
-        unsigned pend_early = 0;
-        // in-sweep duties, by group step: wave 0's split activation (EIK_ACT_SPLIT) and, with
-        // EIK_EARLY_AND, its consumption of the activations that reached the tile
+        // in-sweep duties, by group step: wave 0's split activation (EIK_ACT_SPLIT)
         auto hook = [&](int st) {
             if (EIK_ACT_SPLIT && wave == 0 && st == kActStep) act_complete();
-            if (early && tid == 0 && st == kAndStep) pend_early = atomicAnd(&a.qstate[tile], kBusy | kVisited);
         };
         // ---- sweep rounds (quadrant directions concurrently, one per wave; `dirs` selects them)
         const bool sweep = (dirs >> wave) & 1u;
@@ -518,7 +483,6 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
             } else {  // a wave without a sweep this pass still does its duties, in step order
                 for (int st = 0; st < 2 * kTile; st += kAhead) hook(st);
             }
-            if (early && tid == 0) L.pend = pend_early;  // (waits for the atomicAnd: issued 32 steps ago)
             __syncthreads();
         } else {
             for (int round = 0;; ++round) {
@@ -542,11 +506,7 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
         // before the halo reload) -- an in-place pass then serves them instead of a re-queued
         // visit.  Issued now, awaited with the write-back's drain.
         unsigned pend_old = 0;
-        if (COH && (a.sched & 1) && tid == 0 && !early) pend_old = atomicAnd(&a.qstate[tile], kBusy | kVisited);
-        // EIK_EARLY_AND: the consumption is done -- the next pass's halo now, beside the write-back
-        // (a visit that ends here discards it)
-        R hv_early = INF;
-        if (early) hv_early = load_halo();
+        if (COH && (a.sched & 1) && tid == 0) pend_old = atomicAnd(&a.qstate[tile], kBusy | kVisited);
         // ---- write back changed cells, collect side flags (and entering values, ordered mode).
         // EIK_EDGE_FIRST (persistent mode, full tiles): only the tile's edge cells -- the values a
         // neighbour's halo reads -- are stored and drained before the activations; the interior
@@ -557,25 +517,18 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
         unsigned fl = 0;
         unsigned defer_rows = 0;
         R kmin_self = INF, kmin[4] = {INF, INF, INF, INF};
-        unsigned long long nsum = 0ull;  // EIK_WB_ONCE: this pass's bit-pattern sum
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int ry = (tid >> 4) + 16 * k;
             const int64_t gy = y0 + ry;
-            // EIK_WB_ONCE: an interior row keeps its stored copy (told) at the visit's start,
-            // except for its edge-column cells, whose copies (ecol) are stored every pass
-            const bool once_row = once && ry != 0 && ry != kTile - 1;
             R nv[4];
             bool any = false;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 nv[e] = cell_t(Ts, (ry + 1) * kLds + cx + e + 1, cx + e + 1);
                 any |= nv[e] < told[4 * k + e];
-                if (once) nsum += (unsigned long long)bits_of(nv[e]);
-                // cells whose told follows every pass (all but a once-row's inner cells)
-                const bool trk = !once_row || (e == 0 && cx == 0) || (e == 3 && cx == kTile - 4);
                 // (a ghost cell inside a cut tile is lowered by the halo reload, never by a sweep)
-                if (trk && nv[e] < told[4 * k + e] * keep && (full || (gy < a.H && x0 + cx + e < a.W))) {
+                if (nv[e] < told[4 * k + e] * keep && (full || (gy < a.H && x0 + cx + e < a.W))) {
                     fl |= 128u;  // changed in this visit
                     kmin_self = umin(kmin_self, nv[e]);
                     // A neighbour can only improve if this edge value undercuts the neighbour's
@@ -593,9 +546,7 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
                 }
             }
             if (any) {
-                if (once_row) {
-                    defer_rows |= 1u << k;  // stored when the visit ends (dirty)
-                } else if (COH && EIK_EDGE_FIRST && full && ry != 0 && ry != kTile - 1) {
+                if (COH && EIK_EDGE_FIRST && full && ry != 0 && ry != kTile - 1) {
                     if (cx == 0 && nv[0] < told[4 * k]) T.st(gy * a.W + x0, nv[0]);
                     if (cx == kTile - 4 && nv[3] < told[4 * k + 3]) T.st(gy * a.W + x0 + kTile - 1, nv[3]);
                     defer_rows |= 1u << k;
@@ -615,25 +566,18 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
             }
             if (COH) {
 #pragma unroll
-                for (int e = 0; e < 4; ++e)  // what memory holds now (a once-row: its ecol cells)
-                    if (!once_row || (e == 0 && cx == 0) || (e == 3 && cx == kTile - 4)) told[4 * k + e] = nv[e];
+                for (int e = 0; e < 4; ++e) told[4 * k + e] = nv[e];  // what memory holds now
             }
         }
-        if (once) {
-            if (nsum != ssum) fl |= 128u;  // some cell of this thread decreased in this pass
-            ssum = nsum;
-            dirty |= defer_rows;
-            defer_rows = 0u;
-        }
         if (fl) atomicOr(&L.flags, fl);
-        if (a.delta < INF) {
+        if (a.delta < INF || a.bctl) {  // ordered list mode / priority bands: the entering keys
             if (kmin_self < INF) atomicMin(&L.key[0], __float_as_uint((float)kmin_self));
 #pragma unroll
             for (int q = 0; q < 4; ++q)
                 if (kmin[q] < INF) atomicMin(&L.key[q + 1], __float_as_uint((float)kmin[q]));
         }
         if (tid == 0) L.last = a.max_rounds == 1 ? -1 : (int)last_changed;  // -1: see flags bit 7
-        if (COH && (a.sched & 1) && tid == 0 && !early) L.pend = pend_old;
+        if (COH && (a.sched & 1) && tid == 0) L.pend = pend_old;
         if constexpr (COH) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
         __syncthreads();
         EIK_PROBE(7);
@@ -653,39 +597,19 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
             const unsigned pend = L.pend & (kPending | kFromN | kFromS | kFromW | kFromE);
             const bool self = (f & 128u) != 0u;
             if ((!self && !pend) || pass + 1 >= a.max_passes || a.max_rounds != 1) {
-                if (once) {
-                    // EIK_WB_ONCE: the last pass's edges have drained, so its neighbour activations
-                    // go now, ahead of the interior stores and their drain (activate_after then only
-                    // re-queues the tile itself: the bits cleared here are not read before it)
-                    activate_neighbours(a, tile, f | L.flags_acc, L.key, 0, 0u);  // lanes 0..4
-                    if (tid == 0) {
-                        L.flags = f & ~0x6fu;
-                        L.flags_acc = 0u;
-                    }
-                    asm volatile("" ::: "memory");
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        if (dirty & (1u << k)) {
-                            const int ry = (tid >> 4) + 16 * k;
-                            R v[4];
-#pragma unroll
-                            for (int e = 0; e < 4; ++e) v[e] = cell_t(Ts, (ry + 1) * kLds + cx + e + 1, cx + e + 1);
-                            T.st4((y0 + ry) * a.W + x0 + cx, v);
-                        }
-                    }
-                }
                 store_deferred();  // drained by the persistent loop before the finish
                 break;
             }
             // the halo reload is issued first and the budget charge goes to wave 1, so wave 0's
             // activation atomics are the only round trips the next pass waits for
-            const R hv = early ? hv_early : load_halo();
+            const R hv = load_halo();
             if (tid == 64) charge_inplace_pass(a);  // in-place passes: stats and the visit budget
             // a.sched bit 1: after the first pass, neighbour activations wait for the visit's end
             // (one activation with the converged edges instead of one per pass)
             const bool defer = (a.sched & 2) && pass > 0;
             if constexpr (EIK_ACT_SPLIT)
-                act_tile = activate_neighbours_issue(a, tile, defer ? 0u : f, act_old);  // completed in the next sweep
+                act_tile = activate_neighbours_issue(a, tile, defer ? 0u : f, act_old, L.key, act_k,
+                                                     act_kold);  // completed in the next sweep
             else
                 activate_neighbours(a, tile, defer ? 0u : f, L.key, 0, 0u);  // lanes 0..4 (T already drained)
             if (defer && tid == 0) L.flags_acc |= f & 0x6fu;
@@ -716,8 +640,10 @@ __device__ __forceinline__ void activate_after(const Fim2dArgs& a, int tile, con
         const bool self = L.last < 0 ? (f & 128u) != 0u : L.last != 0;
         if (a.mode == kModePersistent) {
             const unsigned p = L.pend & (kFromN | kFromS | kFromW | kFromE);
-            if (self || (L.pend & kPending))
+            if (self || (L.pend & kPending)) {
+                if (self && a.bctl) atomicMin(&a.key[tile], 0u);  // priority mode: a self re-queue goes first
                 atomicOr(&a.qstate[tile], kPending | (self ? kSelf : p));  // busy: re-queued by its own finish
+            }
         } else if (self) {
             enqueue(a, tile, list, stamp, __uint_as_float(L.key[0]));
         }
@@ -813,13 +739,25 @@ __device__ void live_agent(const Fim2dArgs& a, unsigned* sh) {
             const R* T = static_cast<const R*>(a.T);
             R* tg[4];
             for (int k = 0; k < 4; ++k) tg[k] = static_cast<R*>(box->send[par][k]);
+            // EIK_OPT_LIVE_PACK 1: a cell of a tile that is pending or busy is not packed -- the
+            // receiver's strip of this parity keeps an older (larger) value, which the min-merge
+            // ignores; a round whose snapshot saw no tile pending or busy packs every cell, so the
+            // convergence vote's proof (dd.solve_live) is unchanged
+            const bool skip_busy = a.live_pack && sh[2] != 0u;
+            auto idle = [&](int64_t ty, int64_t tx) {
+                return !skip_busy ||
+                       (__hip_atomic_load(&a.qstate[ty * a.ntx + tx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &
+                        (kPending | kBusy)) == 0u;
+            };
             for (int64_t i = tid; i < a.W; i += blockDim.x) {
-                if (tg[0]) st_scoped(tg[0] + i, ld_agent(T + i), __HIP_MEMORY_SCOPE_SYSTEM);
-                if (tg[1]) st_scoped(tg[1] + i, ld_agent(T + (a.H - 1) * a.W + i), __HIP_MEMORY_SCOPE_SYSTEM);
+                if (tg[0] && idle(0, i / kTile)) st_scoped(tg[0] + i, ld_agent(T + i), __HIP_MEMORY_SCOPE_SYSTEM);
+                if (tg[1] && idle(a.nty - 1, i / kTile))
+                    st_scoped(tg[1] + i, ld_agent(T + (a.H - 1) * a.W + i), __HIP_MEMORY_SCOPE_SYSTEM);
             }
             for (int64_t i = tid; i < a.H; i += blockDim.x) {
-                if (tg[2]) st_scoped(tg[2] + i, ld_agent(T + i * a.W), __HIP_MEMORY_SCOPE_SYSTEM);
-                if (tg[3]) st_scoped(tg[3] + i, ld_agent(T + i * a.W + a.W - 1), __HIP_MEMORY_SCOPE_SYSTEM);
+                if (tg[2] && idle(i / kTile, 0)) st_scoped(tg[2] + i, ld_agent(T + i * a.W), __HIP_MEMORY_SCOPE_SYSTEM);
+                if (tg[3] && idle(i / kTile, a.ntx - 1))
+                    st_scoped(tg[3] + i, ld_agent(T + i * a.W + a.W - 1), __HIP_MEMORY_SCOPE_SYSTEM);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: peer stores complete
         } else if (op == kLiveMerge) {
@@ -844,7 +782,7 @@ __device__ void live_agent(const Fim2dArgs& a, unsigned* sh) {
                             ty = (int)(i / kTile);
                             tx = side == 2 ? 0 : a.ntx - 1;
                         }
-                        qpush(a, ty * a.ntx + tx, kFromN << side);
+                        qpush(a, ty * a.ntx + tx, kFromN << side, (float)v);
                     }
                 }
             }
@@ -881,7 +819,7 @@ __global__ __launch_bounds__(kThreads, WPS) void fim2d_persist_kernel(Fim2dArgs 
     int tile = -1;
     unsigned nvis = 0;  // wave 0 lane 0: visits not yet added to the global counter
     for (;;) {
-        if ((EIK_EDGE_FIRST || kWbOnce<R>) && tile >= 0) {  // uniform: every wave's deferred interior stores
+        if (EIK_EDGE_FIRST && tile >= 0) {  // uniform: every wave's deferred interior stores
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // complete before the finish
             __syncthreads();
         }
@@ -902,13 +840,16 @@ __global__ __launch_bounds__(kThreads, WPS) void fim2d_persist_kernel(Fim2dArgs 
                 }
             }
             EIK_PROBE(5);
-        } else if (threadIdx.x == 64) {
+        } else if (threadIdx.x < 128 && (a.bctl || threadIdx.x == 64)) {
+            // wave 1 takes the next tile (priority bands: the whole wave; else lane 64)
             unsigned trig = 0;
-            const int t = qgrab(a, trig);
-            L.tile = t;
-            L.dirs = sweep_dirs(trig);
-            L.fresh = !(trig & kVisited);
-            if (t >= 0) EIK_VISIT(t, trig, L.dirs);
+            const int t = a.bctl ? qgrab_prio(a, trig) : qgrab(a, trig);
+            if (threadIdx.x == 64) {
+                L.tile = t;
+                L.dirs = sweep_dirs(trig);
+                L.fresh = !(trig & kVisited);
+                if (t >= 0) EIK_VISIT(t, trig, L.dirs);
+            }
         }
         __syncthreads();
         EIK_PROBE(6);
@@ -936,7 +877,7 @@ __global__ void fim2d_init_kernel(R* __restrict__ T, int64_t n, unsigned* __rest
             if (counts) counts[t] = 0u;
             if (edge) edge[t] = 0u;
         }
-        if (t < 6 && visits) visits[t] = 0u;  // full visits, in-place passes, fresh visits (u64 each)
+        if (t < 22 && visits) visits[t] = 0u;  // full visits, in-place passes, fresh visits, 8 queue counters (u64 each)
     }
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) T[i] = Real<R>::inf();
     if (ecol)
@@ -974,6 +915,50 @@ __global__ void fim2d_seed_kernel(Fim2dArgs a, const int64_t* __restrict__ goals
     a.key[tile] = 0u;  // T = 0 enters at the goal
     const int pos = atomicAdd(&a.counts[0], 1);
     a.lists[pos] = tile;
+}
+
+// Priority bands (EIK_OPT_PRIO): the band width, 64 x the geometric mean of the finite positive costs
+// (one tile width of T at a typical cost; C2's cost mean is 40 but its median 3.6 -- obstacles
+// dominate the mean) x the option's multiplier, from 4096 cells sampled across the raster (one block).
+template <typename R>
+__global__ __launch_bounds__(256) void prio_delta_kernel(const R* __restrict__ cost, int64_t n, float mult,
+                                                          float* __restrict__ out) {
+    __shared__ double ssum[4];
+    __shared__ int scnt[4];
+    double sum = 0.0;
+    int cnt = 0;
+    for (int i = threadIdx.x; i < 4096; i += 256) {
+        const double c = (double)cost[(int64_t)((double)i * (double)n / 4096.0)];
+        if (c > 0.0 && c < Real<double>::inf()) {
+            sum += log(c);
+            ++cnt;
+        }
+    }
+    for (int d = 32; d > 0; d >>= 1) {
+        sum += __shfl_down(sum, d);
+        cnt += __shfl_down(cnt, d);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        ssum[threadIdx.x >> 6] = sum;
+        scnt[threadIdx.x >> 6] = cnt;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const double s = ssum[0] + ssum[1] + ssum[2] + ssum[3];
+        const int c = scnt[0] + scnt[1] + scnt[2] + scnt[3];
+        const double g = c ? exp(s / c) : 1.0;
+        *out = (float)(mult * 64.0 * g > 1e-30 ? mult * 64.0 * g : 1e-30);
+    }
+}
+
+hipError_t fim2d_prio_delta(const void* cost, bool f64, int64_t n, float mult, float* out, hipStream_t st) {
+    if (f64)
+        hipLaunchKernelGGL(prio_delta_kernel<double>, dim3(1), dim3(256), 0, st, static_cast<const double*>(cost), n,
+                           mult, out);
+    else
+        hipLaunchKernelGGL(prio_delta_kernel<float>, dim3(1), dim3(256), 0, st, static_cast<const float*>(cost), n,
+                           mult, out);
+    return hipGetLastError();
 }
 
 // After each persistent launch: the tickets of its idle waiters ran ahead of the tail --

@@ -372,7 +372,8 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
     const int kPasses = COH ? a.max_passes : 1;
     unsigned dirs = L.dirs;  // this pass's sweeps (register: see fim2d.hip process_tile)
     int act_tile = -1;       // EIK_ACT_SPLIT_L: this lane's activation issued at the last pass boundary
-    unsigned act_old = 0u;
+    unsigned act_old = 0u, act_kold = 0u;
+    float act_k = 0.f;  // (keys: priority mode only, not used by the layered solver)
     for (int pass = 0;; ++pass) {
         if (EIK_ACT_SPLIT_L && act_tile >= 0) {  // wave 0 lanes 1..4, as its sweep starts (fim2d.hip)
             qpush_complete(a, act_tile, act_old);
@@ -419,7 +420,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
         const LCell<R> hv = load_halo();
         if (tid == 64) charge_inplace_pass(a);  // in-place passes: stats and the visit budget
         if constexpr (COH && EIK_ACT_SPLIT_L)
-            act_tile = activate_neighbours_issue(a, tile, f, act_old);  // queued as the next pass starts
+            act_tile = activate_neighbours_issue(a, tile, f, act_old, L.key, act_k, act_kold);  // queued as the next pass starts
         else
             activate_neighbours(a, tile, f, L.key, 0, 0u);  // lanes 0..4 (T already drained)
         dirs = 0xFu;  // a self revisit: every direction

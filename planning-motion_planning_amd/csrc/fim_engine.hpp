@@ -250,28 +250,113 @@ __device__ __forceinline__ void qslot_put_front(const Fim2dArgs& a, int tile) {
 // pass boundary and finish the second inside its next sweep.  Between the two the neighbour is
 // PENDING but not yet queued: other activations of it do nothing (its entry is on the way), and
 // the activating tile is still busy, so the active count stays above zero.
+// ---------------------------------------------------------------- priority bands (EIK_OPT_PRIO)
+// The FIFO serves tiles in activation order.  With a backlog (every workgroup busy, tiles waiting:
+// the middle of a large solve) that order processes tiles far ahead of the front's settled region,
+// whose halos are still coarse, and they are visited again.  tools/sched_sim.c (lock-step, 512
+// workers): serving the waiting tiles lowest entering T first takes C2 108 -> 90 rounds and
+// 40.6k -> 33.1k passes, an 8192^2 raster 265 -> 190 rounds (Dijkstra order at tile level; a
+// bucket queue of width 250-1000 on C2 does as well as the exact heap).  The device form:
+//  * a tile that becomes pending goes to the FIFO when a workgroup waits there (no backlog: order
+//    is moot and the waiter takes it at once), else to band min(T / pdelta, kBands - 1): kBands
+//    FIFOs of tile ids with their own head / tail words; pdelta = 64 x the geometric mean of the
+//    finite costs (prio_delta_kernel; about one tile width of T) x EIK_OPT_PRIO;
+//  * a pending tile activated again with a key a whole band lower gets a second entry in the lower
+//    band (decrease-key: the sim's lazy re-push; a bucket that kept its first entry did worse than the
+//    FIFO, 170 vs 108 rounds); whichever entry is taken first claims the tile, the others are stale
+//    and are dropped when taken (the claim is a CAS pending -> busy on the state word);
+//  * every workgroup looking for work takes a FIFO ticket; the oldest waiter (its ticket is the next
+//    slot to be filled) moves up to 32 band entries to the FIFO's tail in band order -- three
+//    quarters from the lowest bands, a quarter from the highest (band_dispatch) -- so the band heads
+//    see one claimant at a time.
+// a.key[tile] holds the smallest key since the tile's last claim (atomicMin at each activation).
+__device__ __forceinline__ unsigned band_of(const Fim2dArgs& a, float k) {
+    const float q = k / *a.pdelta;  // k >= 0 (or +inf); a kernel-constant word (scalar cache)
+    return q < float(kBands - 1) ? (unsigned)q : unsigned(kBands - 1);
+}
+#ifndef EIK_QDEBUG
+#define EIK_QDEBUG 0
+#endif
+// queue counters for tools (eik_fim2d_qcount): a.visits[3 + i]
+__device__ __forceinline__ void qcount(const Fim2dArgs& a, int i) {
+    if (EIK_QDEBUG) atomicAdd(a.visits + 3 + i, 1ull);
+}
+__device__ __forceinline__ void band_put(const Fim2dArgs& a, unsigned b, int tile) {
+    qcount(a, 7);
+    const unsigned long long pos = atomicAdd(&a.bctl[16 * b + 8], 1ull);
+    __hip_atomic_store(&a.bslot[(size_t)b * (a.bmask + 1ull) + (pos & a.bmask)], (unsigned)tile + 1u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+// a workgroup waits on the FIFO (a ticket past the filled slots)
+__device__ __forceinline__ bool fifo_waiters(const Fim2dArgs& a) {
+    const unsigned long long h = __hip_atomic_load(a.qhead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long t = __hip_atomic_load(a.qtail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return h > t;
+}
+// a newly pending tile with key k (priority mode): to a waiting workgroup, else to its band
+__device__ __forceinline__ void prio_put(const Fim2dArgs& a, int tile, float k) {
+    if (fifo_waiters(a))
+        qslot_put(a, tile);
+    else
+        band_put(a, band_of(a, k), tile);
+}
+// claim a taken entry: pending -> busy (stale entries -- the tile busy, or no longer pending -- fail)
+__device__ __forceinline__ bool prio_claim(const Fim2dArgs& a, int tile, unsigned& trig) {
+    unsigned old = __hip_atomic_load(&a.qstate[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+        if ((old & kBusy) || !(old & kPending)) return false;
+        const unsigned prev = atomicCAS(&a.qstate[tile], old, kBusy | kVisited);
+        if (prev == old) {
+            trig = old;
+            __hip_atomic_store(&a.key[tile], 0x7f800000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return true;
+        }
+        old = prev;
+    }
+}
+
 __device__ __forceinline__ unsigned qpush_issue(const Fim2dArgs& a, int tile, unsigned trig) {
     const unsigned old = atomicOr(&a.qstate[tile], kPending | trig);
     EIK_ACT(tile, old);
     return old;
 }
-__device__ __forceinline__ void qpush_complete(const Fim2dArgs& a, int tile, unsigned old) {
+// priority mode: the key's atomicMin beside the state word's atomicOr (both in flight together)
+__device__ __forceinline__ unsigned qpush_issue_key(const Fim2dArgs& a, int tile, unsigned trig, float k, unsigned& kold) {
+    kold = atomicMin(&a.key[tile], __float_as_uint(k));  // k >= 0: float order == unsigned order
+    return qpush_issue(a, tile, trig);
+}
+__device__ __forceinline__ void qpush_complete(const Fim2dArgs& a, int tile, unsigned old, float k = 0.f,
+                                               unsigned kold = 0x7f800000u) {
     if ((old & (kPending | kBusy)) == 0u) {
         atomicAdd(a.qactive, 1);  // before the slot store: a waiter never sees "empty and idle"
-        if (!(old & kVisited) && a.fresh_first)
+        if (a.bctl)
+            prio_put(a, tile, fminf(k, __uint_as_float(kold)));
+        else if (!(old & kVisited) && a.fresh_first)
             qslot_put_front(a, tile);
         else
             qslot_put(a, tile);
+    } else if (a.bctl && !(old & kBusy)) {  // queued: a lower band gets a second entry (decrease-key)
+        const unsigned b = band_of(a, k);
+        if (b < band_of(a, __uint_as_float(kold))) {
+            qcount(a, 6);
+            band_put(a, b, tile);
+        }
     }
 }
-__device__ __forceinline__ void qpush(const Fim2dArgs& a, int tile, unsigned trig) {
+__device__ __forceinline__ void qpush(const Fim2dArgs& a, int tile, unsigned trig, float k = 0.f) {
+    if (a.bctl) {
+        unsigned kold;
+        const unsigned old = qpush_issue_key(a, tile, trig, k, kold);
+        qpush_complete(a, tile, old, k, kold);
+        return;
+    }
     qpush_complete(a, tile, qpush_issue(a, tile, trig));
 }
 
 __device__ __forceinline__ void activate(const Fim2dArgs& a, int tile, int list, unsigned stamp, float key,
                                          unsigned trig) {
     if (a.mode == kModePersistent)
-        qpush(a, tile, trig);
+        qpush(a, tile, trig, key);
     else
         enqueue(a, tile, list, stamp, key);
 }
@@ -306,9 +391,11 @@ __device__ __forceinline__ void activate_neighbours(const Fim2dArgs& a, int tile
 // issues its side's state-word atomicOr and returns the neighbour (-1: none) with `old` to be
 // passed to qpush_complete later; thread 0 flags changed subdomain edges as above.
 __device__ __forceinline__ int activate_neighbours_issue(const Fim2dArgs& a, int tile, unsigned f, unsigned& old,
+                                                         const unsigned* key, float& kq, unsigned& kold,
                                                          int tid = threadIdx.x) {
     old = 0u;
     if (tid >= 5) return -1;
+    kq = __uint_as_float(key[tid]);  // priority mode: the side's smallest new edge value
     const int map = tile / a.tiles_per_map;
     const int rem = tile - map * a.tiles_per_map;
     const int ty = rem / a.ntx, tx = rem - (rem / a.ntx) * a.ntx;
@@ -319,7 +406,7 @@ __device__ __forceinline__ int activate_neighbours_issue(const Fim2dArgs& a, int
     if (tid == 2 && (f & 2u) && ty + 1 < a.nty) { nb = base + rem + a.ntx; trig = kFromN; }
     if (tid == 3 && (f & 4u) && tx > 0) { nb = base + rem - 1; trig = kFromE; }
     if (tid == 4 && (f & 8u) && tx + 1 < a.ntx) { nb = base + rem + 1; trig = kFromW; }
-    if (nb >= 0) old = qpush_issue(a, nb, trig);
+    if (nb >= 0) old = a.bctl ? qpush_issue_key(a, nb, trig, kq, kold) : qpush_issue(a, nb, trig);
     if (tid == 0 && a.edge_dirty) {
         unsigned e = 0;
         if ((f & 1u) && ty == 0) e |= 1u;
@@ -395,10 +482,151 @@ __device__ __forceinline__ void charge_inplace_pass(const Fim2dArgs& a) {
 // while busy (it stays counted), else it stops counting as active.
 __device__ __forceinline__ void qfinish(const Fim2dArgs& a, int tile) {
     const unsigned old = atomicAnd(&a.qstate[tile], ~kBusy);
-    if (old & kPending)
-        qslot_put(a, tile);
-    else
+    if (old & kPending) {
+        if (a.bctl)  // its key: the smallest activation since its claim (0 for a self re-queue)
+            prio_put(a, tile, __uint_as_float(__hip_atomic_load(&a.key[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+        else
+            qslot_put(a, tile);
+    } else {
         atomicSub(a.qactive, 1);
+    }
+}
+
+// inclusive prefix sum over the wave's 64 lanes
+__device__ __forceinline__ unsigned wave_incl_sum(unsigned v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned u = __shfl_up(v, d);
+        if (lane >= d) v += u;
+    }
+    return v;
+}
+
+// Priority mode, one wave (all lanes; the oldest FIFO waiter): move up to kDispatch entries of the
+// lowest non-empty bands, in band order, to the FIFO's tail -- each band's share claimed by one CAS
+// of its head (one lane per band, all at once) -- so the waiters take them lowest key first.  Only
+// the oldest waiter does this, so the band heads see little contention (a first design where every
+// idle workgroup CAS-ed the lowest band's head lost ~900k CASes per C2 solve and ran 20x slower),
+// and the batch is the bands' throughput: C4 takes ~9 tiles per us, and one band per dispatch (a few
+// entries each, ~3 round trips) held narrow bands to a fraction of that (C4 2.7 vs 10.9 Gcells/s).
+constexpr unsigned kDispatch = 32;
+__device__ __forceinline__ bool band_dispatch(const Fim2dArgs& a) {
+    const int lane = threadIdx.x & 63;
+    unsigned long long h = 0, t = 0;
+    if (lane < kBands) {
+        h = __hip_atomic_load(&a.bctl[16 * lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        t = __hip_atomic_load(&a.bctl[16 * lane + 8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const unsigned avail = t > h ? (unsigned)(t - h < kDispatch ? t - h : kDispatch) : 0u;
+    const unsigned long long ne = __ballot(avail != 0u);
+    if (!ne) return false;
+    // lowest bands first, but a quarter of the batch goes to the highest non-empty band: the front's
+    // first visits carry the largest keys, and refinements behind it (low keys, re-queued at key 0
+    // when a visit ends still changing) must not starve it -- narrow bands did (C4 2.7 Gcells/s at
+    // a band width of 60 against 10.9 for the FIFO)
+    const int hi = 63 - __builtin_clzll(ne);
+    const unsigned lo_budget = kDispatch - kDispatch / 4;
+    const unsigned before = wave_incl_sum(avail) - avail;  // entries of the lower bands
+    unsigned take = before >= lo_budget ? 0u : (avail < lo_budget - before ? avail : lo_budget - before);
+    if (lane == hi) {
+        const unsigned more = avail - take < kDispatch / 4 ? avail - take : kDispatch / 4;
+        take += more;
+    }
+    const unsigned got = take && atomicCAS(&a.bctl[16 * lane], h, h + take) == h ? take : 0u;
+    const unsigned end = wave_incl_sum(got), start = end - got;
+    const unsigned total = __shfl(end, 63);
+    if (total == 0u) return false;  // another dispatcher moved first: look again at the next poll
+    qcount(a, 5);
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(a.qtail, (unsigned long long)total);
+    base = __shfl(base, 0);
+    // lane e < total moves entry e: band b where start_b <= e < end_b, offset e - start_b
+    int b = -1;
+    unsigned long long src = 0;
+    unsigned long long mask = __ballot(got != 0u);
+    while (mask) {
+        const int j = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        const unsigned sj = __shfl(start, j), ej = __shfl(end, j);
+        const unsigned long long hj = __shfl(h, j);
+        if ((unsigned)lane >= sj && (unsigned)lane < ej) {
+            b = j;
+            src = hj + (lane - sj);
+        }
+    }
+    if (b >= 0) {
+        // the entry's producer may still be storing it (it took the tail first)
+        unsigned* slot = &a.bslot[(size_t)b * (a.bmask + 1ull) + (src & a.bmask)];
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        unsigned v;
+        while ((v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > a.qtimeout) {
+                atomicOr(a.qerror, 1u);
+                v = 1u;  // (the error flag ends the solve; the FIFO slot gets a harmless entry)
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        __hip_atomic_store(slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&a.qslot[(base + lane) & a.qmask], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return true;
+}
+
+// Priority mode: qgrab for one whole wave.  Every workgroup takes a FIFO ticket; pushes go to the
+// FIFO while tickets wait, else to the bands, and the oldest waiter moves band entries to the FIFO
+// in band order.  Entries are claimed by a CAS (stale ones dropped: take another ticket).
+__device__ __forceinline__ int qgrab_prio(const Fim2dArgs& a, unsigned& trig) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        if (__hip_atomic_load(a.qerror, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return -1;
+        unsigned long long pos = 0;
+        if (lane == 0) pos = atomicAdd(a.qhead, 1ull);
+        pos = __shfl(pos, 0);
+        unsigned* slot = &a.qslot[pos & a.qmask];
+        for (unsigned spin = 0;; ++spin) {
+            unsigned v = 0;
+            int oldest = 0;
+            if (lane == 0) {
+                v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (!v) oldest = __hip_atomic_load(a.qtail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == pos;
+            }
+            v = __shfl(v, 0);
+            if (v != 0u) {
+                int got = -1;
+                unsigned tg = 0u;
+                if (lane == 0) {
+                    __hip_atomic_store(slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    got = prio_claim(a, (int)(v - 1u), tg) ? (int)(v - 1u) : -1;
+                    qcount(a, got >= 0 ? 3 : 4);
+                }
+                got = __shfl(got, 0);
+                trig = __shfl(tg, 0);
+                if (got >= 0) return got;
+                break;  // a stale entry: this ticket is spent, take another
+            }
+            // the next slot filled is this one: feed the FIFO from the bands, then poll again at once
+            // (an empty dispatch falls through to the end / error checks and the sleep)
+            if (__shfl(oldest, 0) && band_dispatch(a)) continue;
+            if ((spin & 7u) == 7u) {
+                int stop = 0;
+                if (lane == 0) {
+                    // (live DD: idle is not the end -- a halo merge may queue tiles until the release)
+                    stop = (a.qhold ? __hip_atomic_load(a.qhold, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u
+                                    : __hip_atomic_load(a.qactive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) ||
+                           __hip_atomic_load(a.qerror, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+                    if (!stop && __builtin_amdgcn_s_memrealtime() - t0 > a.qtimeout) {
+                        atomicOr(a.qerror, 1u);
+                        stop = 1;
+                    }
+                }
+                if (__shfl(stop, 0)) return -1;
+            }
+            __builtin_amdgcn_s_sleep(4);
+        }
+    }
 }
 
 }  // namespace eik

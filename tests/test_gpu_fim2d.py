@@ -270,7 +270,8 @@ def test_pass_cap_option(passes):
 
 
 @pytest.mark.parametrize("opts", [(("SCHED", 0),), (("SCHED", 2),), (("SCHED", 3),), (("FRESH_FIRST", 1),),
-                                  (("SCHED", 0), ("FRESH_FIRST", 1))])
+                                  (("SCHED", 0), ("FRESH_FIRST", 1)), (("PRIO", 0.1),), (("PRIO", 1),),
+                                  (("PRIO", 1e4),), (("PRIO", 1), ("SCHED", 0))])
 def test_schedule_options(opts):
     """The queue-scheduling options (EIK_OPT_SCHED other than the default 1, EIK_OPT_FRESH_FIRST)
     change the order of tile visits, never the fixed point: single map and batch vs the oracle."""
@@ -344,3 +345,50 @@ def test_visit_budget_device_buffers(neg):
             f.close()
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("delta", [0.02, 1.0, 20.0])
+@pytest.mark.parametrize("kind", ["maze", "blobs", "obst"])
+def test_priority_bands_fp64(kind, delta):
+    """EIK_OPT_PRIO (priority bands, fim_engine.hpp): waiting tiles taken lowest entering T first,
+    with second entries on a key drop and stale entries dropped at the claim -- a different visit
+    order, the same fixed point: fp64 fields against the oracle (<= 1e-9), incl. a maze (keys far
+    beyond the last band: the open-ended band is a FIFO) and band widths of a few cells' cost."""
+    import eikonal
+    from eikonal import _lib as L
+
+    rng = np.random.default_rng(int(100 * delta) + len(kind))
+    H, W = 777, 1100
+    c = rng.uniform(1, 10, (H, W))
+    if kind == "obst":
+        c[rng.random((H, W)) < 0.2] = np.inf
+    elif kind == "maze":
+        for x in range(6, W - 2, 10):
+            c[:, x] = np.inf
+            c[3 if (x // 10) % 2 == 0 else H - 4, x] = 2.0
+    else:
+        yy, xx = np.mgrid[0:H, 0:W]
+        for _ in range(30):
+            cy, cx, r = rng.integers(0, H), rng.integers(0, W), rng.integers(10, 90)
+            c[(yy - cy) ** 2 + (xx - cx) ** 2 <= r * r] = 300.0
+    goal = [W // 2, H // 3]
+    c[goal[1], goal[0]] = 1.0
+    R = oracle_field(c, goal)
+    fin = np.isfinite(R)
+    ctx = eikonal.Context(0)
+    try:
+        errs = []
+        for prio in (0.0, delta):  # the FIFO beside it: the same order of rounding differences
+            ctx.set_option(L.OPT_PRIO, prio)
+            T = ctx.tmap2d(c, goal, dtype=np.float64)
+            assert np.array_equal(np.isfinite(T), fin) and T[goal[1], goal[0]] == 0
+            errs.append(np.abs(T[fin] - R[fin]))
+        # fp64 rounding of the device's step (eik_common.hpp EIK_CHAIN: one more rounding at T's
+        # magnitude than the reference) accumulated along the maze's ~1e5-cell paths: 1e-9 absolute,
+        # or 1e-13 relative where T is large (T ~ 5e5 there: 1e-9 would be 2e-15, a few ulps) -- the
+        # FIFO solve measures 5.8e-14
+        lim = np.maximum(1e-9, 1e-13 * R[fin])
+        for name, e in zip(("fifo", "prio"), errs):
+            assert (e <= lim).all(), (name, e.max(), (e / np.maximum(R[fin], 1)).max())
+    finally:
+        ctx.close()

@@ -116,6 +116,38 @@ def test_c2_full_size_fp64_vs_oracle(env):
     assert np.abs(path - ref).max() <= 1e-6
 
 
+def test_c2_full_size_fp64_priority_bands(env):
+    """The headline solve with EIK_OPT_PRIO (priority bands at the default width) against
+    the default FIFO solve of the same raster: the same fixed point up to rounding (masks equal,
+    <= 1e-11 relative), and the Godunov properties of check_properties."""
+    torch, eikonal, L, terrain, dev, ctx = env
+    N = 4096
+    cost = terrain.cost_block(0, 0, N, N, N, N, seed=42, device=dev).double().contiguous()
+    goal = (N // 2, N // 2)
+    stream = torch.cuda.current_stream(dev)
+    out = []
+    for prio in (0.0, 1.0):
+        c2 = eikonal.Context(0)
+        try:
+            c2.set_option(L.OPT_PRIO, prio)
+            T = torch.empty_like(cost)
+            fim = eikonal.Fim2d(c2, 1, N, N, L.EIK_F64)
+            fim.solve(cost.data_ptr(), T.data_ptr(), [goal], stream.cuda_stream)
+            torch.cuda.synchronize()
+            out.append((T, fim.stats()))
+            fim.close()
+        finally:
+            c2.close()
+    (T0, s0), (T1, s1) = out
+    fin = torch.isfinite(T0)
+    assert torch.equal(fin, torch.isfinite(T1))
+    rel = ((T1[fin] - T0[fin]).abs() / T0[fin].clamp(min=1e-30)).max().item()
+    assert rel <= 1e-11, rel
+    check_properties(torch, T1, cost, goal, tol=1e-11)
+    print(f"C2 fp64 FIFO: {s0['tile_visits']} visits + {s0['inplace_passes']} passes; priority bands: "
+          f"{s1['tile_visits']} + {s1['inplace_passes']}")
+
+
 def test_c2_full_size_vs_oracle(env):
     torch, eikonal, L, terrain, dev, ctx = env
     N = 4096

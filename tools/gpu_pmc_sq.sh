@@ -1,7 +1,7 @@
 # SQ-level counters of the persistent FIM kernel on the bench raster (one --pmc pass per group,
 # each its own run): LDS vs VALU occupancy of the sweep.   bash tools/gpu_pmc_sq.sh
 export TMPDIR=/tmp
-O=gpurun_out
+O=${O:-gpurun_out}
 rocprofv3 -L > $O/pmc_list.txt 2>&1 || true
 B=${BENCH:-"python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-path --no-timing --no-extra"}
 i=0
