@@ -107,10 +107,14 @@ typedef enum {
                                 of tiles that are neither pending nor busy (converged edges), so a
                                 neighbour is not re-activated by every intermediate refinement
                                 (a round whose snapshot had no tile pending or busy packs all)   */
-    EIK_OPT_PRIO = 15        /* 2D persistent solves of one or two maps: v > 0 serves waiting tiles
+    EIK_OPT_PRIO = 15,       /* 2D persistent solves of one or two maps: v > 0 serves waiting tiles
                                 lowest entering T first, in 64 bands of width v x 64 x the geometric
-                                mean of the finite costs (fim_engine.hpp "priority bands");
-                                0 = the FIFO                                                      */
+                                mean of the finite costs (fim_engine.hpp "priority bands"); 0 =
+                                the FIFO; < 0 (default) = 1 for fp64 solves, 0 for fp32          */
+    EIK_OPT_LAYER_PLANAR = 16 /* few-layer 3D volumes (the layered solver): 1 solves on layer-planar
+                                copies [nl][H][W] of the solved layers (one copy in, one out per
+                                solve; every tile-row access one contiguous run per layer);
+                                0 = in the volume's [y][x][L] layout                             */
 } eik_option;
 
 typedef enum { EIK_MODE_LIST = 0, EIK_MODE_PERSISTENT = 1 } eik_mode;
@@ -202,6 +206,20 @@ void eik_fim2d_destroy(eik_fim2d* fim);
 
 /* Ghost strips for a subdomain of a decomposed raster (device pointers, NULL = +inf border):
  * north/south length W, west/east length H.  Values are min-merged by eik_fim2d_merge_ghost. */
+/* A block of a domain-decomposed few-layer 3D volume ([H][W][L], layers z0 .. z0+nl-1 solved: the
+ * layered solver; FastMarching3D.py:19-145 semantics; SURVEY §8(e) "C5: split x-y only, layers stay
+ * together").  The handle is an eik_fim2d: eik_fim2d_set_ghosts (strips of nl values per edge cell,
+ * [i][z]), eik_fim2d_iterate (one persistent launch to local convergence), eik_fim2d_pack_edges,
+ * eik_fim2d_merge_ghost, eik_fim2d_active, eik_fim2d_stats and eik_fim2d_destroy apply; start with
+ * eik_fim3dl_start (goal (x, y, z), z absolute; x < 0: the goal is in another block). */
+int eik_fim3dl_create(eik_ctx* ctx, int64_t H, int64_t W, int64_t L, int z0, int nl, int dtype, eik_fim2d** out);
+int eik_fim3dl_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t goal[3], void* stream);
+
+/* Diagnostics: the queue counters of the solver's last persistent launch (builds with -DEIK_QDEBUG=1:
+ * FIFO claims, stale FIFO entries, band dispatches, decrease-key entries, band puts at out[3..7];
+ * zeros otherwise).  tools/prio_probe.py. */
+int eik_fim2d_qcount(const eik_fim2d* f, uint64_t out[8]);
+
 int eik_fim2d_set_ghosts(eik_fim2d* fim, void* north, void* south, void* west, void* east);
 
 /* Bind device cost/T (B*H*W of dtype), set T = inf, T[goal] = 0, seed the goal tiles.

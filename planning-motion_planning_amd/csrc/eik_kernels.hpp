@@ -46,8 +46,9 @@ struct Fim2dArgs {
     // west / east halo of a tile visit is one contiguous 64-cell read instead of 64 rows' lines
     void* ecol;
     // layered solver (fim2dl.hip): cell (y, x) holds ls consecutive values, layers z0.. solved
-    int64_t ls;            // layer stride (1 for the 2D solver)
-    int z0;                // first solved layer
+    int64_t ls;            // cell stride (the [y][x][L] volume: L; 1 for the 2D solver and layer-planar copies)
+    int z0;                // offset of the first solved layer in a cell (the volume: its index; planar: 0)
+    int64_t lzs;           // layer stride: 1 in the [y][x][L] volume, H * W in a layer-planar copy
     // live domain decomposition (eik_fim2d_launch with live != 0): the persistent launch stays up
     // -- its last workgroup is the halo agent serving the host's commands -- and ends when
     // *qhold != 0
@@ -101,7 +102,14 @@ hipError_t fim2d_pack_edges(const Fim2dArgs& a, bool f64, void* n, void* s, void
 // (persistent mode only; a.ls / a.z0 set, no ghosts, no ordering window; a.nty counts tiles of
 // fim2dl_rows(f64) rows).
 int fim2dl_rows(bool f64);
-hipError_t fim2dl_init(const Fim2dArgs& a, bool f64, int64_t gx, int64_t gy, int64_t gz, hipStream_t st);
+hipError_t fim2dl_init(const Fim2dArgs& a, bool f64, int64_t gx, int64_t gy, int64_t gz, int64_t n, hipStream_t st);
+// [y][x][L] volume <-> layer-planar copy [nl][H][W] of layers z0 .. z0+nl-1 (in: volume -> copy;
+// out: copy -> volume, the other layers of every cell set to +inf)
+hipError_t layer_planar(const void* src, void* dst, bool f64, int64_t hw, int64_t L, int z0, int nl, bool in,
+                        hipStream_t st);
+// layered domain decomposition: edges of nl values per cell into strips; strips min-merged into ghosts
+hipError_t fim2dl_pack_edges(const Fim2dArgs& a, int nl, bool f64, void* n, void* s, void* w, void* e, hipStream_t st);
+hipError_t fim2dl_merge_ghost(const Fim2dArgs& a, int nl, bool f64, int side, const void* recv, hipStream_t st);
 hipError_t fim2dl_persist(const Fim2dArgs& a, int nl, bool f64, int grid, hipStream_t st);
 int fim2dl_persist_resident(int nl, bool f64, int cus);
 hipError_t layer_finite(const void* cost, bool f64, int64_t hw, int64_t L, int64_t z, int* d_flag, hipStream_t st);

@@ -141,7 +141,14 @@ struct eik_ctx {
     bool fresh_first = false;    // EIK_OPT_FRESH_FIRST: fresh tiles jump a backlogged FIFO
     int sched = 1;               // EIK_OPT_SCHED: in-place scheduling of persistent visits
     int live_pack = 0;           // EIK_OPT_LIVE_PACK: the halo agent packs only idle tiles' edges
-    double prio = 0.0;           // EIK_OPT_PRIO: band width of the priority bands in T (0: plain FIFO)
+    // EIK_OPT_PRIO: the priority bands' width in units of 64 x the cost's geometric mean (0: the
+    // plain FIFO; < 0, the default: 1 in fp64, 0 in fp32).  fp64 at 1: C2 2.44-2.50 -> 2.37 ms, C4 at
+    // one GPU 10.5 -> 13.8 Gcells/s; 0.5 / 2 lose on C4 (6.9 / 12.9; profiles/r05i_prio_ab.log).  fp32
+    // solves are twice as fast per pass and the one-dispatcher bands held them back: C2 fp32 1.6 ->
+    // 1.9 ms, C4 fp32 18.7 -> 10.8 Gcells/s (profiles/r05j_bench.json).  Batches of > 2 maps: FIFO.
+    double prio = -1.0;
+    int layer_planar = 0;        // EIK_OPT_LAYER_PLANAR: the layered solver works on layer-planar copies
+    DevBuf lp_cost, lp_T;        // those copies (solve_layered)
     int path_loop = 2;           // EIK_OPT_PATH_LOOP: 2D walker loop form (profiles/r02i_path_walker.log)
     int timing = 0;
     int grid = 0;
@@ -201,6 +208,9 @@ struct eik_fim2d {
     DevBuf hold;
     LiveBox* box = nullptr;              // pinned, coherent
     bool live_on = false;
+    // a layered volume's block (eik_fim3dl_create: the layered solver, fim2dl.hip): nl > 0
+    int lnl = 0, lz0 = 0;
+    int64_t lL = 1;
 };
 
 static int set_err(eik_ctx* c, int code, const char* fmt, ...) {
@@ -376,7 +386,8 @@ int eik_set_option(eik_ctx* c, int opt, double v) {
         case EIK_OPT_FRESH_FIRST: c->fresh_first = v != 0; break;
         case EIK_OPT_SCHED: c->sched = std::max(0, std::min(3, (int)v)); break;
         case EIK_OPT_LIVE_PACK: c->live_pack = v != 0; break;
-        case EIK_OPT_PRIO: c->prio = v > 0 ? v : 0.0; break;
+        case EIK_OPT_PRIO: c->prio = v; break;
+        case EIK_OPT_LAYER_PLANAR: c->layer_planar = v != 0; break;
         case EIK_OPT_PATH_LOOP: c->path_loop = std::max(0, std::min(2, (int)v)); break;
         case EIK_OPT_FRONTS_CAP: c->fronts_cap = v <= 0 ? 0.0 : v == 1 ? kFrontsMargin : std::max(1.0, v); break;
         default: return set_err(c, EIK_ERR_ARG, "unknown option %d", opt);
@@ -418,6 +429,7 @@ static int fim2d_create_rows(eik_ctx* c, int64_t B, int64_t H, int64_t W, int dt
     for (auto& g : a.ghost) g = nullptr;
     a.ls = 1;
     a.z0 = 0;
+    a.lzs = 1;
     // FIFO slots: a power of two with ample headroom over the tiles (each tile holds at most one
     // filled slot; the margin keeps a slow poller's slot from being lapped by the tail)
     uint64_t q = 4096;
@@ -480,7 +492,7 @@ void eik_fim2d_destroy(eik_fim2d* f) {
 }
 
 // the queue counters of the last persistent launch (EIK_QDEBUG builds; zeros otherwise)
-extern "C" int eik_fim2d_qcount(const eik_fim2d* f, uint64_t out[8]) {
+int eik_fim2d_qcount(const eik_fim2d* f, uint64_t out[8]) {
     if (!f || !out) return EIK_ERR_ARG;
     memcpy(out, (const char*)f->h_q + kVisitsOff + 24, 8 * sizeof(uint64_t));
     return EIK_OK;
@@ -542,7 +554,8 @@ int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
     // with the queue before the seed kernel pushes the goal's tile
     f->a.bctl = nullptr;
     // (one map or a few: a batch of independent maps keeps the FIFO -- their keys do not compare)
-    if (c->prio > 0 && f->a.mode == kModePersistent && f->B <= 2) {
+    const double prio = c->prio < 0 ? (f->f64 ? 1.0 : 0.0) : c->prio;
+    if (prio > 0 && f->a.mode == kModePersistent && f->B <= 2) {
         uint64_t bc = 1024;
         while (bc < 2 * (uint64_t)f->a.capacity) bc <<= 1;
         HIPCHK(c, f->bslot.ensure(sizeof(unsigned) * kBands * bc));
@@ -553,7 +566,7 @@ int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
         f->a.bmask = (unsigned)(bc - 1);
         f->a.bctl = (unsigned long long*)f->bctl.p;
         float* pd = (float*)((char*)f->bctl.p + 128 * kBands);
-        HIPCHK(c, fim2d_prio_delta(d_cost, f->f64, f->H * f->W, (float)c->prio, pd, f->stream));
+        HIPCHK(c, fim2d_prio_delta(d_cost, f->f64, f->H * f->W, (float)prio, pd, f->stream));
         f->a.pdelta = pd;
     }
     HIPCHK(c, fim2d_init(f->a, f->f64, (int)f->B, (const int64_t*)f->goals.p, (unsigned*)f->edge.p, f->stream));
@@ -595,10 +608,84 @@ static hipError_t rewind_if_needed(eik_fim2d* f) {
     return fim2d_qrewind(f->a, f->stream);
 }
 
+// ---- a layered volume's block in a domain decomposition (split in x-y, the
+// layers stay together): the layered solver (fim2dl.hip) with ghost strips of nl values per edge
+// cell, driven by the relaunch schedule (eikonal/dd.py solve: iterate to local convergence, pack,
+// exchange, merge)
+int eik_fim3dl_create(eik_ctx* c, int64_t H, int64_t W, int64_t L, int z0, int nl, int dtype, eik_fim2d** out) {
+    if (!c || !out) return EIK_ERR_ARG;
+    const int kmax = dtype == EIK_F64 ? 3 : 4;
+    if (nl < 1 || nl > kmax || z0 < 0 || z0 + nl > L)
+        return set_err(c, EIK_ERR_ARG, "layered block: nl=%d z0=%d L=%ld (nl <= %d)", nl, z0, (long)L, kmax);
+    const int rc = fim2d_create_rows(c, 1, H, W, dtype, fim2dl_rows(dtype == EIK_F64), out);
+    if (rc) return rc;
+    (*out)->lnl = nl;
+    (*out)->lz0 = z0;
+    (*out)->lL = L;
+    return EIK_OK;
+}
+
+int eik_fim3dl_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t goal[3], void* stream) {
+    if (!f || !f->lnl || !d_cost || !d_T || !goal) return EIK_ERR_ARG;
+    eik_ctx* c = f->ctx;
+    HIPCHK(c, hipSetDevice(c->device));
+    f->stream = (hipStream_t)stream;
+    Fim2dArgs& a = f->a;
+    a.cost = d_cost;
+    a.T = d_T;
+    a.ls = f->lL;
+    a.z0 = f->lz0;
+    a.lzs = 1;
+    a.mode = kModePersistent;
+    a.max_rounds = 1;
+    a.keep = (float)(1.0 - c->tol);
+    a.delta = __builtin_inff();
+    a.edge_dirty = nullptr;
+    a.bctl = nullptr;
+    a.qhold = nullptr;
+    a.live = nullptr;
+    a.qtimeout = (unsigned long long)(c->qtimeout_s * 1e8);
+    a.max_passes = c->passes > 0 ? c->passes : 24;  // the layered solver's (solve_layered)
+    a.qbudget = c->max_visits ? c->max_visits : 1024ull * (unsigned long long)a.tiles_per_map + (1ull << 20);
+    a.fresh_first = c->fresh_first;
+    f->iterations = 0;
+    f->host_syncs = 0;
+    f->sweep_ms = f->solve_ms = 0.0;
+    HIPCHK(c, hipMemsetAsync((void*)a.visits, 0, 3 * sizeof(unsigned long long), f->stream));
+    const bool in = goal[0] >= 0 && goal[1] >= 0 && goal[0] < f->W && goal[1] < f->H;
+    if (in && (goal[2] < f->lz0 || goal[2] >= f->lz0 + f->lnl))
+        return set_err(c, EIK_ERR_ARG, "goal layer %ld outside the solved layers", (long)goal[2]);
+    // (a block without the goal: no seed -- its first launch ends at once, its ghosts bring the front)
+    HIPCHK(c, fim2dl_init(a, f->f64, in ? goal[0] : -1, goal[1], goal[2] - f->lz0, f->H * f->W * f->lL, f->stream));
+    f->started = true;
+    f->need_rewind = false;
+    return EIK_OK;
+}
+
 int eik_fim2d_iterate(eik_fim2d* f, int64_t max_iters, int64_t* active) {
     if (!f || !f->started) return EIK_ERR_ARG;
     eik_ctx* c = f->ctx;
     HIPCHK(c, hipSetDevice(c->device));
+    if (f->lnl) {  // a layered block: one persistent launch to local convergence (fim2dl.hip)
+        if (max_iters < 1) {
+            if (active) *active = -1;
+            return EIK_OK;
+        }
+        int& res = c->resident_l[f->f64 ? 1 : 0][f->lnl];
+        if (res == 0) res = fim2dl_persist_resident(f->lnl, f->f64, c->cu_count);
+        const int g = std::min(c->grid > 0 ? c->grid : 4 * c->cu_count, res);
+        HIPCHK(c, hipEventRecord(f->ev_start, f->stream));
+        HIPCHK(c, fim2dl_persist(f->a, f->lnl, f->f64, g, f->stream));  // (+ the queue rewind)
+        HIPCHK(c, hipEventRecord(f->ev_stop, f->stream));
+        ++f->iterations;
+        HIPCHK(c, hipMemcpyAsync(f->h_q, f->qctl.p, kQueueCtlBytes, hipMemcpyDeviceToHost, f->stream));
+        HIPCHK(c, hipStreamSynchronize(f->stream));
+        ++f->host_syncs;
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, f->ev_start, f->ev_stop) == hipSuccess) f->solve_ms += ms;
+        memcpy(f->h_visits, (const char*)f->h_q + kVisitsOff, 3 * sizeof(unsigned long long));
+        return persist_result(f, active);
+    }
     int64_t done = 0;
     int h = 1;
     const int grid = c->grid > 0 ? c->grid : 4 * c->cu_count;
@@ -739,12 +826,19 @@ int eik_fim2d_solve(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
 
 int eik_fim2d_pack_edges(eik_fim2d* f, void* n, void* s, void* w, void* e) {
     if (!f || !f->started) return EIK_ERR_ARG;
-    HIPCHK(f->ctx, fim2d_pack_edges(f->a, f->f64, n, s, w, e, f->stream));
+    if (f->lnl)  // a layered block: nl values per edge cell
+        HIPCHK(f->ctx, fim2dl_pack_edges(f->a, f->lnl, f->f64, n, s, w, e, f->stream));
+    else
+        HIPCHK(f->ctx, fim2d_pack_edges(f->a, f->f64, n, s, w, e, f->stream));
     return EIK_OK;
 }
 
 int eik_fim2d_merge_ghost(eik_fim2d* f, int side, const void* recv) {
     if (!f || !f->started || side < 0 || side > 3 || !recv || !f->a.ghost[side]) return EIK_ERR_ARG;
+    if (f->lnl) {  // a layered block (its launches rewind their queue themselves)
+        HIPCHK(f->ctx, fim2dl_merge_ghost(f->a, f->lnl, f->f64, side, recv, f->stream));
+        return EIK_OK;
+    }
     f->a.iter = (unsigned)f->iterations;  // enqueue for the next sweep launch
     HIPCHK(f->ctx, rewind_if_needed(f));
     HIPCHK(f->ctx, fim2d_merge_ghost(f->a, f->f64, side, recv, side < 2 ? f->W : f->H, f->stream));
@@ -1311,6 +1405,20 @@ static int solve_layered(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, i
     a.T = d_T;
     a.ls = L;
     a.z0 = z0;
+    a.lzs = 1;
+    int64_t nT = H * W * L;  // T's elements (the init's +inf)
+    const bool planar = c->layer_planar != 0;
+    const size_t esz = f64 ? 8 : 4;
+    if (planar) {  // the solve on layer-planar copies (fim2dl.hip layer_planar_in_kernel)
+        HIPCHK(c, c->lp_cost.ensure(esz * nl * H * W));
+        HIPCHK(c, c->lp_T.ensure(esz * nl * H * W));
+        a.cost = c->lp_cost.p;
+        a.T = c->lp_T.p;
+        a.ls = 1;
+        a.z0 = 0;
+        a.lzs = H * W;
+        nT = (int64_t)nl * H * W;
+    }
     a.mode = kModePersistent;
     a.max_rounds = 1;
     a.keep = (float)(1.0 - c->tol);
@@ -1327,8 +1435,10 @@ static int solve_layered(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, i
     a.fresh_first = c->fresh_first;
     HIPCHK(c, hipEventRecord(f->ev_start, st));
     HIPCHK(c, hipMemsetAsync((void*)f->a.visits, 0, 3 * sizeof(unsigned long long), st));
-    HIPCHK(c, fim2dl_init(a, f64, goal[0], goal[1], goal[2], st));
+    if (planar) HIPCHK(c, layer_planar(d_cost, c->lp_cost.p, f64, H * W, L, z0, nl, true, st));
+    HIPCHK(c, fim2dl_init(a, f64, goal[0], goal[1], goal[2] - z0, nT, st));
     HIPCHK(c, fim2dl_persist(a, nl, f64, grid, st));
+    if (planar) HIPCHK(c, layer_planar(c->lp_T.p, d_T, f64, H * W, L, z0, nl, false, st));
     HIPCHK(c, hipEventRecord(f->ev_stop, st));
     HIPCHK(c, hipMemcpyAsync(f->h_q, f->qctl.p, kQueueCtlBytes, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipMemcpyAsync(f->h_visits, (void*)f->a.visits, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
@@ -1350,12 +1460,14 @@ static int solve_layered(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, i
     c->last.solve_ms = ms;
     // per visit: cost + T read and T write of the tile's nl layers plus the halo ring (a first
     // visit reads no T); per in-place pass: T write + halo
-    const double esz = f64 ? 8.0 : 4.0;
-    c->last.bytes_alg = esz * nl *
-                        ((double)c->last.tile_visits * (3.0 * kTile * th + 2.0 * (kTile + th)) -
-                         (double)c->last.fresh_visits * kTile * th +
-                         (double)c->last.inplace_passes * (1.0 * kTile * th + 2.0 * (kTile + th))) +
-                        esz * H * W * L;
+    // (esz: the element size above)
+    // (+ the init's T store; planar: + the copies, cost in (L read, nl written) and field out (nl
+    // read, L written) per cell, instead of the init's L)
+    c->last.bytes_alg = (double)esz * nl *
+                            ((double)c->last.tile_visits * (3.0 * kTile * th + 2.0 * (kTile + th)) -
+                             (double)c->last.fresh_visits * kTile * th +
+                             (double)c->last.inplace_passes * (1.0 * kTile * th + 2.0 * (kTile + th))) +
+                        (double)esz * H * W * (planar ? 2.0 * (L + nl) + nl : (double)L);
     return EIK_OK;
 }
 

@@ -928,7 +928,9 @@ __global__ __launch_bounds__(256) void prio_delta_kernel(const R* __restrict__ c
     double sum = 0.0;
     int cnt = 0;
     for (int i = threadIdx.x; i < 4096; i += 256) {
-        const double c = (double)cost[(int64_t)((double)i * (double)n / 4096.0)];
+        // scattered over rows AND columns (an even stride over a 2^k raster would sample one column)
+        const unsigned long long hsh = (unsigned long long)(i + 1) * 0x9E3779B97F4A7C15ull;
+        const double c = (double)cost[(int64_t)((hsh >> 11) % (unsigned long long)n)];
         if (c > 0.0 && c < Real<double>::inf()) {
             sum += log(c);
             ++cnt;

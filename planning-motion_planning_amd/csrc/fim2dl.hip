@@ -270,7 +270,9 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
     const int map = tile / a.tiles_per_map;
     const int rem = tile - map * a.tiles_per_map;
     const int ty = rem / a.ntx, tx = rem - (rem / a.ntx) * a.ntx;
-    const int64_t ls = a.ls, plane = a.H * a.W * ls;
+    // value (y, x, solved layer z) at (y * W + x) * ls + z0 + z * lzs: the [y][x][L] volume (ls = L,
+    // lzs = 1) or its layer-planar copy (ls = 1, z0 = 0, lzs = H * W; solve_layered)
+    const int64_t ls = a.ls, lzs = a.lzs, plane = a.H * a.W * (lzs > 1 ? NL : ls);
     const R* __restrict__ cost = static_cast<const R*>(a.cost) + map * plane;
     const TMem<R, COH> T(static_cast<R*>(a.T) + map * plane, plane);
     const int64_t y0 = (int64_t)ty * TH, x0 = (int64_t)tx * kTile;
@@ -288,12 +290,24 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
     const bool hcell = wave < 2 || lane < TH;
     const bool hin = hcell && hy >= 0 && hy < a.H && hx >= 0 && hx < a.W;
     const int64_t hgi = hin ? (hy * a.W + hx) * ls + a.z0 : 0;
+    // domain decomposition (relaunch schedule, eik_fim3dl_start: the ghosts change only between
+    // launches): the halo cell just outside the block comes from the side's ghost strip, nl values
+    // per edge cell ([i][z], as fim2dl_pack_edges_kernel writes them)
+    const R* hg = nullptr;
+    int64_t hgo = 0;
+    if (hcell && !hin) {
+        const R* const* G = reinterpret_cast<const R* const*>(a.ghost);
+        if (wave == 0 && hy == -1 && hx < a.W)         { hg = G[0]; hgo = hx * NL; }
+        else if (wave == 1 && hy == a.H && hx < a.W)   { hg = G[1]; hgo = hx * NL; }
+        else if (wave == 2 && hx == -1 && hy < a.H)    { hg = G[2]; hgo = hy * NL; }
+        else if (wave == 3 && hx == a.W && hy < a.H)   { hg = G[3]; hgo = hy * NL; }
+    }
     auto load_halo = [&]() {  // unconditional loads (an in-range index), then the +inf select
         R v[4] = {INF, INF, INF, INF};
 #pragma unroll
-        for (int z = 0; z < NL; ++z) v[z] = T.ld(hgi + z);
+        for (int z = 0; z < NL; ++z) v[z] = T.ld(hgi + z * lzs);
 #pragma unroll
-        for (int z = 0; z < NL; ++z) v[z] = hin ? v[z] : INF;
+        for (int z = 0; z < NL; ++z) v[z] = hin ? v[z] : (hg ? hg[hgo + z] : INF);
         return LCell<R>::make(v);
     };
     // ---- stage: every global load of the visit (T, cost, halo) is issued before the first LDS
@@ -328,7 +342,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
 #pragma unroll
             for (int z = 0; z < NL; ++z) {
                 told[j][z] = INF;
-                cc[j][z] = scost(cost[gi + z]);
+                cc[j][z] = scost(cost[gi + z * lzs]);
             }
         }
         store_tile(cc, load_halo());
@@ -340,8 +354,8 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
             const int64_t gi = ((y0 + wave + 4 * j) * a.W + x0 + lane) * ls + a.z0;
 #pragma unroll
             for (int z = 0; z < NL; ++z) {
-                told[j][z] = T.ld(gi + z);
-                cc[j][z] = scost(cost[gi + z]);
+                told[j][z] = T.ld(gi + z * lzs);
+                cc[j][z] = scost(cost[gi + z * lzs]);
             }
         }
         store_tile(cc, load_halo());
@@ -352,10 +366,15 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
             const int64_t gy = y0 + wave + 4 * j, gx = x0 + lane;
             const bool in = gy < a.H && gx < a.W;
             const int64_t gi = in ? (gy * a.W + gx) * ls + a.z0 : 0;
+            // a block's south / east ghost cells inside a tile cut by the block's end: the ghost's
+            // value with an infinite cost (a halo cell, never updated)
+            const R* const* G = reinterpret_cast<const R* const*>(a.ghost);
+            const R* gc = (gy == a.H && gx < a.W) ? G[1] : (gx == a.W && gy < a.H) ? G[3] : nullptr;
+            const int64_t go = (gy == a.H ? gx : gy) * NL;
 #pragma unroll
             for (int z = 0; z < NL; ++z) {
-                const R t = T.ld(gi + z), c = cost[gi + z];
-                told[j][z] = in ? t : INF;
+                const R t = T.ld(gi + z * lzs), c = cost[gi + z * lzs];
+                told[j][z] = in ? t : (gc ? gc[go + z] : INF);
                 cc[j][z] = in ? scost(c) : INF;
             }
         }
@@ -398,7 +417,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
 #pragma unroll
             for (int z = 0; z < NL; ++z) {
                 const R nv = nv4.get(z);
-                if (in && nv < told[j][z]) T.st(gi + z, nv);
+                if (in && nv < told[j][z]) T.st(gi + z * lzs, nv);
                 if (nv < told[j][z] * R(keep)) {
                     fl |= 128u;
                     // a neighbour can improve only if this edge value undercuts its adjacent cell
@@ -488,7 +507,7 @@ __global__ void fim2dl_init_kernel(R* __restrict__ T, int64_t n, unsigned* __res
 // T[goal] = 0 (gz: absolute layer index) and the goal's tile (th rows) queued
 template <typename R>
 __global__ void fim2dl_seed_kernel(Fim2dArgs a, int64_t gx, int64_t gy, int64_t gz, int th) {
-    static_cast<R*>(a.T)[(gy * a.W + gx) * a.ls + gz] = R(0);
+    static_cast<R*>(a.T)[(gy * a.W + gx) * a.ls + a.z0 + gz * a.lzs] = R(0);  // gz: the solved layer's index
     __threadfence();
     qpush(a, (int)(gy / th) * a.ntx + (int)(gx / kTile), kSelf | kVisited);  // T not all +inf
 }
@@ -505,23 +524,136 @@ __global__ void layer_finite_kernel(const R* __restrict__ cost, int64_t hw, int6
     if (__any(any) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
 }
 
+// Layer-planar working copies (EIK_LAYER_PLANAR, solve_layered): the planner's volumes are
+// [y][x][L] with z fastest and +inf padding layers, so a tile row's stores of its nl solved layers
+// touch every line of the cells' L values (the fp32 C5 kernel wrote 1.69x its algorithmic bytes,
+// profiles/pmc_traffic_c5.json).  The solve runs on copies [nl][H][W] instead (every tile-row load
+// and store one contiguous run per layer), the cost copied in and the field copied out once.
+template <typename R>
+__global__ void layer_planar_in_kernel(const R* __restrict__ vol, int64_t hw, int64_t L, int z0, int nl,
+                                       R* __restrict__ out) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < hw; c += stride)
+        for (int z = 0; z < nl; ++z) out[z * hw + c] = vol[c * L + z0 + z];
+}
+// the whole cell: the solved layers from the copy, +inf elsewhere (the padding's field) -- the
+// volume's lines are written whole
+template <typename R>
+__global__ void layer_planar_out_kernel(const R* __restrict__ pl, int64_t hw, int64_t L, int z0, int nl,
+                                        R* __restrict__ vol) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < hw * L; i += stride) {
+        const int64_t c = i / L;
+        const int z = (int)(i - c * L) - z0;
+        vol[i] = (z >= 0 && z < nl) ? pl[z * hw + c] : Real<R>::inf();
+    }
+}
+hipError_t layer_planar(const void* src, void* dst, bool f64, int64_t hw, int64_t L, int z0, int nl, bool in,
+                        hipStream_t st) {
+    const int grid = (int)std::min<int64_t>(8192, (hw * (in ? 1 : L) + 255) / 256);
+    if (f64) {
+        if (in)
+            hipLaunchKernelGGL(layer_planar_in_kernel<double>, dim3(grid), dim3(256), 0, st,
+                               static_cast<const double*>(src), hw, L, z0, nl, static_cast<double*>(dst));
+        else
+            hipLaunchKernelGGL(layer_planar_out_kernel<double>, dim3(grid), dim3(256), 0, st,
+                               static_cast<const double*>(src), hw, L, z0, nl, static_cast<double*>(dst));
+    } else {
+        if (in)
+            hipLaunchKernelGGL(layer_planar_in_kernel<float>, dim3(grid), dim3(256), 0, st,
+                               static_cast<const float*>(src), hw, L, z0, nl, static_cast<float*>(dst));
+        else
+            hipLaunchKernelGGL(layer_planar_out_kernel<float>, dim3(grid), dim3(256), 0, st,
+                               static_cast<const float*>(src), hw, L, z0, nl, static_cast<float*>(dst));
+    }
+    return hipGetLastError();
+}
+
+// Domain decomposition of a layered volume ("C5: split x-y only, layers stay
+// together"): a rank's edge rows / columns, nl values per edge cell ([i][z]), into send strips ...
+template <typename R>
+__global__ void fim2dl_pack_edges_kernel(Fim2dArgs a, int nl, R* __restrict__ n, R* __restrict__ s,
+                                         R* __restrict__ w, R* __restrict__ e) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const R* T = static_cast<const R*>(a.T);
+    auto at = [&](int64_t y, int64_t x, int z) { return T[(y * a.W + x) * a.ls + a.z0 + z * a.lzs]; };
+    for (int z = 0; z < nl; ++z) {
+        if (i < a.W) {
+            if (n) n[i * nl + z] = at(0, i, z);
+            if (s) s[i * nl + z] = at(a.H - 1, i, z);
+        }
+        if (i < a.H) {
+            if (w) w[i * nl + z] = at(i, 0, z);
+            if (e) e[i * nl + z] = at(i, a.W - 1, z);
+        }
+    }
+}
+// ... and the received strips min-merged into the ghosts; an edge cell whose ghost dropped in any
+// layer queues its tile (th: tile rows) for the next launch
+template <typename R>
+__global__ void fim2dl_merge_ghost_kernel(Fim2dArgs a, int nl, int th, int side, const R* __restrict__ recv,
+                                          int64_t len) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= len) return;
+    R* g = static_cast<R*>(const_cast<void*>(a.ghost[side]));
+    bool dropped = false;
+    for (int z = 0; z < nl; ++z) {
+        const R v = recv[i * nl + z];
+        if (v < g[i * nl + z]) {
+            g[i * nl + z] = v;
+            dropped = true;
+        }
+    }
+    if (!dropped) return;
+    const int ty = side < 2 ? (side == 0 ? 0 : a.nty - 1) : (int)(i / th);
+    const int tx = side < 2 ? (int)(i / kTile) : (side == 2 ? 0 : a.ntx - 1);
+    qpush(a, ty * a.ntx + tx, kFromN << side);
+}
+
+hipError_t fim2dl_pack_edges(const Fim2dArgs& a, int nl, bool f64, void* n, void* s, void* w, void* e, hipStream_t st) {
+    const int64_t len = a.H > a.W ? a.H : a.W;
+    const int grid = (int)((len + 255) / 256);
+    if (f64)
+        hipLaunchKernelGGL(fim2dl_pack_edges_kernel<double>, dim3(grid), dim3(256), 0, st, a, nl, (double*)n,
+                           (double*)s, (double*)w, (double*)e);
+    else
+        hipLaunchKernelGGL(fim2dl_pack_edges_kernel<float>, dim3(grid), dim3(256), 0, st, a, nl, (float*)n, (float*)s,
+                           (float*)w, (float*)e);
+    return hipGetLastError();
+}
+
+hipError_t fim2dl_merge_ghost(const Fim2dArgs& a, int nl, bool f64, int side, const void* recv, hipStream_t st) {
+    const int64_t len = side < 2 ? a.W : a.H;
+    const int grid = (int)((len + 255) / 256);
+    if (f64)
+        hipLaunchKernelGGL(fim2dl_merge_ghost_kernel<double>, dim3(grid), dim3(256), 0, st, a, nl, kRowsOf<double>,
+                           side, static_cast<const double*>(recv), len);
+    else
+        hipLaunchKernelGGL(fim2dl_merge_ghost_kernel<float>, dim3(grid), dim3(256), 0, st, a, nl, kRowsOf<float>, side,
+                           static_cast<const float*>(recv), len);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------------- host launchers
 int fim2dl_rows(bool f64) { return f64 ? kRowsOf<double> : kRowsOf<float>; }
 
-hipError_t fim2dl_init(const Fim2dArgs& a, bool f64, int64_t gx, int64_t gy, int64_t gz, hipStream_t st) {
-    const int64_t n = a.H * a.W * a.ls;
+// gz: the goal's layer among the solved ones (0 .. nl-1); n: T's elements to set to +inf
+hipError_t fim2dl_init(const Fim2dArgs& a, bool f64, int64_t gx, int64_t gy, int64_t gz, int64_t n, hipStream_t st) {
     const int64_t nslots = (int64_t)a.qmask + 1;
     const int grid = (int)std::min<int64_t>(4096, (std::max(n, nslots) + 255) / 256);
     hipError_t e = hipMemsetAsync(a.qhead, 0, kQueueCtlBytes, st);  // head tail active error
     if (e != hipSuccess) return e;
+    // (gx < 0: no goal in this block -- a domain-decomposed volume's other ranks)
     if (f64) {
         hipLaunchKernelGGL(fim2dl_init_kernel<double>, dim3(grid), dim3(256), 0, st, static_cast<double*>(a.T), n,
                            a.qstate, (int64_t)a.tiles_per_map, a.qslot, nslots);
-        hipLaunchKernelGGL(fim2dl_seed_kernel<double>, dim3(1), dim3(1), 0, st, a, gx, gy, gz, kRowsOf<double>);
+        if (gx >= 0)
+            hipLaunchKernelGGL(fim2dl_seed_kernel<double>, dim3(1), dim3(1), 0, st, a, gx, gy, gz, kRowsOf<double>);
     } else {
         hipLaunchKernelGGL(fim2dl_init_kernel<float>, dim3(grid), dim3(256), 0, st, static_cast<float*>(a.T), n,
                            a.qstate, (int64_t)a.tiles_per_map, a.qslot, nslots);
-        hipLaunchKernelGGL(fim2dl_seed_kernel<float>, dim3(1), dim3(1), 0, st, a, gx, gy, gz, kRowsOf<float>);
+        if (gx >= 0)
+            hipLaunchKernelGGL(fim2dl_seed_kernel<float>, dim3(1), dim3(1), 0, st, a, gx, gy, gz, kRowsOf<float>);
     }
     return hipGetLastError();
 }

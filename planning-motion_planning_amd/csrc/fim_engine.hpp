@@ -266,9 +266,8 @@ __device__ __forceinline__ void qslot_put_front(const Fim2dArgs& a, int tile) {
 //    FIFO, 170 vs 108 rounds); whichever entry is taken first claims the tile, the others are stale
 //    and are dropped when taken (the claim is a CAS pending -> busy on the state word);
 //  * every workgroup looking for work takes a FIFO ticket; the oldest waiter (its ticket is the next
-//    slot to be filled) moves up to 32 band entries to the FIFO's tail in band order -- three
-//    quarters from the lowest bands, a quarter from the highest (band_dispatch) -- so the band heads
-//    see one claimant at a time.
+//    slot to be filled) moves up to 32 band entries to the FIFO's tail, lowest bands first
+//    (band_dispatch), so the band heads see one claimant at a time.
 // a.key[tile] holds the smallest key since the tile's last claim (atomicMin at each activation).
 __device__ __forceinline__ unsigned band_of(const Fim2dArgs& a, float k) {
     const float q = k / *a.pdelta;  // k >= 0 (or +inf); a kernel-constant word (scalar cache)
@@ -519,20 +518,12 @@ __device__ __forceinline__ bool band_dispatch(const Fim2dArgs& a) {
         t = __hip_atomic_load(&a.bctl[16 * lane + 8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     const unsigned avail = t > h ? (unsigned)(t - h < kDispatch ? t - h : kDispatch) : 0u;
-    const unsigned long long ne = __ballot(avail != 0u);
-    if (!ne) return false;
-    // lowest bands first, but a quarter of the batch goes to the highest non-empty band: the front's
-    // first visits carry the largest keys, and refinements behind it (low keys, re-queued at key 0
-    // when a visit ends still changing) must not starve it -- narrow bands did (C4 2.7 Gcells/s at
-    // a band width of 60 against 10.9 for the FIFO)
-    const int hi = 63 - __builtin_clzll(ne);
-    const unsigned lo_budget = kDispatch - kDispatch / 4;
+    if (!__ballot(avail != 0u)) return false;
+    // lowest bands first.  (Reserving a quarter of the batch for the highest band -- the front's
+    // first visits -- was measured and removed: C4 at one GPU 14 -> 2.6-6 Gcells/s, C2 no gain,
+    // profiles/r05h_prio_planar_ab.log.)
     const unsigned before = wave_incl_sum(avail) - avail;  // entries of the lower bands
-    unsigned take = before >= lo_budget ? 0u : (avail < lo_budget - before ? avail : lo_budget - before);
-    if (lane == hi) {
-        const unsigned more = avail - take < kDispatch / 4 ? avail - take : kDispatch / 4;
-        take += more;
-    }
+    const unsigned take = before >= kDispatch ? 0u : (avail < kDispatch - before ? avail : kDispatch - before);
     const unsigned got = take && atomicCAS(&a.bctl[16 * lane], h, h + take) == h ? take : 0u;
     const unsigned end = wave_incl_sum(got), start = end - got;
     const unsigned total = __shfl(end, 63);

@@ -14,7 +14,7 @@ EIK_F32, EIK_F64 = 0, 1
 PATH_DONE, PATH_FALLBACK, PATH_ERROR = 0, 1, 2
 OPT_MAX_ROUNDS, OPT_SYNC_EVERY, OPT_TIMING, OPT_GRID, OPT_TOL, OPT_DELTA = 0, 1, 2, 3, 4, 5
 OPT_MODE, OPT_QTIMEOUT, OPT_MAX_VISITS, OPT_PASSES, OPT_FRESH_FIRST, OPT_SCHED, OPT_PATH_LOOP = 6, 7, 8, 9, 10, 11, 12
-OPT_FRONTS_CAP, OPT_LIVE_PACK, OPT_PRIO = 13, 14, 15
+OPT_FRONTS_CAP, OPT_LIVE_PACK, OPT_PRIO, OPT_LAYER_PLANAR = 13, 14, 15, 16
 MODE_LIST, MODE_PERSISTENT = 0, 1
 
 i64 = C.c_int64
@@ -185,6 +185,9 @@ def lib():
         L.eik_arm_path_f64.argtypes = [vp, _f64p, _f64p, i64, i64, _f64p, _f64p, i64, P(ArmVolume), C.c_double, _f64p,
                                        i64, P(i64), P(C.c_int), vp, vp]
         L.eik_tmap3d_batch_f64.argtypes = [vp, _f64p, i64, i64, i64, i64, _i64p, _f64p]
+        L.eik_fim3dl_create.argtypes = [vp, i64, i64, i64, C.c_int, C.c_int, C.c_int, P(vp)]
+        L.eik_fim3dl_start.argtypes = [vp, vp, vp, _i64p, vp]
+        L.eik_fim2d_qcount.argtypes = [vp, P(C.c_uint64)]
         _lib = L
         return L
 
@@ -201,7 +204,8 @@ EXPORTED = [
     "eik_fim2d_live_merge", "eik_fim2d_release", "eik_node_allreduce", "eik_node_shm_open",
     "eik_node_shm_close", "eik_node_shm_unlink", "eik_ipc_alloc", "eik_ipc_free", "eik_ipc_open", "eik_ipc_close",
     "eik_rover_assemble", "eik_rover_path_f64", "eik_arm_obst_map_f64", "eik_arm_tunnel_cost_f64",
-    "eik_arm_path_f64", "eik_tmap3d_batch_f64", "eik_host_alloc", "eik_host_free",
+    "eik_arm_path_f64", "eik_tmap3d_batch_f64", "eik_host_alloc", "eik_host_free", "eik_fim2d_qcount",
+    "eik_fim3dl_create", "eik_fim3dl_start",
 ]
 
 
@@ -569,6 +573,24 @@ class Fim2d:
         a = i64(0)
         self.ctx._chk(lib().eik_fim2d_release(self._h, C.byref(a)))
         return a.value
+
+
+class Fim3dLayered(Fim2d):
+    """A block of a domain-decomposed few-layer 3D volume (eik_fim3dl_create: the layered solver on a
+    [H][W][L] block, layers z0 .. z0+nl-1; ghost strips of nl values per edge cell).  The eik_fim2d
+    methods apply; start takes the goal as (x, y, z) with z absolute (x < 0: not in this block)."""
+
+    def __init__(self, ctx, H, W, L, z0, nl, dtype=EIK_F32):
+        self.ctx = ctx
+        h = vp()
+        ctx._chk(lib().eik_fim3dl_create(ctx._h, int(H), int(W), int(L), int(z0), int(nl), int(dtype), C.byref(h)))
+        self._h = h
+        self.B, self.H, self.W, self.dtype = 1, H, W, dtype
+        self.L, self.z0, self.nl = L, z0, nl
+
+    def start(self, d_cost, d_T, goal, stream=None):
+        g = np.asarray(goal, np.int64).reshape(3)
+        self.ctx._chk(lib().eik_fim3dl_start(self._h, d_cost, d_T, g, stream))
 
 
 # ----------------------------------------------------------------- pinned result arrays

@@ -10,7 +10,9 @@ out-of-block neighbours are GHOST strips, and every `exchange_every` outer itera
   4. all-reduces the number of active tiles; the solve ends when it is zero everywhere.
 Updates are monotone min-merges, so stale ghosts only delay convergence, never change the
 fixed point.  The local solver is duck-typed (eikonal.Fim2d on the GPU; a numpy solver in the
-CPU tests) with start / iterate / pack_edges / merge_ghost / active.
+CPU tests) with start / iterate / pack_edges / merge_ghost / active.  A few-layer 3D volume splits
+the same way in x-y, its layers kept together (eikonal.Fim3dLayered / GpuLocalLayered: strips of
+nl values per edge cell).
 
 solve_live is the GPU-native schedule (the default of bench.py at N > 1): ONE persistent launch
 per rank stays up for the whole solve, serving its tile FIFO, while the host runs halo rounds
@@ -59,12 +61,13 @@ class Block:
         return self.w if side in (N_, S_) else self.h
 
 
-def make_strips(block, dtype, device, fill):
-    """send/recv strips and ghosts for the sides that have a neighbour (None elsewhere)."""
+def make_strips(block, dtype, device, fill, per_cell=1):
+    """send/recv strips and ghosts for the sides that have a neighbour (None elsewhere).
+    per_cell: values per edge cell (a layered volume's block: its nl solved layers, [i][z])."""
     send, recv, ghost = [None] * 4, [None] * 4, [None] * 4
     for s in range(4):
         if block.nb[s] is not None:
-            n = block.strip_len(s)
+            n = block.strip_len(s) * per_cell
             send[s] = torch.full((n,), fill, dtype=dtype, device=device)
             recv[s] = torch.full((n,), fill, dtype=dtype, device=device)
             ghost[s] = torch.full((n,), fill, dtype=dtype, device=device)
@@ -132,6 +135,19 @@ class GpuLocal:
     def active(self):
         self.last_active = self.fim.active()
         return self.last_active
+
+
+class GpuLocalLayered(GpuLocal):
+    """dd.solve adapter over eikonal.Fim3dLayered: a block of a few-layer 3D volume (SURVEY §8(e),
+    C5: split in x-y, the layers stay together); ghosts of nl values per edge cell.  goal: the
+    block-local (x, y, z) or x < 0."""
+
+    def start(self, cost, T, goal, stream):
+        for g in self.ghosts:
+            if g is not None:
+                g.fill_(float("inf"))
+        self.fim.start(cost.data_ptr(), T.data_ptr(), goal, stream)
+        self.last_active = 1
 
 
 # ------------------------------------------------------------------------- live schedule

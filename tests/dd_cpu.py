@@ -101,3 +101,66 @@ class CpuLocal:
 
     def active(self):
         return int(self.dirty)
+
+
+def godunov3(a, b, c, C):
+    """FastMarching3D's n-D local solve (:59-75) on the axis minima a, b, c (the 3D Godunov update:
+    three axes when C^2 exceeds the spread to the largest, else two, else one)."""
+    s = np.sort(np.stack([a, b, c]), axis=0)
+    s0, s1, s2 = s[0], s[1], s[2]
+    with np.errstate(invalid="ignore", over="ignore"):
+        t1 = s0 + C
+        d = s1 - s0
+        t2 = 0.5 * (s0 + s1 + np.sqrt(np.maximum(2 * C * C - d * d, 0.0)))
+        q3 = 3 * C * C - 2 * ((s1 - s0) ** 2 + (s2 - s0) ** 2 - (s1 - s0) * (s2 - s0))
+        t3 = (s0 + s1 + s2 + np.sqrt(np.maximum(q3, 0.0))) / 3.0
+        three = C * C > (s2 - s0) ** 2 + (s2 - s1) ** 2
+        two = C > d
+    return np.where(three, t3, np.where(two, t2, t1))
+
+
+class CpuLocalLayered(CpuLocal):
+    """The layered protocol of eikonal/dd.py on CPU: a block [h][w][nl] of a few-layer volume, ghost
+    strips of nl values per edge cell ([i][z] flattened), Jacobi sweeps of the n-D update with the
+    layer neighbours inside the cell (FastMarching3D.py:21-57's six neighbours)."""
+
+    def __init__(self, cost, ghosts):
+        super().__init__(cost, ghosts)
+        self.nl = self.cost.shape[2]
+
+    def start(self, goal):
+        self.T = np.full(self.cost.shape, np.inf)
+        for g in self.ghosts:
+            if g is not None:
+                g.fill_(float("inf"))
+        if goal[0] >= 0:
+            self.T[goal[1], goal[0], goal[2]] = 0.0
+        self.dirty = True
+
+    def _padded(self):
+        h, w, nl = self.T.shape
+        P = np.full((h + 2, w + 2, nl), np.inf)
+        P[1:-1, 1:-1] = self.T
+        for side, sl in ((0, (0, slice(1, -1))), (1, (-1, slice(1, -1))), (2, (slice(1, -1), 0)),
+                         (3, (slice(1, -1), -1))):
+            if self.ghosts[side] is not None:
+                P[sl] = self.ghosts[side].numpy().reshape(-1, nl)
+        return P
+
+    def _sweep(self):
+        P = self._padded()
+        a = np.minimum(P[1:-1, :-2], P[1:-1, 2:])
+        b = np.minimum(P[:-2, 1:-1], P[2:, 1:-1])
+        Z = np.full((self.T.shape[0], self.T.shape[1], self.nl + 2), np.inf)
+        Z[:, :, 1:-1] = self.T
+        c = np.minimum(Z[:, :, :-2], Z[:, :, 2:])
+        nv = np.minimum(self.T, godunov3(a, b, c, self.cost))
+        if np.array_equal(nv, self.T):
+            return False
+        self.T = nv
+        return True
+
+    def pack_edges(self, n, s, w, e):
+        for t, v in ((n, self.T[0]), (s, self.T[-1]), (w, self.T[:, 0]), (e, self.T[:, -1])):
+            if t is not None:
+                t.copy_(torch.from_numpy(np.ascontiguousarray(v).reshape(-1)))

@@ -189,3 +189,90 @@ def test_nan_cost_blocks_fp64_device(mode):
     fin = np.isfinite(R)
     assert np.array_equal(np.isfinite(Tg), fin)
     assert np.abs(Tg[fin] - R[fin]).max() <= 1e-9
+
+
+def solve_blocks_layered(cost, goal, px, py, f64, z0, nl):
+    """The in-process rounds schedule (as solve_blocks) over blocks of a [H][W][L] volume, each an
+    eikonal.Fim3dLayered (the layered solver with ghost strips of nl values per edge cell)."""
+    import eikonal
+    from eikonal import _lib as L
+    from eikonal import dd
+
+    dev = torch.device("cuda", 0)
+    H, W, Lz = cost.shape
+    R = px * py
+    ctx = eikonal.Context(0)
+    dt = torch.float64 if f64 else torch.float32
+    blocks = [dd.Block(H, W, px, py, r) for r in range(R)]
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    locs, sends, recvs, Ts = [], [], [], []
+    for b in blocks:
+        c = torch.from_numpy(np.ascontiguousarray(cost[b.y0:b.y1, b.x0:b.x1])).to(dev, dt)
+        send, recv, ghost = dd.make_strips(b, dt, dev, float("inf"), per_cell=nl)
+        fim = eikonal.Fim3dLayered(ctx, b.h, b.w, Lz, z0, nl, L.EIK_F64 if f64 else L.EIK_F32)
+        loc = dd.GpuLocalLayered(fim, ghost)
+        T = torch.empty_like(c)
+        lg = b.local_goal(goal[0], goal[1])
+        loc.start(c, T, (lg[0], lg[1], goal[2]), stream)
+        locs.append((loc, c)), sends.append(send), recvs.append(recv), Ts.append(T)
+    for rounds in range(1, 100000):
+        for (loc, _), send in zip(locs, sends):
+            loc.iterate(1)
+            loc.pack_edges(*send)
+        for r, b in enumerate(blocks):
+            for s in range(4):
+                if b.nb[s] is not None:
+                    recvs[r][s].copy_(sends[b.nb[s]][OPP[s]])
+        for r, b in enumerate(blocks):
+            for s in range(4):
+                if b.nb[s] is not None:
+                    locs[r][0].merge_ghost(s, recvs[r][s])
+        if sum(loc.active() for loc, _ in locs) == 0:
+            break
+    torch.cuda.synchronize()
+    out = np.empty((H, W, Lz), np.float64)
+    for b, T in zip(blocks, Ts):
+        out[b.y0:b.y1, b.x0:b.x1] = T.cpu().double().numpy()
+    ctx.close()
+    return out, rounds
+
+
+def _volume(H, W, seed, pad):
+    rng = np.random.default_rng(seed)
+    c = rng.uniform(1, 5, (H, W, 3))
+    c[rng.random((H, W, 3)) < 0.08] = np.inf
+    c[:, : W // 2, 0] *= 0.3
+    c[:, W // 2:, 2] *= 0.3
+    if pad:  # the planner's z padding (Coupled_motion_planner.py:355-356)
+        inf = np.full((H, W, 1), np.inf)
+        c = np.concatenate([inf, c, inf], axis=2)
+    return c
+
+
+@pytest.mark.parametrize("shape,px,py,pad", [((1024, 1024), 2, 1, True), ((1024, 1024), 2, 2, True),
+                                             ((390, 455), 4, 2, False), ((300, 333), 1, 2, True)])
+@pytest.mark.parametrize("f64", [True, False])
+def test_dd_layered_blocks_match_single_domain(shape, px, py, pad, f64):
+    """SURVEY §8(e), C5 across GPUs: a few-layer volume split in x-y, layers together (strips of nl
+    values per edge cell, eik_fim3dl_create / eik_fim2d_pack_edges / eik_fim2d_merge_ghost), blocks
+    not multiples of the tile (40-row fp64 / 64-row fp32 tiles cut by the block ends, where the
+    south / east ghosts sit inside a tile).  The assembled field equals the single-domain layered
+    solve of the same volume: masks equal, fp64 <= 1e-11 / fp32 <= 1e-5 relative."""
+    import eikonal
+
+    H, W = shape
+    cost = _volume(H, W, px * 10 + py, pad)
+    z0 = 1 if pad else 0
+    goal = (W // 3, H // 2, z0 + 1)
+    cost[goal[1], goal[0], goal[2]] = 1.0
+    ctx = eikonal.Context(0)
+    try:
+        ref = ctx.tmap3d(cost, np.array(goal), dtype=np.float64 if f64 else np.float32).astype(np.float64)
+    finally:
+        ctx.close()
+    T, rounds = solve_blocks_layered(cost, goal, px, py, f64, z0, 3)
+    assert rounds >= 2
+    fin = np.isfinite(ref)
+    assert np.array_equal(np.isfinite(T), fin)
+    rel = np.abs(T[fin] - ref[fin]) / np.maximum(ref[fin], 1e-30)
+    assert rel.max() <= (1e-11 if f64 else 1e-5), rel.max()

@@ -125,6 +125,35 @@ def test_layered_vs_oracle(ctx, shape, seed, pad, switch):
             assert np.all(np.isinf(T[:, :, 0])) and np.all(np.isinf(T[:, :, -1]))
 
 
+@pytest.fixture(scope="module")
+def ctx_planar():
+    """The layered solver on layer-planar copies of the solved layers (EIK_OPT_LAYER_PLANAR)."""
+    import eikonal
+
+    c = eikonal.Context(0, options={"LAYER_PLANAR": 1})
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("shape,seed,pad,switch", [((130, 150, 2), 11, False, True), ((90, 140, 3), 14, True, True),
+                                                     ((300, 257, 3), 15, False, True), ((70, 65, 1), 16, False, False),
+                                                     ((5, 3, 2), 42, False, False), ((39, 65, 3), 43, True, False)])
+def test_layered_planar_vs_oracle(ctx_planar, shape, seed, pad, switch):
+    """EIK_OPT_LAYER_PLANAR: the same solve on [nl][H][W] copies (cost copied in, field copied out with
+    +inf in the padding layers) -- fields against the oracle in both dtypes, the padding +inf."""
+    c, goal = _layered_case(shape, seed, pad, switch)
+    O.set_strict(False)
+    try:
+        R = O.fmm3d(c, goal, None)
+    finally:
+        O.set_strict(True)
+    for f64 in (False, True):
+        T = ctx_planar.tmap3d(c, goal, dtype=np.float64 if f64 else np.float32)
+        check(T, R, f64)
+        if pad:
+            assert np.all(np.isinf(T[:, :, 0])) and np.all(np.isinf(T[:, :, -1]))
+
+
 @pytest.mark.parametrize("shape,seed", [((1, 1, 1), 41), ((5, 3, 2), 42), ((39, 65, 3), 43), ((41, 64, 1), 44),
                                         ((80, 129, 2), 45)])
 def test_layered_edge_shapes(ctx, shape, seed):

@@ -264,6 +264,44 @@ def local_solve3(torch, T, c):
 
 
 @pytest.mark.parametrize("f64", [False, True])
+def test_c5_planar_matches_volume_layout(env, f64):
+    """configs[4] with EIK_OPT_LAYER_PLANAR (the layered solver on [nl][H][W] copies): the field equals
+    the volume-layout solve's (masks equal; fp32 <= 1e-5, fp64 <= 1e-11 relative -- a different
+    tile order rounds differently), the padding layers +inf."""
+    torch, eikonal, L, terrain, dev, ctx = env
+    N = 4096
+    c0 = terrain.cost_block(0, 0, N, N, N, N, seed=42, device=dev).contiguous()
+    if f64:
+        c0 = c0.double()
+    inf = torch.full_like(c0, float("inf"))
+    c1 = torch.where(c0 > 100, inf, 1.6 * c0)
+    yy = torch.arange(N, device=dev)[:, None] // 64
+    xx = torch.arange(N, device=dev)[None, :] // 64
+    c2 = torch.where(((yy + 2 * xx) % 5) == 0, inf, 0.8 * c0)
+    cost = torch.stack([inf, c0, c1, c2, inf], dim=-1).contiguous()
+    del c1, c2, inf
+    goal = np.array((N // 2, N // 2, 1), np.int64)
+    stream = torch.cuda.current_stream(dev)
+    out = []
+    for planar in (0, 1):
+        c = eikonal.Context(0, options={"LAYER_PLANAR": planar})
+        try:
+            T = torch.full_like(cost, 7.0)  # the planar solve writes every value (padding +inf)
+            c._chk(L.lib().eik_fim3d_solve(c._h, cost.data_ptr(), T.data_ptr(), N, N, 5,
+                                           L.EIK_F64 if f64 else L.EIK_F32, goal, stream.cuda_stream))
+            torch.cuda.synchronize()
+            out.append(T)
+        finally:
+            c.close()
+    T0, T1 = out
+    assert bool(torch.isinf(T1[:, :, 0]).all()) and bool(torch.isinf(T1[:, :, 4]).all())
+    fin = torch.isfinite(T0)
+    assert torch.equal(fin, torch.isfinite(T1))
+    rel = ((T1[fin].double() - T0[fin].double()).abs() / T0[fin].double().clamp(min=1e-30)).max().item()
+    assert rel <= (1e-11 if f64 else 1e-5), rel
+
+
+@pytest.mark.parametrize("f64", [False, True])
 def test_c5_full_size_properties(env, f64):
     """configs[4]: the bench's 4096 x 4096 x 3 layered volume (z padded with +inf layers, 5 in
     memory) through the layered solver, fp32 (64-row tiles) and fp64 (40-row tiles, the reference's

@@ -23,6 +23,9 @@ T = torch.empty_like(cost)
 lib = L.lib()
 lib.eik_fim2d_qcount.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
 names = ["-", "-", "-", "fifo_ok", "fifo_stale", "dispatches", "dup_push", "band_put"]
+cf = cost[torch.isfinite(cost) & (cost > 0)]
+print(f"cost geomean {float(torch.exp(torch.log(cf).mean())):.3f}: band width = multiplier x {64 * float(torch.exp(torch.log(cf).mean())):.1f}",
+      flush=True)
 for p in [float(v) for v in sys.argv[1:]]:
     ctx = eikonal.Context(0)
     ctx.set_option(L.OPT_PRIO, p)
