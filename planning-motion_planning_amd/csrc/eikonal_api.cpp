@@ -147,7 +147,10 @@ struct eik_ctx {
     // solves are twice as fast per pass and the one-dispatcher bands held them back: C2 fp32 1.6 ->
     // 1.9 ms, C4 fp32 18.7 -> 10.8 Gcells/s (profiles/r05j_bench.json).  Batches of > 2 maps: FIFO.
     double prio = -1.0;
-    int layer_planar = 0;        // EIK_OPT_LAYER_PLANAR: the layered solver works on layer-planar copies
+    // EIK_OPT_LAYER_PLANAR (default 1): the layered solver works on layer-planar copies.  C5 kernel
+    // traffic per launch 9.06 -> 3.92 GB (fp32), 20.3 -> 8.6 GB (fp64), the time within noise
+    // (the layered sweep is VALU-bound; profiles/r05c_pmc_traffic_c5*.json, r05h_prio_planar_ab.log)
+    int layer_planar = 1;
     DevBuf lp_cost, lp_T;        // those copies (solve_layered)
     int path_loop = 2;           // EIK_OPT_PATH_LOOP: 2D walker loop form (profiles/r02i_path_walker.log)
     int timing = 0;

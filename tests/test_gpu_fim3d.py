@@ -126,11 +126,12 @@ def test_layered_vs_oracle(ctx, shape, seed, pad, switch):
 
 
 @pytest.fixture(scope="module")
-def ctx_planar():
-    """The layered solver on layer-planar copies of the solved layers (EIK_OPT_LAYER_PLANAR)."""
+def ctx_volume():
+    """The layered solver in the volume's own [y][x][L] layout (EIK_OPT_LAYER_PLANAR 0; the default
+    solves on layer-planar copies of the solved layers)."""
     import eikonal
 
-    c = eikonal.Context(0, options={"LAYER_PLANAR": 1})
+    c = eikonal.Context(0, options={"LAYER_PLANAR": 0})
     yield c
     c.close()
 
@@ -138,9 +139,9 @@ def ctx_planar():
 @pytest.mark.parametrize("shape,seed,pad,switch", [((130, 150, 2), 11, False, True), ((90, 140, 3), 14, True, True),
                                                      ((300, 257, 3), 15, False, True), ((70, 65, 1), 16, False, False),
                                                      ((5, 3, 2), 42, False, False), ((39, 65, 3), 43, True, False)])
-def test_layered_planar_vs_oracle(ctx_planar, shape, seed, pad, switch):
-    """EIK_OPT_LAYER_PLANAR: the same solve on [nl][H][W] copies (cost copied in, field copied out with
-    +inf in the padding layers) -- fields against the oracle in both dtypes, the padding +inf."""
+def test_layered_volume_layout_vs_oracle(ctx_volume, shape, seed, pad, switch):
+    """EIK_OPT_LAYER_PLANAR 0: the solve in the volume's [y][x][L] layout (the default solves on
+    [nl][H][W] copies, test_layered_vs_oracle) -- fields against the oracle in both dtypes."""
     c, goal = _layered_case(shape, seed, pad, switch)
     O.set_strict(False)
     try:
@@ -148,7 +149,7 @@ def test_layered_planar_vs_oracle(ctx_planar, shape, seed, pad, switch):
     finally:
         O.set_strict(True)
     for f64 in (False, True):
-        T = ctx_planar.tmap3d(c, goal, dtype=np.float64 if f64 else np.float32)
+        T = ctx_volume.tmap3d(c, goal, dtype=np.float64 if f64 else np.float32)
         check(T, R, f64)
         if pad:
             assert np.all(np.isinf(T[:, :, 0])) and np.all(np.isinf(T[:, :, -1]))
