@@ -96,7 +96,9 @@ typedef enum {
                                 computed before its special cases are tested) with the f64 sqrt /
                                 division free of range handling inside their safe domain; 1 = the
                                 same loop with the compiler's sqrt / division; 0 = the loop in
-                                the reference's statement order.  Same path bits in all three.  */
+                                the reference's statement order; 3 = form 2 with both divisions
+                                taken from the square roots' reciprocals (gdm.hip div_rs, checked
+                                by eik_selftest_walker_math).  Same path bits in all four.      */
     EIK_OPT_FRONTS_CAP = 13, /* biComputeTmap / rover path, rasters >= 2^20 cells: 1 (default) solves
                                 each front only up to a cap on T estimated from a coarse copy of
                                 the raster (x 1.25) and falls back to the full solve when the
@@ -287,8 +289,10 @@ int eik_ipc_close(eik_ctx* ctx, void* d_ptr);
 /* Self-test (no reference counterpart): the 2D path kernel's fast-path f64 square root,
  * division and interpolation against the exact forms they replace, on n pseudo-random inputs
  * each from their domain (gdm.hip walker_math_selftest_kernel); counts[0..2] = mismatches of
- * each (0 expected), counts[3] = samples evaluated (n). */
-int eik_selftest_walker_math(eik_ctx* ctx, int64_t n, uint64_t seed, int64_t counts[4]);
+ * each (0 expected), counts[3] = samples evaluated (n), counts[4] = mismatches of the division
+ * taken from the square root's reciprocal (path loop forms 3-4), counts[5] = mismatches of the
+ * one-correction square root (form 4); 0 expected in both. */
+int eik_selftest_walker_math(eik_ctx* ctx, int64_t n, uint64_t seed, int64_t counts[6]);
 
 /* getPathGDM on a device-resident field; out/n_out/status are device pointers. */
 int eik_path2d_dev(eik_ctx* ctx, const void* d_T, int dtype, int64_t H, int64_t W, const double init[2],

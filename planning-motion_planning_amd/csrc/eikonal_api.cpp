@@ -391,7 +391,7 @@ int eik_set_option(eik_ctx* c, int opt, double v) {
         case EIK_OPT_LIVE_PACK: c->live_pack = v != 0; break;
         case EIK_OPT_PRIO: c->prio = v; break;
         case EIK_OPT_LAYER_PLANAR: c->layer_planar = v != 0; break;
-        case EIK_OPT_PATH_LOOP: c->path_loop = std::max(0, std::min(2, (int)v)); break;
+        case EIK_OPT_PATH_LOOP: c->path_loop = std::max(0, std::min(4, (int)v)); break;
         case EIK_OPT_FRONTS_CAP: c->fronts_cap = v <= 0 ? 0.0 : v == 1 ? kFrontsMargin : std::max(1.0, v); break;
         default: return set_err(c, EIK_ERR_ARG, "unknown option %d", opt);
     }
@@ -1324,17 +1324,17 @@ int eik_bidir_join_f64(eik_ctx* c, const double* TG, const double* TS, int64_t H
     return EIK_OK;
 }
 
-int eik_selftest_walker_math(eik_ctx* c, int64_t n, uint64_t seed, int64_t mismatches[4]) {
+int eik_selftest_walker_math(eik_ctx* c, int64_t n, uint64_t seed, int64_t mismatches[6]) {
     if (!c || !mismatches || n < 1) return EIK_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, c->misc.ensure(64));
     unsigned long long* d = (unsigned long long*)c->misc.p;
-    HIPCHK(c, hipMemsetAsync(d, 0, 4 * sizeof(unsigned long long), c->stream));
+    HIPCHK(c, hipMemsetAsync(d, 0, 6 * sizeof(unsigned long long), c->stream));
     HIPCHK(c, walker_math_selftest((long long)n, (unsigned long long)seed, d, c->stream));
-    unsigned long long h[4];
+    unsigned long long h[6];
     HIPCHK(c, hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    for (int k = 0; k < 4; ++k) mismatches[k] = (int64_t)h[k];
+    for (int k = 0; k < 6; ++k) mismatches[k] = (int64_t)h[k];
     return EIK_OK;
 }
 

@@ -101,6 +101,49 @@ __device__ __forceinline__ double sqrt_core(double x) {
     d = __builtin_fma(-g, g, x);
     return __builtin_fma(d, h, g);
 }
+// sqrt_core that also hands out its refined half reciprocal hh ~ 1 / (2 sqrt(x)) (one
+// Goldschmidt update of v_rsq_f64's estimate: ~2^-44 relative or better).  Same bits as sqrt_core.
+__device__ __forceinline__ double sqrt_core_h(double x, double& hh) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = y * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    hh = h;
+    double d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, x);
+    return __builtin_fma(d, h, g);
+}
+// sqrt_core_h with ONE residual correction after the Goldschmidt update instead of two: g is
+// within ~2^-43 of sqrt(x) there, so g + (x - g^2) h is within ~2^-86 and the final fma rounds it
+// as the correctly rounded root unless sqrt(x) lies that close to a rounding midpoint (~2^-33 of
+// roots; an exact midpoint is impossible).  Checked bit for bit against sqrt by
+// walker_math_selftest_kernel (counts[5]) on the walker's domain x in [2^-767, 2^200].  Two
+// dependent operations shorter: the lane-pair walker's chain (LOOP 4) holds two of them per step.
+__device__ __forceinline__ double sqrt_c1_h(double x, double& hh) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = y * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    hh = h;
+    const double d = __builtin_fma(-g, g, x);
+    return __builtin_fma(d, h, g);
+}
+// n / d for d = sqrt_core_h(x, h), from the reciprocal 2h the square root already holds: q0 =
+// n * 2h is formed while the root is still being refined, and ONE residual correction (e = n -
+// d q0 by fma, q0 + e 2h by fma) leaves two dependent operations after d instead of div_core's
+// eight.  The exact sum q0 + e 2h is within ~2^-86 (relative) of n / d, so the final fma rounds it
+// as the correctly rounded quotient unless n / d lies that close to a rounding midpoint (~2^-33
+// of quotients): checked bit for bit against n / d by walker_math_selftest_kernel (counts[4]) on
+// the walker's domain (d = sqrt(x), x in [2^-767, 2^200], |n| <= d, n = 0 or |n| >= 2^-900).
+__device__ __forceinline__ double div_rs(double n, double d, double h) {
+    const double r = h + h;  // exact
+    const double q0 = n * r;
+    const double e = __builtin_fma(-d, q0, n);
+    return __builtin_fma(e, r, q0);
+}
 __device__ __forceinline__ double div_core(double n, double d) {
     double r = __builtin_amdgcn_rcp(d);
     double e = __builtin_fma(-d, r, 1.0);
@@ -128,6 +171,24 @@ __device__ __forceinline__ bool walk_odd(double dx, double dy, double s1) {
     const double lo = 0x1p-767, big = 0x1p200, tiny = 0x1p-900;
     return !(s1 >= lo && s1 <= big) | ((dx != 0.0) & (__builtin_fabs(dx) < tiny)) |
            ((dy != 0.0) & (__builtin_fabs(dy) < tiny));
+}
+
+// DPP quad_perm moves of a double, the 2D walker's lane-pair form: Q = 0xB1 [1, 0, 3, 2] the
+// partner lane's value (lane ^ 1), 0xA0 [0, 0, 2, 2] the even lane's, 0xF5 [1, 1, 3, 3] the odd one's
+template <int Q>
+__device__ __forceinline__ double quad_perm_f64(double v) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)b, Q, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(unsigned)(b >> 32), Q, 0xf, 0xf, false);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ __forceinline__ double pair_swap(double v) { return quad_perm_f64<0xB1>(v); }
+
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
 enum { kGdmDone = 0, kGdmFallback = 1, kGdmError = 2 };
@@ -410,6 +471,27 @@ __global__ __launch_bounds__(kPathThreads) void gdm2d_kernel(Gdm2dArgs a) {
         odd = walk_odd(o.dx, o.dy, s1);
         return o;
     };
+    // step_math_core with the divisions taken from the square roots' reciprocals (div_rs): the
+    // step's dependent f64 chain 45 -> 33 operations (LOOP 3)
+    auto step_math_rs = [&](const double2& g00, const double2& g01, const double2& g10, const double2& g11, double fa,
+                            double fb, bool& odd) -> StepOut {
+        StepOut o;
+        o.dx = interp2_general(fa, fb, g00.x, g01.x, g10.x, g11.x);
+        o.dy = interp2_general(fa, fb, g00.y, g01.y, g10.y, g11.y);
+        const double s1 = o.dx * o.dx + o.dy * o.dy;
+        double h1, h2;
+        const double nrm = sqrt_core_h(s1, h1);
+        const double dxn = div_rs(o.dx, nrm, h1);
+        const double r2 = sqrt_core_h(dxn * dxn + o.dy * o.dy, h2);
+        const long long small = -(long long)(nrm < 0.01);
+        const double den = __longlong_as_double((__double_as_longlong(nrm) & small) | (__double_as_longlong(r2) & ~small));
+        const double hd = __longlong_as_double((__double_as_longlong(h1) & small) | (__double_as_longlong(h2) & ~small));
+        const double dyn = div_rs(o.dy, den, hd);
+        o.sx = px - tau * dxn;
+        o.sy = py - tau * dyn;
+        odd = walk_odd(o.dx, o.dy, s1);
+        return o;
+    };
     // the point budget folded into the step count: point n = k + 1 is stored at step k (:173)
     const long kmax = a.steps < a.cap - 1 ? a.steps : a.cap - 1;
     long k = 0;
@@ -422,11 +504,92 @@ __global__ __launch_bounds__(kPathThreads) void gdm2d_kernel(Gdm2dArgs a) {
         // the arithmetic they skip.  The LDS address of a step whose cell is outside the fast
         // bounds is clamped into the window buffers (its values are discarded).
         constexpr unsigned kWinBytes = sizeof(s.g[0]);
+        // LOOP 4, the lane-pair form: even lanes carry the x component of every per-component
+        // quantity (coordinate, fraction, interpolated gradient, quotient), odd lanes the y one,
+        // so each f64 instruction of the step does the work of both components; the few sums and
+        // hand-overs across the pair are DPP moves (pair_swap).  Every lane computes the same
+        // operations on the same operands as form 3 does for its component -- sums of the two
+        // components (dx dx + dy dy, ex ex + ey ey) are commutative, so both lanes of a pair hold
+        // the same bits -- and the exit conditions are wave-uniform votes.
+        const bool yl = (threadIdx.x & 1) != 0;
+        const double dmax = __builtin_fabs(tau) * 1.4142135623730951 * (1.0 + 0x1p-20) + 0x1p-20;
+        double* const outl = out + (threadIdx.x & 1);
         for (; k < kmax;) {
             uint32_t i, j;
             bool in, odd = false;
             StepOut o;
             double fa, fb;
+            if constexpr (LOOP == 4) {
+                double p = yl ? py : px, d = 0.0, pn = 0.0;
+                // this lane's fast bounds (x or y) as a half-open f64 range: lo <= p < hi + 1 (NaN
+                // fails it; p in (-1, 0) goes to the handler, which is exact anyway)
+                const double loc = yl ? lo_y : lo_x, hic = (yl ? hi_y : hi_x) + 1;
+                // Steps this loop may take without the stop test: none of them can come within 1.5
+                // of the goal (:231) -- a step moves each coordinate by at most |tau| (|dxn|, |dyn|
+                // <= 1), so k steps move at most k |tau| sqrt(2) (with slack for rounding) -- and
+                // within the point budget.  The step after them leaves to the handler, which tests.
+                const double ex0 = px - a.ex, ey0 = py - a.ey;
+                const double room = (__builtin_sqrt(ex0 * ex0 + ey0 * ey0) * (1.0 - 0x1p-30) - 1.5) / dmax;
+                long kl = kmax - 1 - k;
+                const long safe = room >= 1.0 ? (room < 2e9 ? (long)room : 2000000000L) : 0L;  // NaN: 0
+                kl = kl < safe ? kl : safe;
+                const int left = (int)kl;
+                // the corners' LDS address in vector registers: each lane scales its own cell
+                // index (x: 16 B per column, y: kPW x 16 B per row) and adds its partner's (DPP)
+                const unsigned sc = yl ? kPW * (unsigned)sizeof(double2) : (unsigned)sizeof(double2);
+                const unsigned c0 = (unsigned)(yl ? cy0i : cx0i) * sc;
+                const char* const base = reinterpret_cast<const char*>(s.g[cur]) + (yl ? sizeof(double) : 0);
+                int kk = 0;
+                for (;;) {
+                    const double t = __builtin_trunc(p);
+                    const uint32_t u = (uint32_t)t;
+                    in = __builtin_amdgcn_ballot_w64(!(p >= loc && p < hic)) == 0ull;
+                    const unsigned own = u * sc - c0;
+                    unsigned off = own + (unsigned)__builtin_amdgcn_mov_dpp((int)own, 0xB1, 0xf, 0xf, false);
+                    off = off < kWinBytes - (kPW + 2) * (unsigned)sizeof(double2) ? off : kWinBytes - (kPW + 2) * (unsigned)sizeof(double2);
+                    const char* gq = base + off;
+                    const double g00 = *reinterpret_cast<const double*>(gq);
+                    const double g01 = *reinterpret_cast<const double*>(gq + sizeof(double2));
+                    const double g10 = *reinterpret_cast<const double*>(gq + kPW * sizeof(double2));
+                    const double g11 = *reinterpret_cast<const double*>(gq + (kPW + 1) * sizeof(double2));
+                    const double f = p - t;  // fa (even) / fb (odd); in bounds t = i or j
+                    fa = quad_perm_f64<0xA0>(f);
+                    fb = quad_perm_f64<0xF5>(f);
+                    d = interp2_general(fa, fb, g00, g01, g10, g11);  // dx (even) / dy (odd)
+                    const double sq = d * d;
+                    const double s1 = sq + pair_swap(sq);            // dx dx + dy dy in both lanes
+                    double h1, h2;
+                    const double nrm = sqrt_c1_h(s1, h1);
+                    const double q1 = div_rs(d, nrm, h1);            // dxn (even) / dy / nrm (odd)
+                    const double dxn = pair_swap(q1);                // odd lanes: dxn
+                    const double r2 = sqrt_c1_h(dxn * dxn + sq, h2);
+                    const double q2 = div_rs(d, r2, h2);             // odd lanes: dy / r2
+                    const double dn = (yl && !(nrm < 0.01)) ? q2 : q1;
+                    pn = p - tau * dn;                               // sx (even) / sy (odd)
+                    // (a NaN d makes s1 NaN: odd)
+                    const bool oddl = !(s1 >= 0x1p-767 && s1 <= 0x1p200) | ((d != 0.0) & (__builtin_fabs(d) < 0x1p-900));
+                    const bool bad = __builtin_amdgcn_ballot_w64(oddl) != 0ull;
+                    if ((int)!in | (int)bad | (int)(kk >= left)) break;
+                    outl[2 * n] = pn;  // every lane: its component's address
+                    ++n;
+                    p = pn;
+                    ++kk;
+                }
+                k += kk;
+                // the scalar state of the exit step for the handler below: lanes 0 (x) and 1 (y)
+                // read into scalar registers, so the handler stays wave-uniform code
+                px = readlane_f64(p, 0);
+                py = readlane_f64(p, 1);
+                i = (uint32_t)__builtin_trunc(px);
+                j = (uint32_t)__builtin_trunc(py);
+                o.dx = readlane_f64(d, 0);
+                o.dy = readlane_f64(d, 1);
+                o.sx = readlane_f64(pn, 0);
+                o.sy = readlane_f64(pn, 1);
+                odd = walk_odd(o.dx, o.dy, o.dx * o.dx + o.dy * o.dy);  // the loop's test, on lanes 0 / 1
+                fa = px - i;
+                fb = py - j;
+            } else
             for (;;) {
                 EIK_P2PROBE(0);
                 i = (uint32_t)__builtin_trunc(px);
@@ -438,7 +601,9 @@ __global__ __launch_bounds__(kPathThreads) void gdm2d_kernel(Gdm2dArgs a) {
                 EIK_P2PROBE(1);
                 fa = px - i;
                 fb = py - j;
-                if constexpr (LOOP == 2)
+                if constexpr (LOOP == 3)
+                    o = step_math_rs(g[0], g[1], g[kPW], g[kPW + 1], fa, fb, odd);
+                else if constexpr (LOOP == 2)
                     o = step_math_core(g[0], g[1], g[kPW], g[kPW + 1], fa, fb, odd);
                 else
                     o = step_math(g[0], g[1], g[kPW], g[kPW + 1], fa, fb);
@@ -528,7 +693,10 @@ __global__ __launch_bounds__(kPathThreads) void gdm2d_kernel(Gdm2dArgs a) {
 // false): sqrt_core(x) vs sqrt(x) for x in [2^-767, 2^1000]; div_core(n, d) vs n / d for d in
 // [2^-900, 2^100], |n| <= d, n = 0 or |n| >= 2^-900 (a zero quotient may differ in sign only);
 // interp2_general vs interp2_sel for corners in [-1, 1] and fractions in [0, 1) that are exactly
-// 0 a quarter of the time.  counts[0..2]: mismatches of each; counts[3]: samples evaluated.
+// 0 a quarter of the time; div_rs(n, sqrt_core_h(x, h), h) vs n / sqrt(x) for x in [2^-767, 2^200],
+// |n| <= sqrt(x), n = 0 or |n| >= 2^-900.  counts[0..2]: mismatches of the first three;
+// counts[3]: samples evaluated; counts[4]: mismatches of div_rs; counts[5]: sqrt_c1_h(x) vs sqrt(x)
+// on the same x.
 __device__ __forceinline__ unsigned long long mix64(unsigned long long z) {  // splitmix64
     z += 0x9e3779b97f4a7c15ull;
     z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
@@ -541,7 +709,7 @@ __device__ __forceinline__ double dbl_exp(unsigned long long r, int e_lo, int e_
 }
 __device__ __forceinline__ double unit_f(unsigned long long r) { return (double)(r >> 11) * 0x1p-53; }  // [0, 1)
 __global__ void walker_math_selftest_kernel(long long n, unsigned long long seed, unsigned long long* counts) {
-    unsigned long long bad[3] = {0, 0, 0}, done = 0;
+    unsigned long long bad[5] = {0, 0, 0, 0, 0}, done = 0;
     for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (long long)gridDim.x * blockDim.x) {
         ++done;
         const unsigned long long r0 = mix64(seed ^ (4 * t)), r1 = mix64(seed ^ (4 * t + 1)), r2 = mix64(seed ^ (4 * t + 2)),
@@ -558,9 +726,22 @@ __global__ void walker_math_selftest_kernel(long long n, unsigned long long seed
         for (int c = 0; c < 4; ++c) g[c] = 2.0 * unit_f(mix64(r3 + 2 + c)) - 1.0;
         const double i1 = interp2_general(fa, fb, g[0], g[1], g[2], g[3]), i0 = interp2_sel(fa, fb, g[0], g[1], g[2], g[3]);
         if (i0 == 0.0 ? i1 != 0.0 : __double_as_longlong(i1) != __double_as_longlong(i0)) ++bad[2];
+        const unsigned long long r4 = mix64(seed ^ ~(4 * t)), r5 = mix64(r4);
+        const double xs = dbl_exp(r4, -767, 199);
+        double hs;
+        const double ds = sqrt_core_h(xs, hs);
+        double ns = ds * (2.0 * unit_f(r5) - 1.0);
+        if (__builtin_fabs(ns) < 0x1p-900 || (r5 & 15) == 0) ns = (r5 & 16) ? -0.0 : 0.0;
+        if ((r5 & 0x300) == 0) ns = (r5 & 32) ? -ds : ds;  // |n| = d exactly (a unit component)
+        const double f1 = div_rs(ns, ds, hs), f0 = ns / __builtin_sqrt(xs);
+        if (f0 == 0.0 ? f1 != 0.0 : __double_as_longlong(f1) != __double_as_longlong(f0)) ++bad[3];
+        double hc;
+        if (__double_as_longlong(sqrt_c1_h(xs, hc)) != __double_as_longlong(__builtin_sqrt(xs))) ++bad[4];
     }
     for (int k = 0; k < 3; ++k)
         if (bad[k]) atomicAdd(&counts[k], bad[k]);
+    if (bad[3]) atomicAdd(&counts[4], bad[3]);
+    if (bad[4]) atomicAdd(&counts[5], bad[4]);
     if (done) atomicAdd(&counts[3], done);
 }
 hipError_t walker_math_selftest(long long n, unsigned long long seed, unsigned long long* d_counts, hipStream_t st) {
@@ -571,11 +752,15 @@ hipError_t walker_math_selftest(long long n, unsigned long long seed, unsigned l
 hipError_t gdm2d(const Gdm2dArgs& a, bool f64, hipStream_t st) {
     const dim3 g(1), b(kPathThreads);
     if (f64) {
-        if (a.fused == 2)      hipLaunchKernelGGL((gdm2d_kernel<double, 2>), g, b, 0, st, a);
+        if (a.fused == 4)      hipLaunchKernelGGL((gdm2d_kernel<double, 4>), g, b, 0, st, a);
+        else if (a.fused == 3) hipLaunchKernelGGL((gdm2d_kernel<double, 3>), g, b, 0, st, a);
+        else if (a.fused == 2) hipLaunchKernelGGL((gdm2d_kernel<double, 2>), g, b, 0, st, a);
         else if (a.fused == 1) hipLaunchKernelGGL((gdm2d_kernel<double, 1>), g, b, 0, st, a);
         else                   hipLaunchKernelGGL((gdm2d_kernel<double, 0>), g, b, 0, st, a);
     } else {
-        if (a.fused == 2)      hipLaunchKernelGGL((gdm2d_kernel<float, 2>), g, b, 0, st, a);
+        if (a.fused == 4)      hipLaunchKernelGGL((gdm2d_kernel<float, 4>), g, b, 0, st, a);
+        else if (a.fused == 3) hipLaunchKernelGGL((gdm2d_kernel<float, 3>), g, b, 0, st, a);
+        else if (a.fused == 2) hipLaunchKernelGGL((gdm2d_kernel<float, 2>), g, b, 0, st, a);
         else if (a.fused == 1) hipLaunchKernelGGL((gdm2d_kernel<float, 1>), g, b, 0, st, a);
         else                   hipLaunchKernelGGL((gdm2d_kernel<float, 0>), g, b, 0, st, a);
     }
@@ -735,12 +920,6 @@ __device__ __forceinline__ int rint_i32(double x) {
     int r;
     asm("v_cvt_i32_f64 %0, %1" : "=v"(r) : "v"(__builtin_rint(x)));
     return r;
-}
-__device__ __forceinline__ double readlane_f64(double v, int l) {
-    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
-    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
 // v from lane - SH of the same 16-lane row (DPP row_shr); lanes with no source keep their own

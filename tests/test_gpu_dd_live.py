@@ -292,3 +292,130 @@ def test_c4_split_4x2_assembled_field():
     assert rel.max() <= 1e-11, rel.max()
     res = _residual(Tdd, cost)
     assert res <= 1e-9, res
+
+
+class _HostStaged:
+    """dd.solve adapter for gloo between processes on one GPU: the device strips of a block solver
+    are staged through host tensors (RCCL cannot put two ranks on one device; on a node the strips
+    go over RCCL directly)."""
+
+    def __init__(self, loc, dsend, drecv):
+        self.loc, self.dsend, self.drecv = loc, dsend, drecv
+
+    def iterate(self, k):
+        self.loc.iterate(k)
+
+    def pack_edges(self, *hsend):
+        self.loc.pack_edges(*self.dsend)
+        for h, d in zip(hsend, self.dsend):
+            if h is not None:
+                h.copy_(d)
+
+    def merge_ghost(self, side, hrecv):
+        self.drecv[side].copy_(hrecv)
+        self.loc.merge_ghost(side, self.drecv[side])
+
+    def active(self):
+        return self.loc.active()
+
+
+def _layered_worker(rank, world, port, H, W, goal, q):
+    """One rank of a C5-style volume split in x-y (layers together): eikonal.Fim3dLayered on its
+    block with ghost strips of nl values per edge cell, the relaunch schedule (dd.solve) over gloo."""
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "planning-motion_planning_amd"))
+    import torch.distributed as dist
+
+    import eikonal
+    from eikonal import _lib as L
+    from eikonal import dd
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        px, py = dd.SPLITS[world]
+        blk = dd.Block(H, W, px, py, rank)
+        vol = _volume5(H, W, goal)
+        c = torch.from_numpy(np.ascontiguousarray(vol[blk.y0:blk.y1, blk.x0:blk.x1])).to(dev)
+        T = torch.empty_like(c)
+        ctx = eikonal.Context(0)
+        ctx.set_option(L.OPT_GRID, max(2, 2 * torch.cuda.get_device_properties(dev).multi_processor_count // world))
+        nl = 3
+        dsend, drecv, ghost = dd.make_strips(blk, torch.float64, dev, float("inf"), per_cell=nl)
+        hsend, hrecv, _ = dd.make_strips(blk, torch.float64, "cpu", float("inf"), per_cell=nl)
+        fim = eikonal.Fim3dLayered(ctx, blk.h, blk.w, 5, 1, nl, L.EIK_F64)
+        loc = dd.GpuLocalLayered(fim, ghost)
+        lg = blk.local_goal(goal[0], goal[1])
+        loc.start(c, T, (lg[0], lg[1], goal[2]), torch.cuda.current_stream(dev).cuda_stream)
+        rounds = dd.solve(_HostStaged(loc, dsend, drecv), blk, hsend, hrecv, exchange_every=4,
+                          count_device="cpu")
+        torch.cuda.synchronize()
+        q.put((rank, blk.y0, blk.y1, blk.x0, blk.x1, T.cpu().numpy(), rounds, None))
+        fim.close()
+        ctx.close()
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, 0, 0, 0, 0, None, 0, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _volume5(H, W, goal):
+    """a z-padded [H][W][5] volume as the planner builds its FM3D volumes (Coupled_motion_planner.py:
+    355-356): +inf first / last layers, three locomotion-mode layers of terrain-like cost"""
+    rng = np.random.default_rng(23)
+    c = rng.uniform(1, 5, (H, W, 3))
+    c[rng.random((H, W, 3)) < 0.08] = np.inf
+    c[:, : W // 2, 0] *= 0.3
+    c[:, W // 2:, 2] *= 0.3
+    inf = np.full((H, W, 1), np.inf)
+    v = np.concatenate([inf, c, inf], axis=2)
+    v[goal[1], goal[0], goal[2]] = 1.0
+    return v
+
+
+def test_c5_split_2x1_processes():
+    """SURVEY §8(e), C5 across GPUs: a 1024^2 x 3 fp64 volume (z-padded to 5) split 2 x 1 over two
+    processes sharing cuda:0, layers together, the relaunch schedule over gloo.  The assembled field
+    equals the single-domain layered solve (eik_tmap3d): masks equal, <= 1e-11 relative."""
+    import torch.multiprocessing as mp
+
+    import eikonal
+
+    world, H, W = 2, 1024, 1024
+    goal = (W // 3, H // 2, 2)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_layered_worker, args=(r, world, port, H, W, goal, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        parts = [q.get(timeout=240) for _ in range(world)]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    errs = [x[-1] for x in parts if x[-1]]
+    assert not errs, errs
+    Tdd = np.full((H, W, 5), np.nan)
+    for _, y0, y1, x0, x1, Tb, rounds, _ in parts:
+        Tdd[y0:y1, x0:x1] = Tb
+        assert rounds >= 2
+    vol = _volume5(H, W, goal)
+    ectx = eikonal.Context(0)
+    try:
+        ref = ectx.tmap3d(vol, np.array(goal), dtype=np.float64)
+    finally:
+        ectx.close()
+    inner = (slice(None), slice(None), slice(1, 4))
+    Tdd, ref = Tdd[inner], ref[inner]
+    fin = np.isfinite(ref)
+    assert fin.mean() > 0.5
+    assert np.array_equal(np.isfinite(Tdd), fin)
+    rel = np.abs(Tdd[fin] - ref[fin]) / np.maximum(ref[fin], 1e-30)
+    assert rel.max() <= 1e-11, rel.max()

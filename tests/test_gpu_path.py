@@ -158,11 +158,13 @@ def _walker_fields():
     return out
 
 
-@pytest.mark.parametrize("form", [1, 2])
+@pytest.mark.parametrize("form", [1, 2, 3, 4])
 @pytest.mark.parametrize("tau", [0.5, 1.7])
 def test_walker_loop_forms_bit_identical(golden, tau, form):
-    """EIK_OPT_PATH_LOOP: the single-exit step loop (1) and that loop with the range-free f64
-    sqrt / division (2, gdm.hip sqrt_core / div_core) return the SAME bits as the loop in the
+    """EIK_OPT_PATH_LOOP: the single-exit step loop (1), that loop with the range-free f64
+    sqrt / division (2, gdm.hip sqrt_core / div_core) and with the divisions taken from the square
+    roots' reciprocals (3, div_rs) and that arithmetic on lane pairs (4: x on even lanes, y on odd)
+    return the SAME bits as the loop in the
     reference's statement order (0) (array_equal, same status) -- on the golden fields and on
     fields that exercise window switches, NaN fallbacks, |g| < 0.01 unit steps and, at tau = 1.7,
     points that move more than one cell per step (the walker's slow path)."""
@@ -189,7 +191,7 @@ def test_walker_loop_forms_bit_identical(golden, tau, form):
 
 
 def test_walker_fast_math_exact():
-    """The 2D walker's fast-path arithmetic (gdm.hip sqrt_core, div_core, interp2_general) equals
+    """The 2D walker's fast-path arithmetic (gdm.hip sqrt_core, div_core, div_rs, interp2_general) equals
     the exact forms it replaces -- the correctly rounded f64 sqrt and division and interpolatePoint's
     special cases (FastMarching.py:327-336) -- bit for bit (a zero quotient up to its sign) on 4M
     pseudo-random inputs each from the domain the walker uses them on (walk_odd false)."""
@@ -199,9 +201,12 @@ def test_walker_fast_math_exact():
     c = eikonal.Context(0)
     try:
         for seed in (1, 0x9E3779B97F4A7C15):
-            counts = np.zeros(4, np.int64)
+            counts = np.zeros(6, np.int64)
             c._chk(L.lib().eik_selftest_walker_math(c._h, 1 << 22, seed, counts))
-            assert counts.tolist() == [0, 0, 0, 1 << 22], counts
+            assert counts.tolist() == [0, 0, 0, 1 << 22, 0, 0], counts
+        counts = np.zeros(6, np.int64)  # the one-correction square root and div_rs: 2^28 samples
+        c._chk(L.lib().eik_selftest_walker_math(c._h, 1 << 28, 77, counts))
+        assert counts[[0, 1, 2, 4, 5]].tolist() == [0, 0, 0, 0, 0] and counts[3] == 1 << 28, counts
     finally:
         c.close()
 
