@@ -92,13 +92,15 @@ typedef enum {
                                 reach it in place (no re-queued visit); 2 = after a visit's first
                                 pass, neighbour activations wait for the visit's end (default 1:
                                 profiles/r02d_grab_sched_ab.log)                                 */
-    EIK_OPT_PATH_LOOP = 12,  /* 2D path kernel: 2 (default) = one exit branch per step (the step is
+    EIK_OPT_PATH_LOOP = 12,  /* 2D path kernel: 2 = one exit branch per step (the step is
                                 computed before its special cases are tested) with the f64 sqrt /
                                 division free of range handling inside their safe domain; 1 = the
                                 same loop with the compiler's sqrt / division; 0 = the loop in
                                 the reference's statement order; 3 = form 2 with both divisions
                                 taken from the square roots' reciprocals (gdm.hip div_rs, checked
-                                by eik_selftest_walker_math).  Same path bits in all four.      */
+                                by eik_selftest_walker_math); 4 (default) = form 3 on lane pairs,
+                                x on even lanes, y on odd, one-correction square roots.  Same
+                                path bits in all five.                                          */
     EIK_OPT_FRONTS_CAP = 13, /* biComputeTmap / rover path, rasters >= 2^20 cells: 1 (default) solves
                                 each front only up to a cap on T estimated from a coarse copy of
                                 the raster (x 1.25) and falls back to the full solve when the

@@ -152,7 +152,8 @@ struct eik_ctx {
     // (the layered sweep is VALU-bound; profiles/r05c_pmc_traffic_c5*.json, r05h_prio_planar_ab.log)
     int layer_planar = 1;
     DevBuf lp_cost, lp_T;        // those copies (solve_layered)
-    int path_loop = 2;           // EIK_OPT_PATH_LOOP: 2D walker loop form (profiles/r02i_path_walker.log)
+    int path_loop = 4;           // EIK_OPT_PATH_LOOP: 2D walker loop form (4: lane pairs, round 5,
+                                 // 0.405 -> 0.30 us/step on the bench path, profiles/r05k_walker_ab.log)
     int timing = 0;
     int grid = 0;
     eik_stats last{};

@@ -200,6 +200,9 @@ enum { kGdmDone = 0, kGdmFallback = 1, kGdmError = 2 };
 #ifndef EIK_P3RUN
 #define EIK_P3RUN 1  // the 3D walker's integer-descent run loop (gdm3d_kernel)
 #endif
+#ifndef EIK_P4_CVT
+#define EIK_P4_CVT 0  // lane-pair walker (LOOP 4): the cell index by one v_cvt_u32_f64 (A/B switch)
+#endif
 #ifndef EIK_P2PROBE
 #define EIK_P2PROBE(k) ((void)0)  // 2D walker phase timing hooks (tools/path2_prof.hip)
 #define EIK_P2DECL ((void)0)
@@ -540,9 +543,21 @@ __global__ __launch_bounds__(kPathThreads) void gdm2d_kernel(Gdm2dArgs a) {
                 const unsigned c0 = (unsigned)(yl ? cy0i : cx0i) * sc;
                 const char* const base = reinterpret_cast<const char*>(s.g[cur]) + (yl ? sizeof(double) : 0);
                 int kk = 0;
-                for (;;) {
+                // One conditional branch per step: the point is stored and the state advanced before
+                // the exit test (the stores are in range -- n < cap -- and a step the handler below
+                // redoes stores its point at the same index), and the exit undoes the advance.
+                double pp = p;
+                bool leave;
+                do {
+#if EIK_P4_CVT
+                    // v_cvt_u32_f64 truncates: the address chain starts with one conversion, and the
+                    // cell corner comes back as a double beside it (equal to trunc(p) in bounds)
+                    const uint32_t u = (uint32_t)p;
+                    const double t = (double)u;
+#else
                     const double t = __builtin_trunc(p);
                     const uint32_t u = (uint32_t)t;
+#endif
                     in = __builtin_amdgcn_ballot_w64(!(p >= loc && p < hic)) == 0ull;
                     const unsigned own = u * sc - c0;
                     unsigned off = own + (unsigned)__builtin_amdgcn_mov_dpp((int)own, 0xB1, 0xf, 0xf, false);
@@ -569,12 +584,16 @@ __global__ __launch_bounds__(kPathThreads) void gdm2d_kernel(Gdm2dArgs a) {
                     // (a NaN d makes s1 NaN: odd)
                     const bool oddl = !(s1 >= 0x1p-767 && s1 <= 0x1p200) | ((d != 0.0) & (__builtin_fabs(d) < 0x1p-900));
                     const bool bad = __builtin_amdgcn_ballot_w64(oddl) != 0ull;
-                    if ((int)!in | (int)bad | (int)(kk >= left)) break;
                     outl[2 * n] = pn;  // every lane: its component's address
+                    leave = (int)!in | (int)bad | (int)(kk >= left);
                     ++n;
+                    pp = p;
                     p = pn;
                     ++kk;
-                }
+                } while (!leave);
+                --n;  // the exit step is the handler's
+                --kk;
+                p = pp;
                 k += kk;
                 // the scalar state of the exit step for the handler below: lanes 0 (x) and 1 (y)
                 // read into scalar registers, so the handler stays wave-uniform code
