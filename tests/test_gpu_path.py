@@ -236,3 +236,44 @@ def test_pinned_results_round_trip(ctx):
     T2 = ctx.tmap2d(cost, goal)  # reuses it (a second solve: equal up to the fp64 rounding of its schedule)
     fin = np.isfinite(Tp)
     assert np.array_equal(np.isfinite(T2), fin) and np.abs(T2[fin] - Tp[fin]).max() <= 1e-9
+
+
+@pytest.mark.parametrize("form", [2, 4])
+def test_walker_forms_budget_and_stop_edges(form):
+    """The lane-pair loop's own exits against the reference-order loop (form 0), bit for bit with the
+    same point count and status: point budgets that end the walk mid-way (cap 2, 3, 50, 1001: the
+    loop's 32-bit budget count), starts inside and just outside the stop radius (the safe-step count
+    is 0 or a few steps), a large and a tiny tau, and a start on a NaN point."""
+    import torch
+
+    import eikonal
+    from eikonal import _lib as L
+
+    (T, _, goal), = _walker_fields()[:1]
+    dev = torch.device("cuda", 0)
+    Td = torch.from_numpy(np.ascontiguousarray(T)).to(dev)
+    H, W = T.shape
+    g = np.array(goal, np.float64)
+    cases = [((25.3, 31.7), 0.5, cap) for cap in (2, 3, 50, 1001)]
+    cases += [((goal[0] + 1.0, goal[1] + 0.5), 0.5, 30004), ((goal[0] + 1.6, goal[1]), 0.5, 30004),
+              ((goal[0] - 2.9, goal[1] + 2.9), 0.5, 30004), ((400.5, 300.25), 2.3, 30004),
+              ((400.5, 300.25), 1e-3, 3000), ((float("nan"), 300.0), 0.5, 100)]
+    res = {}
+    for f in (0, form):
+        c = eikonal.Context(0)
+        try:
+            c.set_option(L.OPT_PATH_LOOP, f)
+            s = torch.cuda.current_stream(dev)
+            for q, (start, tau, cap) in enumerate(cases):
+                out = torch.full((cap, 2), -7.0, dtype=torch.float64, device=dev)
+                n = torch.zeros(1, dtype=torch.int64, device=dev)
+                st = torch.zeros(1, dtype=torch.int32, device=dev)
+                c._chk(L.lib().eik_path2d_dev(c._h, Td.data_ptr(), L.EIK_F64, H, W, np.array(start, np.float64), g,
+                                              tau, out.data_ptr(), cap, n.data_ptr(), st.data_ptr(), s.cuda_stream))
+                k = int(n.item())
+                res.setdefault(q, []).append((k, int(st.item()), out[:k].cpu().numpy()))
+        finally:
+            c.close()
+    for q, ((k0, s0, p0), (k1, s1, p1)) in res.items():
+        assert (k0, s0) == (k1, s1), (cases[q], k0, s0, k1, s1)
+        assert np.array_equal(p0, p1, equal_nan=True), cases[q]
