@@ -200,9 +200,6 @@ enum { kGdmDone = 0, kGdmFallback = 1, kGdmError = 2 };
 #ifndef EIK_P3RUN
 #define EIK_P3RUN 1  // the 3D walker's integer-descent run loop (gdm3d_kernel)
 #endif
-#ifndef EIK_P4_CVT
-#define EIK_P4_CVT 0  // lane-pair walker (LOOP 4): the cell index by one v_cvt_u32_f64 (A/B switch)
-#endif
 #ifndef EIK_P2PROBE
 #define EIK_P2PROBE(k) ((void)0)  // 2D walker phase timing hooks (tools/path2_prof.hip)
 #define EIK_P2DECL ((void)0)
@@ -549,15 +546,10 @@ __global__ __launch_bounds__(kPathThreads) void gdm2d_kernel(Gdm2dArgs a) {
                 double pp = p;
                 bool leave;
                 do {
-#if EIK_P4_CVT
-                    // v_cvt_u32_f64 truncates: the address chain starts with one conversion, and the
-                    // cell corner comes back as a double beside it (equal to trunc(p) in bounds)
-                    const uint32_t u = (uint32_t)p;
-                    const double t = (double)u;
-#else
+                    // (one v_cvt_u32_f64 on p, the corner as (double)u beside it: no difference,
+                    // profiles/r05k_walker_ab.log P4_CVT=1)
                     const double t = __builtin_trunc(p);
                     const uint32_t u = (uint32_t)t;
-#endif
                     in = __builtin_amdgcn_ballot_w64(!(p >= loc && p < hic)) == 0ull;
                     const unsigned own = u * sc - c0;
                     unsigned off = own + (unsigned)__builtin_amdgcn_mov_dpp((int)own, 0xB1, 0xf, 0xf, false);

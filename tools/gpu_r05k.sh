@@ -11,7 +11,6 @@ mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_gpu_path.py -x -v --timeout 120 --timeout-method thread -k "fast_math or loop_forms" > $O/r05k_tests.log 2>&1 || { echo "tests rc=$?"; tail -20 $O/r05k_tests.log; exit 1; }
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -DP2_NOPROBE tools/path2_prof.hip -o /tmp/p2n || exit 1
 hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/path2_prof.hip -o /tmp/p2p || exit 1
-hipcc --offload-arch=gfx950 -O3 -std=c++17 -DP2_NOPROBE -DEIK_P4_CVT=1 tools/path2_prof.hip -o /tmp/p2c || exit 1
 timeout -k 10 120 python tools/dumpT.py /tmp/T.f32 > /dev/null || exit 1
 {
 for r in 1 2 3; do
@@ -19,8 +18,6 @@ for r in 1 2 3; do
     echo "FUSED=$sp synthetic: $(FUSED=$sp timeout -k 10 60 /tmp/p2n | grep rep | tail -1)"
     echo "FUSED=$sp bench T:   $(FUSED=$sp timeout -k 10 60 /tmp/p2n /tmp/T.f32 | grep rep | tail -1)"
   done
-  echo "FUSED=4 P4_CVT=1 synthetic: $(FUSED=4 timeout -k 10 60 /tmp/p2c | grep rep | tail -1)"
-  echo "FUSED=4 P4_CVT=1 bench T:   $(FUSED=4 timeout -k 10 60 /tmp/p2c /tmp/T.f32 | grep rep | tail -1)"
 done
 echo "# s_memtime phase breakdown (probe build; the probes add their own cycles)"
 for sp in 2 4; do
