@@ -115,10 +115,13 @@ typedef enum {
                                 lowest entering T first, in 64 bands of width v x 64 x the geometric
                                 mean of the finite costs (fim_engine.hpp "priority bands"); 0 =
                                 the FIFO; < 0 (default) = 1 for fp64 solves, 0 for fp32          */
-    EIK_OPT_LAYER_PLANAR = 16 /* few-layer 3D volumes (the layered solver): 1 (default) solves on
+    EIK_OPT_LAYER_PLANAR = 16, /* few-layer 3D volumes (the layered solver): 1 (default) solves on
                                 layer-planar copies [nl][H][W] of the solved layers (one copy in,
                                 one out per solve; every tile-row access one contiguous run per
                                 layer); 0 = in the volume's [y][x][L] layout                     */
+    EIK_OPT_PRIO_RING = 17   /* slots per priority band (rounded up to a power of two; 0, the
+                                default: >= 2 x the tiles).  A band whose ring fills stops the
+                                launch; eik_fim2d_solve then solves again with the FIFO.         */
 } eik_option;
 
 typedef enum { EIK_MODE_LIST = 0, EIK_MODE_PERSISTENT = 1 } eik_mode;

@@ -147,6 +147,7 @@ struct eik_ctx {
     // solves are twice as fast per pass and the one-dispatcher bands held them back: C2 fp32 1.6 ->
     // 1.9 ms, C4 fp32 18.7 -> 10.8 Gcells/s (profiles/r05j_bench.json).  Batches of > 2 maps: FIFO.
     double prio = -1.0;
+    int prio_ring = 0;           // EIK_OPT_PRIO_RING: slots per priority band (0: pow2 >= 2 x the tiles)
     // EIK_OPT_LAYER_PLANAR (default 1): the layered solver works on layer-planar copies.  C5 kernel
     // traffic per launch 9.06 -> 3.92 GB (fp32), 20.3 -> 8.6 GB (fp64), the time within noise
     // (the layered sweep is VALU-bound; profiles/r05c_pmc_traffic_c5*.json, r05h_prio_planar_ab.log)
@@ -207,6 +208,8 @@ struct eik_fim2d {
     bool started = false;
     bool defer_sync = false;             // eik_fim2d_solve: the launch's read-back syncs with the finish
     bool need_rewind = false;            // a launch without its queue rewind ran since the last init
+    bool band_overflow = false;          // the last launch stopped on a full priority band (qerror bit 4)
+    bool no_bands = false;               // ... so this solver's next starts use the FIFO
     int persist_grid = 0;                // co-resident workgroups of the persistent kernel
     // live domain decomposition: hold word on the device, mailbox of the halo agent on the host
     DevBuf hold;
@@ -391,6 +394,7 @@ int eik_set_option(eik_ctx* c, int opt, double v) {
         case EIK_OPT_SCHED: c->sched = std::max(0, std::min(3, (int)v)); break;
         case EIK_OPT_LIVE_PACK: c->live_pack = v != 0; break;
         case EIK_OPT_PRIO: c->prio = v; break;
+        case EIK_OPT_PRIO_RING: c->prio_ring = v < 0 ? 0 : (int)std::min(v, 1073741824.0); break;
         case EIK_OPT_LAYER_PLANAR: c->layer_planar = v != 0; break;
         case EIK_OPT_PATH_LOOP: c->path_loop = std::max(0, std::min(4, (int)v)); break;
         case EIK_OPT_FRONTS_CAP: c->fronts_cap = v <= 0 ? 0.0 : v == 1 ? kFrontsMargin : std::max(1.0, v); break;
@@ -559,9 +563,13 @@ int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
     f->a.bctl = nullptr;
     // (one map or a few: a batch of independent maps keeps the FIFO -- their keys do not compare)
     const double prio = c->prio < 0 ? (f->f64 ? 1.0 : 0.0) : c->prio;
-    if (prio > 0 && f->a.mode == kModePersistent && f->B <= 2) {
+    if (prio > 0 && f->a.mode == kModePersistent && f->B <= 2 && !f->no_bands) {
         uint64_t bc = 1024;
         while (bc < 2 * (uint64_t)f->a.capacity) bc <<= 1;
+        if (c->prio_ring > 0) {  // (tests: a small ring forces the overflow fallback)
+            bc = 1;
+            while (bc < (uint64_t)c->prio_ring) bc <<= 1;
+        }
         HIPCHK(c, f->bslot.ensure(sizeof(unsigned) * kBands * bc));
         HIPCHK(c, f->bctl.ensure(128 * kBands + 128));  // + the band width's word
         HIPCHK(c, hipMemsetAsync(f->bslot.p, 0, sizeof(unsigned) * kBands * bc, f->stream));
@@ -583,6 +591,10 @@ int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
 static int persist_result(eik_fim2d* f, int64_t* active) {
     eik_ctx* c = f->ctx;
     const unsigned err = f->h_q[192 / 4];
+    f->band_overflow = (err & 4u) != 0u;
+    if (f->band_overflow)
+        return set_err(c, EIK_ERR_HIP, "persistent solver: a priority band's ring is full (EIK_OPT_PRIO=0 "
+                                       "uses the FIFO; eik_fim2d_solve falls back by itself)");
     if (err & 1u)
         return set_err(c, EIK_ERR_HIP, "persistent solver: a queue wait exceeded %.1f s (EIK_OPT_QTIMEOUT)",
                        c->qtimeout_s);
@@ -813,14 +825,21 @@ static int finish_solve(eik_fim2d* f, int64_t* active) {
 }
 
 int eik_fim2d_solve(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* goals, void* stream) {
-    int rc = eik_fim2d_start(f, d_cost, d_T, goals, stream);
-    if (rc) return rc;
     int64_t active = 0;
-    f->defer_sync = f->a.mode == kModePersistent;
-    rc = eik_fim2d_iterate(f, f->max_iters, &active);
-    f->defer_sync = false;
-    if (rc) return rc;
-    rc = finish_solve(f, &active);
+    int rc = EIK_OK;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        rc = eik_fim2d_start(f, d_cost, d_T, goals, stream);
+        if (rc) return rc;
+        f->defer_sync = f->a.mode == kModePersistent;
+        rc = eik_fim2d_iterate(f, f->max_iters, &active);
+        f->defer_sync = false;
+        if (!rc) rc = finish_solve(f, &active);  // (the persistent launch's error word is read here)
+        if (!(rc && f->band_overflow)) break;
+        // a priority band's ring was full: solve again from the start with the FIFO (this solver
+        // keeps it); finish_solve waited for the stream
+        f->band_overflow = false;
+        f->no_bands = true;
+    }
     if (rc) return rc;
     if (active != 0)
         return set_err(f->ctx, EIK_ERR_NOCONVERGE, "no convergence after %ld iterations (negative costs?)",
@@ -895,6 +914,9 @@ static int live_cmd(eik_fim2d* f, unsigned op, unsigned par) {
         __builtin_ia32_pause();
     }
     const unsigned err = __atomic_load_n(&b->error, __ATOMIC_RELAXED);
+    if (err & 4u)
+        return set_err(c, EIK_ERR_HIP, "live solve: a priority band's ring is full (EIK_OPT_PRIO=0 or a larger "
+                                       "EIK_OPT_PRIO_RING)");
     if (err & 1u)
         return set_err(c, EIK_ERR_HIP, "live solve: a queue wait exceeded %.1f s (EIK_OPT_QTIMEOUT)", c->qtimeout_s);
     if (err & 2u)
@@ -971,6 +993,9 @@ int eik_fim2d_release(eik_fim2d* f, int64_t* active) {
     if (c->timing) drain_timing(f);
     if (rc_cmd) return rc_cmd;
     const unsigned err = f->h_q[192 / 4];
+    if (err & 4u)
+        return set_err(c, EIK_ERR_HIP, "live solve: a priority band's ring is full (EIK_OPT_PRIO=0 or a larger "
+                                       "EIK_OPT_PRIO_RING)");
     if (err & 1u)
         return set_err(c, EIK_ERR_HIP, "live solve: a queue wait exceeded %.1f s (EIK_OPT_QTIMEOUT)", c->qtimeout_s);
     if (err & 2u)

@@ -280,9 +280,16 @@ __device__ __forceinline__ unsigned band_of(const Fim2dArgs& a, float k) {
 __device__ __forceinline__ void qcount(const Fim2dArgs& a, int i) {
     if (EIK_QDEBUG) atomicAdd(a.visits + 3 + i, 1ull);
 }
+// A band is a ring of bmask + 1 slots (eikonal_api.cpp: >= 2 x the tiles, EIK_OPT_PRIO_RING).  A
+// tile has at most one live entry per band per pending episode, but stale entries of earlier
+// episodes wait in their band until dispatched; a put that would lap an undispatched entry flags
+// qerror bit 4 (its head is loaded beside the tail's add, so no extra round trip; an older head
+// only errs on the safe side) and the host re-solves with the FIFO (eik_fim2d_solve).
 __device__ __forceinline__ void band_put(const Fim2dArgs& a, unsigned b, int tile) {
     qcount(a, 7);
+    const unsigned long long hd = __hip_atomic_load(&a.bctl[16 * b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long pos = atomicAdd(&a.bctl[16 * b + 8], 1ull);
+    if (pos > hd + a.bmask) atomicOr(a.qerror, 4u);
     __hip_atomic_store(&a.bslot[(size_t)b * (a.bmask + 1ull) + (pos & a.bmask)], (unsigned)tile + 1u, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
 }

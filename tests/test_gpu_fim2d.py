@@ -392,3 +392,30 @@ def test_priority_bands_fp64(kind, delta):
             assert (e <= lim).all(), (name, e.max(), (e / np.maximum(R[fin], 1)).max())
     finally:
         ctx.close()
+
+
+def test_priority_band_ring_overflow_falls_back():
+    """A priority band whose ring fills (EIK_OPT_PRIO_RING forced to 8 slots on a raster of ~200
+    tiles) stops the launch with qerror bit 4 and eik_fim2d_solve solves again with the FIFO: the
+    same field as a plain FIFO solve (<= 1e-9 / 1e-13 relative vs the oracle), no error raised."""
+    import eikonal
+    from eikonal import _lib as L
+
+    rng = np.random.default_rng(77)
+    H, W = 777, 1100
+    c = rng.uniform(1, 10, (H, W))
+    goal = [W // 3, H // 2]
+    R = oracle_field(c, goal)
+    fin = np.isfinite(R)
+    ctx = eikonal.Context(0)
+    try:
+        ctx.set_option(L.OPT_PRIO, 1.0)
+        ctx.set_option(L.OPT_PRIO_RING, 8)
+        T = ctx.tmap2d(c, goal, dtype=np.float64)
+        T2 = ctx.tmap2d(c, goal, dtype=np.float64)  # the same solver again: FIFO from the start
+    finally:
+        ctx.close()
+    lim = np.maximum(1e-9, 1e-13 * R[fin])
+    for X in (T, T2):
+        assert np.array_equal(np.isfinite(X), fin)
+        assert (np.abs(X[fin] - R[fin]) <= lim).all()
