@@ -176,6 +176,15 @@ __device__ __forceinline__ double min_nn(double a, double b) { return fmin_nn(a,
 // concurrent sweeps cover every x/y neighbour pair and the n-D update is monotone, so the fixed
 // point is the one of reading both neighbours per axis -- 3 cell reads per step instead of 5).
 // TH tile rows: TH + 64 skewed steps.
+// EIK_SWEEP_UNROLL_L: groups of kAhead steps per loop iteration (one back-branch each; fim2d.hip's
+// EIK_SWEEP_UNROLL).  1 -> 2: C5 fp64 1.85-1.92 -> 1.98-2.00, fp32 4.67 -> 4.76-4.85 Gcells/s; 4 in
+// between (profiles/r05p_layered_unroll_ab.log)
+#ifndef EIK_SWEEP_UNROLL_L
+#define EIK_SWEEP_UNROLL_L 2
+#endif
+#define EIK_STRL_(x) #x
+#define EIK_UNROLL_L_(n) _Pragma(EIK_STRL_(unroll n))
+#define EIK_UNROLL_L(n) EIK_UNROLL_L_(n)
 template <typename R, int TH, int NL, int DX, int DY>
 __device__ __forceinline__ void sweep_layered(LCell<R>* __restrict__ Ts, int lane) {
     constexpr R INF = Real<R>::inf();
@@ -212,6 +221,7 @@ __device__ __forceinline__ void sweep_layered(LCell<R>* __restrict__ Ts, int lan
     };
 #pragma unroll
     for (int u = 0; u < D; ++u) fetch(u);
+    EIK_UNROLL_L(EIK_SWEEP_UNROLL_L)
     for (int s = 0; s < TH + kTile; s += D) {
         const int gcur = gb;
         gb = clampb(raw);
