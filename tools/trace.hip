@@ -33,7 +33,7 @@ using namespace eik;
 #define CK(x) do { hipError_t e = (x); if (e) { printf("%s -> %s\n", #x, hipGetErrorString(e)); exit(2);} } while (0)
 int main(int argc, char** argv) {
     if (argc < 5) { printf("usage: trace N grid cost.f32|- out.bin [passes]\n"); return 2; }
-    int N = atoi(argv[1]), grid = atoi(argv[2]);
+    int N = atoi(argv[1]), grid = atoi(argv[2]);  // grid 0: the co-resident workgroups (as the library)
     const char* cf = strcmp(argv[3], "-") != 0 ? argv[3] : nullptr;  // "-": uniform cost
     const int passes = argc > 5 ? atoi(argv[5]) : 24;
     std::vector<float> hc((size_t)N * N, 1.f);
@@ -55,21 +55,41 @@ int main(int argc, char** argv) {
     a.cost = cost; a.T = T; a.H = N; a.W = N; a.ntx = ntx; a.nty = ntx; a.tiles_per_map = tiles;
     CK(hipMalloc(&a.lists, 12ull * tiles)); CK(hipMalloc(&a.counts, 256)); CK(hipMalloc(&a.mark, 4ull * tiles));
     a.capacity = tiles; a.max_rounds = 1; a.keep = 1.f; CK(hipMalloc(&a.key, 4ull * tiles)); a.minkey = (unsigned*)a.counts + 16;
-    a.delta = __builtin_inff(); CK(hipMalloc(&a.visits, 16));
+    a.delta = __builtin_inff(); CK(hipMalloc(&a.visits, 256));  // (the init kernel clears 22 words)
     char* q; CK(hipMalloc(&q, 256)); a.qhead = (unsigned long long*)q; a.qtail = (unsigned long long*)(q + 64);
     a.qactive = (int*)(q + 128); a.qerror = (unsigned*)(q + 192); a.mode = kModePersistent;
     unsigned qn = 4096; while (qn < 8u * tiles) qn <<= 1;
     a.qmask = qn - 1; CK(hipMalloc(&a.qslot, 4ull * qn)); CK(hipMalloc(&a.qstate, 4ull * tiles));
     a.qtimeout = 1000000000ull; a.qbudget = 1ull << 40; a.max_passes = passes;
-    a.ls = 1; a.z0 = 0;
+    a.ls = 1; a.z0 = 0; a.lzs = 1;
+    if (grid == 0) {
+        int cus = 0; CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+        grid = fim2d_persist_resident(f64, cus, false);
+        CK(hipFree(ev)); CK(hipMalloc(&ev, 8ull * kCap * grid));
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(g_ev), &ev, sizeof ev));
+        printf("grid: %d co-resident workgroups\n", grid);
+    }
+    // the W / E edge-column copies (fim2d.hip kEcol: on in fp64) and, with EIK_TRACE_PRIO=1, the
+    // priority bands as eikonal_api.cpp sets them up (width multiplier 1)
+    CK(hipMalloc(&a.ecol, esz * 2 * 64ull * tiles));
+    const bool prio = getenv("EIK_TRACE_PRIO") && atoi(getenv("EIK_TRACE_PRIO")) == 1;
+    if (prio) {
+        unsigned long long bc = 1024; while (bc < 2ull * tiles) bc <<= 1;
+        CK(hipMalloc(&a.bslot, 4ull * kBands * bc)); CK(hipMemset(a.bslot, 0, 4ull * kBands * bc));
+        CK(hipMalloc(&a.bctl, 128 * kBands + 128)); a.bmask = (unsigned)(bc - 1);
+        float* pd = (float*)((char*)a.bctl + 128 * kBands);
+        CK(fim2d_prio_delta(cost, f64, (int64_t)N * N, 1.f, pd, 0));
+        a.pdelta = pd;
+    }
     a.fresh_first = getenv("EIK_FRESH_FIRST") && atoi(getenv("EIK_FRESH_FIRST")) == 1;
     a.sched = getenv("EIK_SCHED") ? atoi(getenv("EIK_SCHED")) : 1;  // library default
     int64_t* goals; CK(hipMalloc(&goals, 16)); int64_t hg[2] = {N / 2, N / 2}; CK(hipMemcpy(goals, hg, 16, hipMemcpyHostToDevice));
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     float ms = 0;
     for (int rep = 0; rep < 4; ++rep) {
-        CK(hipMemset(a.visits, 0, 16)); CK(hipMemset(ev, 0, 8ull * kCap * grid));
-        CK(fim2d_init(a, f64, 1, goals, 0));
+        CK(hipMemset(a.visits, 0, 256)); CK(hipMemset(ev, 0, 8ull * kCap * grid));
+        if (a.bctl) CK(hipMemset(a.bctl, 0, 128 * kBands));
+        CK(fim2d_init(a, f64, 1, goals, nullptr, 0));
         CK(hipEventRecord(e0, 0));
         CK(fim2d_persist(a, f64, grid, 0));
         CK(hipEventRecord(e1, 0));
@@ -78,7 +98,7 @@ int main(int argc, char** argv) {
     }
     unsigned hq[64]; CK(hipMemcpy(hq, q, 256, hipMemcpyDeviceToHost));
     unsigned long long vv[2]; CK(hipMemcpy(vv, a.visits, 16, hipMemcpyDeviceToHost));
-    printf("%s N=%d grid=%d passes=%d: kernel %.3f ms, visits %llu (+%llu in place), err %u\n", f64 ? "f64" : "f32", N, grid, passes, ms, vv[0], vv[1], hq[48]);
+    printf("%s%s N=%d grid=%d passes=%d: kernel %.3f ms, visits %llu (+%llu in place), err %u\n", f64 ? "f64" : "f32", a.bctl ? " prio" : "", N, grid, passes, ms, vv[0], vv[1], hq[48]);
     std::vector<unsigned long long> he(1ull * kCap * grid);
     CK(hipMemcpy(he.data(), ev, 8ull * kCap * grid, hipMemcpyDeviceToHost));
     FILE* o = fopen(argv[4], "wb");

@@ -153,6 +153,7 @@ def main():
         if c[0] == "act":
             _, t, ax, prod, n = c
             rec["in"] = t
+            rec["busy"] = bool(ax & kBusy)
             chain.append(rec)
             v, out_t, out_n = prod, t, n
         else:
@@ -170,6 +171,15 @@ def main():
         kinds[r["kind"]] = kinds.get(r["kind"], 0) + 1
     print(f"  critical chain: {len(chain)} visits {kinds}, end {chain[-1]['out'] * us:.1f} us: wait {W:.1f} + stage {S:.1f} + work {K:.1f} us;"
           f" passes before hand-off mean {np.mean(npass):.2f}")
+    wb = [(r["grab"] - r["in"]) * us for r in chain if r.get("busy") and r["in"] is not None]
+    wf = [(r["grab"] - r["in"]) * us for r in chain if r.get("busy") is False and r["in"] is not None]
+    print(f"  chain hops whose activation found the tile busy: {len(wb)} (wait mean {np.mean(wb) if wb else 0:.1f} us), "
+          f"idle: {len(wf)} (wait mean {np.mean(wf) if wf else 0:.1f} us)")
+    # every visit caused by an activation: the wait split the same way
+    ab = [(v.grab - v.cause[1]) * us for v in visits if v.cause and v.cause[0] == "act" and (v.cause[2] & kBusy)]
+    af = [(v.grab - v.cause[1]) * us for v in visits if v.cause and v.cause[0] == "act" and not (v.cause[2] & kBusy)]
+    print(f"  all visits: busy at activation {len(ab)} (wait p50 {np.median(ab) if ab else 0:.1f} us), "
+          f"idle {len(af)} (wait p50 {np.median(af) if af else 0:.1f} us)")
     first = chain[0]
     print(f"  chain start: grab {first['grab'] * us:.1f} us")
     for r in chain[:: max(1, len(chain) // 24)]:
