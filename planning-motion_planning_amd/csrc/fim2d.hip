@@ -195,11 +195,11 @@ __device__ __forceinline__ Cell<R> make_cell(R t, R c, int col) {
 // groups per iteration took C2 fp64 2.35 -> 2.25 -> 2.23 ms, C2 fp32 1.63 -> 1.57 ms, C3 fp64 +4 %
 // (profiles/r05n_sweep_unroll_ab.log, r05o_sweep_unroll_248_ab.log); 8 loses in fp64.
 #ifndef EIK_SWEEP_UNROLL
-#define EIK_SWEEP_UNROLL 4
+#define EIK_SWEEP_UNROLL 4  // fp64
 #endif
-#define EIK_STR_(x) #x
-#define EIK_UNROLL_(n) _Pragma(EIK_STR_(unroll n))
-#define EIK_UNROLL(n) EIK_UNROLL_(n)
+#ifndef EIK_SWEEP_UNROLL_F32
+#define EIK_SWEEP_UNROLL_F32 4
+#endif
 template <typename R, int DX, int DY, bool TRACK, class Hook>
 __device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lane, R keep, Hook&& hook) {
     constexpr int S = (int)sizeof(Cell<R>);
@@ -247,7 +247,8 @@ __device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lan
     };
 #pragma unroll
     for (int u = 0; u < D; ++u) fetch(u);
-    EIK_UNROLL(EIK_SWEEP_UNROLL)
+    constexpr int kUnroll = sizeof(R) == 8 ? EIK_SWEEP_UNROLL : EIK_SWEEP_UNROLL_F32;
+#pragma unroll kUnroll
     for (int s = 0; s < 2 * kTile; s += D) {
         hook(s);  // per group: the in-sweep duties of the persistent driver (process_tile)
         const int gcur = gb;  // this group's rows (its ds_min targets)
