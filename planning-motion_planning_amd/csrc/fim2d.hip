@@ -198,7 +198,7 @@ __device__ __forceinline__ Cell<R> make_cell(R t, R c, int col) {
 #define EIK_SWEEP_UNROLL 4  // fp64
 #endif
 #ifndef EIK_SWEEP_UNROLL_F32
-#define EIK_SWEEP_UNROLL_F32 4
+#define EIK_SWEEP_UNROLL_F32 8  // C4 fp32 +3 %, C2 / C3 within noise (profiles/r05v_sweep_unroll_f32_ab.log)
 #endif
 template <typename R, int DX, int DY, bool TRACK, class Hook>
 __device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lane, R keep, Hook&& hook) {
