@@ -61,6 +61,7 @@ struct Fim2dArgs {
     unsigned bmask;
     unsigned long long* bctl;   // band b: head at bctl[16 b], tail at bctl[16 b + 8] (own 64-B lines)
     const float* pdelta;        // band width in units of T (device word: prio_delta_kernel sets it per solve)
+    unsigned disp;              // band entries moved per dispatch (fim_engine.hpp band_dispatch; 0: kDispatch)
 };
 
 // Host <-> halo-agent mailbox (pinned, coherent host memory).  The host writes cmd, then seq

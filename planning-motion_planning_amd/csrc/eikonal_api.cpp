@@ -580,6 +580,7 @@ int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
         float* pd = (float*)((char*)f->bctl.p + 128 * kBands);
         HIPCHK(c, fim2d_prio_delta(d_cost, f->f64, f->H * f->W, (float)prio, pd, f->stream));
         f->a.pdelta = pd;
+        f->a.disp = f->a.tiles_per_map >= kWideTiles ? 64u : 32u;  // (fim_engine.hpp band_dispatch)
     }
     HIPCHK(c, fim2d_init(f->a, f->f64, (int)f->B, (const int64_t*)f->goals.p, (unsigned*)f->edge.p, f->stream));
     f->started = true;

@@ -516,6 +516,11 @@ __device__ __forceinline__ unsigned wave_incl_sum(unsigned v) {
 // idle workgroup CAS-ed the lowest band's head lost ~900k CASes per C2 solve and ran 20x slower),
 // and the batch is the bands' throughput: C4 takes ~9 tiles per us, and one band per dispatch (a few
 // entries each, ~3 round trips) held narrow bands to a fraction of that (C4 2.7 vs 10.9 Gcells/s).
+// The batch a dispatch moves: Fim2dArgs::disp, set per solve (eikonal_api.cpp), else kDispatch;
+// at most 64 (one lane per entry).  32 on C2-sized maps; 64 on maps of >= kWideTiles tiles: C4 at
+// one GPU 13.8-14.3 -> 16.3-16.7 Gcells/s, while C2 loses 4 % with 64 -- a larger batch leaves a FIFO
+// backlog that no longer follows the bands' order.  (A batch limited to the waiting workgroups,
+// qhead - qtail: C4 10.6 -- the backlog is what feeds a busy chip; profiles/r05x_dispatch_ab.log.)
 constexpr unsigned kDispatch = 32;
 __device__ __forceinline__ bool band_dispatch(const Fim2dArgs& a) {
     const int lane = threadIdx.x & 63;
@@ -524,13 +529,14 @@ __device__ __forceinline__ bool band_dispatch(const Fim2dArgs& a) {
         h = __hip_atomic_load(&a.bctl[16 * lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         t = __hip_atomic_load(&a.bctl[16 * lane + 8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    const unsigned avail = t > h ? (unsigned)(t - h < kDispatch ? t - h : kDispatch) : 0u;
+    const unsigned lim = a.disp ? (a.disp < 64u ? a.disp : 64u) : kDispatch;
+    const unsigned avail = t > h ? (unsigned)(t - h < lim ? t - h : lim) : 0u;
     if (!__ballot(avail != 0u)) return false;
     // lowest bands first.  (Reserving a quarter of the batch for the highest band -- the front's
     // first visits -- was measured and removed: C4 at one GPU 14 -> 2.6-6 Gcells/s, C2 no gain,
     // profiles/r05h_prio_planar_ab.log.)
     const unsigned before = wave_incl_sum(avail) - avail;  // entries of the lower bands
-    const unsigned take = before >= kDispatch ? 0u : (avail < kDispatch - before ? avail : kDispatch - before);
+    const unsigned take = before >= lim ? 0u : (avail < lim - before ? avail : lim - before);
     const unsigned got = take && atomicCAS(&a.bctl[16 * lane], h, h + take) == h ? take : 0u;
     const unsigned end = wave_incl_sum(got), start = end - got;
     const unsigned total = __shfl(end, 63);
