@@ -119,9 +119,11 @@ typedef enum {
                                 layer-planar copies [nl][H][W] of the solved layers (one copy in,
                                 one out per solve; every tile-row access one contiguous run per
                                 layer); 0 = in the volume's [y][x][L] layout                     */
-    EIK_OPT_PRIO_RING = 17   /* slots per priority band (rounded up to a power of two; 0, the
+    EIK_OPT_PRIO_RING = 17,  /* slots per priority band (rounded up to a power of two; 0, the
                                 default: >= 2 x the tiles).  A band whose ring fills stops the
                                 launch; eik_fim2d_solve then solves again with the FIFO.         */
+    EIK_OPT_PRIO_DISPATCH = 18 /* band entries moved to the FIFO per dispatch, 1..64 (0, the
+                                default: 64 on maps of >= 16384 tiles, else 16)                 */
 } eik_option;
 
 typedef enum { EIK_MODE_LIST = 0, EIK_MODE_PERSISTENT = 1 } eik_mode;

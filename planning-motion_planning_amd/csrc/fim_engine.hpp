@@ -516,11 +516,13 @@ __device__ __forceinline__ unsigned wave_incl_sum(unsigned v) {
 // idle workgroup CAS-ed the lowest band's head lost ~900k CASes per C2 solve and ran 20x slower),
 // and the batch is the bands' throughput: C4 takes ~9 tiles per us, and one band per dispatch (a few
 // entries each, ~3 round trips) held narrow bands to a fraction of that (C4 2.7 vs 10.9 Gcells/s).
-// The batch a dispatch moves: Fim2dArgs::disp, set per solve (eikonal_api.cpp), else kDispatch;
-// at most 64 (one lane per entry).  32 on C2-sized maps; 64 on maps of >= kWideTiles tiles: C4 at
-// one GPU 13.8-14.3 -> 16.3-16.7 Gcells/s, while C2 loses 4 % with 64 -- a larger batch leaves a FIFO
-// backlog that no longer follows the bands' order.  (A batch limited to the waiting workgroups,
-// qhead - qtail: C4 10.6 -- the backlog is what feeds a busy chip; profiles/r05x_dispatch_ab.log.)
+// The batch a dispatch moves: Fim2dArgs::disp, set per solve (eikonal_api.cpp, EIK_OPT_PRIO_DISPATCH),
+// else kDispatch; at most 64 (one lane per entry).  64 on maps of >= kWideTiles tiles: C4 at one GPU
+// 13.8-14.3 -> 16.3-16.7 Gcells/s (48: 15.5-15.7); 16 below: C2 2.22-2.27 (32) -> 2.16-2.19 ms (8:
+// 2.20-2.22, 48: 2.31) -- a larger batch leaves a FIFO backlog that no longer follows the bands'
+// order, a smaller one dispatches more often.  (A batch limited to the waiting workgroups, qhead -
+// qtail: C4 10.6 -- the backlog is what feeds a busy chip.  profiles/r05x_dispatch_ab.log,
+// r05z2_dispatch_sweep.log.)
 constexpr unsigned kDispatch = 32;
 __device__ __forceinline__ bool band_dispatch(const Fim2dArgs& a) {
     const int lane = threadIdx.x & 63;

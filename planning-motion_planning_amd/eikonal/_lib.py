@@ -14,7 +14,7 @@ EIK_F32, EIK_F64 = 0, 1
 PATH_DONE, PATH_FALLBACK, PATH_ERROR = 0, 1, 2
 OPT_MAX_ROUNDS, OPT_SYNC_EVERY, OPT_TIMING, OPT_GRID, OPT_TOL, OPT_DELTA = 0, 1, 2, 3, 4, 5
 OPT_MODE, OPT_QTIMEOUT, OPT_MAX_VISITS, OPT_PASSES, OPT_FRESH_FIRST, OPT_SCHED, OPT_PATH_LOOP = 6, 7, 8, 9, 10, 11, 12
-OPT_FRONTS_CAP, OPT_LIVE_PACK, OPT_PRIO, OPT_LAYER_PLANAR, OPT_PRIO_RING = 13, 14, 15, 16, 17
+OPT_FRONTS_CAP, OPT_LIVE_PACK, OPT_PRIO, OPT_LAYER_PLANAR, OPT_PRIO_RING, OPT_PRIO_DISPATCH = 13, 14, 15, 16, 17, 18
 MODE_LIST, MODE_PERSISTENT = 0, 1
 
 i64 = C.c_int64
