@@ -583,6 +583,9 @@ __device__ __forceinline__ bool band_dispatch(const Fim2dArgs& a) {
 // Priority mode: qgrab for one whole wave.  Every workgroup takes a FIFO ticket; pushes go to the
 // FIFO while tickets wait, else to the bands, and the oldest waiter moves band entries to the FIFO
 // in band order.  Entries are claimed by a CAS (stale ones dropped: take another ticket).
+#ifndef EIK_PRIO_SLEEP
+#define EIK_PRIO_SLEEP 4  // s_sleep between a waiter's polls (x 64 cycles)
+#endif
 __device__ __forceinline__ int qgrab_prio(const Fim2dArgs& a, unsigned& trig) {
     const int lane = threadIdx.x & 63;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -630,7 +633,7 @@ __device__ __forceinline__ int qgrab_prio(const Fim2dArgs& a, unsigned& trig) {
                 }
                 if (__shfl(stop, 0)) return -1;
             }
-            __builtin_amdgcn_s_sleep(4);
+            __builtin_amdgcn_s_sleep(EIK_PRIO_SLEEP);
         }
     }
 }
