@@ -146,6 +146,8 @@ struct eik_ctx {
     // one GPU 10.5 -> 13.8 Gcells/s; 0.5 / 2 lose on C4 (6.9 / 12.9; profiles/r05i_prio_ab.log).  fp32
     // solves are twice as fast per pass and the one-dispatcher bands held them back: C2 fp32 1.6 ->
     // 1.9 ms, C4 fp32 18.7 -> 10.8 Gcells/s (profiles/r05j_bench.json).  Batches of > 2 maps: FIFO.
+    // The layered solver's default (both dtypes) is kLayeredPrio: C5 fp64 1.92 -> 3.65, fp32 4.73 ->
+    // 6.2 Gcells/s (profiles/r05ac_layered_prio_ab.json.log, r05ad_prio_width_ab.log).
     double prio = -1.0;
     int prio_ring = 0;           // EIK_OPT_PRIO_RING: slots per priority band (0: pow2 >= 2 x the tiles)
     int prio_dispatch = 0;       // EIK_OPT_PRIO_DISPATCH: band entries per dispatch (0: 64 on maps of >= kWideTiles, else 16)
@@ -1420,6 +1422,9 @@ int eik_path2d_f64(eik_ctx* c, const double* T, int64_t H, int64_t W, const doub
 // ------------------------------------------------------------------------------ 3D
 // Few-layer fp32 volumes (the rover's (x, y, mode) costmaps) on the layered 2D-tile solver:
 // layers z0 .. z0+nl-1 of a [H][W][L] volume, one persistent launch.
+// the layered solver's default band width (EIK_OPT_PRIO < 0): C5 A/B 0.125 / 0.25 / 0.5 / 1 = fp64 3.61 /
+// 3.65 / 3.58 / 3.40, fp32 6.20 / 6.22 / 6.21 / 6.07 Gcells/s, FIFO 1.92 / 4.73 (profiles/r05ad_prio_width_ab.log)
+constexpr double kLayeredPrio = 0.25;
 static int solve_layered(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, int64_t W, int64_t L, int z0, int nl,
                          const int64_t goal[3], int dtype, hipStream_t st) {
     const bool f64 = dtype == EIK_F64;
@@ -1466,9 +1471,35 @@ static int solve_layered(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, i
     if (res == 0) res = fim2dl_persist_resident(nl, f64, c->cu_count);
     const int grid = std::min(c->grid > 0 ? c->grid : 4 * c->cu_count, res);
     a.fresh_first = c->fresh_first;
+    unsigned err = 0;
+    // attempt 1 without bands when attempt 0's band ring overflowed (qerror bit 4, as eik_fim2d_solve)
+    for (int attempt = 0; attempt < 2; ++attempt) {
     HIPCHK(c, hipEventRecord(f->ev_start, st));
     HIPCHK(c, hipMemsetAsync((void*)f->a.visits, 0, 3 * sizeof(unsigned long long), st));
     if (planar) HIPCHK(c, layer_planar(d_cost, c->lp_cost.p, f64, H * W, L, z0, nl, true, st));
+    // priority bands (fim_engine.hpp), as eik_fim2d_start sets them up: on an explicit EIK_OPT_PRIO
+    a.bctl = nullptr;
+    const double prio = c->prio < 0 ? kLayeredPrio : c->prio;
+    if (prio > 0 && attempt == 0) {
+        uint64_t bc = 1024;
+        while (bc < 2 * (uint64_t)a.capacity) bc <<= 1;
+        if (c->prio_ring > 0) {  // (tests: a small ring forces the overflow fallback)
+            bc = 1;
+            while (bc < (uint64_t)c->prio_ring) bc <<= 1;
+        }
+        HIPCHK(c, f->bslot.ensure(sizeof(unsigned) * kBands * bc));
+        HIPCHK(c, f->bctl.ensure(128 * kBands + 128));
+        HIPCHK(c, hipMemsetAsync(f->bslot.p, 0, sizeof(unsigned) * kBands * bc, st));
+        HIPCHK(c, hipMemsetAsync(f->bctl.p, 0, 128 * kBands, st));
+        HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)a.key, 0x7f800000u, (size_t)a.capacity, st));  // keys: +inf
+        a.bslot = (unsigned*)f->bslot.p;
+        a.bmask = (unsigned)(bc - 1);
+        a.bctl = (unsigned long long*)f->bctl.p;
+        float* pd = (float*)((char*)f->bctl.p + 128 * kBands);
+        HIPCHK(c, fim2d_prio_delta(a.cost, f64, planar ? (int64_t)nl * H * W : H * W * L, (float)prio, pd, st));
+        a.pdelta = pd;
+        a.disp = c->prio_dispatch > 0 ? (unsigned)c->prio_dispatch : a.tiles_per_map >= kWideTiles ? 64u : 16u;
+    }
     HIPCHK(c, fim2dl_init(a, f64, goal[0], goal[1], goal[2] - z0, nT, st));
     HIPCHK(c, fim2dl_persist(a, nl, f64, grid, st));
     if (planar) HIPCHK(c, layer_planar(c->lp_T.p, d_T, f64, H * W, L, z0, nl, false, st));
@@ -1476,7 +1507,9 @@ static int solve_layered(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, i
     HIPCHK(c, hipMemcpyAsync(f->h_q, f->qctl.p, kQueueCtlBytes, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipMemcpyAsync(f->h_visits, (void*)f->a.visits, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));
-    const unsigned err = f->h_q[192 / 4];
+    err = f->h_q[192 / 4];
+    if (!(err & 4u) || (err & 3u)) break;
+    }
     if (err & 1u)
         return set_err(c, EIK_ERR_HIP, "layered solver: a queue wait exceeded %.1f s (EIK_OPT_QTIMEOUT)", c->qtimeout_s);
     if (err & 2u)

@@ -401,11 +401,11 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
     const int kPasses = COH ? a.max_passes : 1;
     unsigned dirs = L.dirs;  // this pass's sweeps (register: see fim2d.hip process_tile)
     int act_tile = -1;       // EIK_ACT_SPLIT_L: this lane's activation issued at the last pass boundary
-    unsigned act_old = 0u, act_kold = 0u;
-    float act_k = 0.f;  // (keys: priority mode only, not used by the layered solver)
+    unsigned act_old = 0u, act_kold = 0x7f800000u;
+    float act_k = 0.f;  // priority mode: the activation's key and the neighbour's key before it
     for (int pass = 0;; ++pass) {
         if (EIK_ACT_SPLIT_L && act_tile >= 0) {  // wave 0 lanes 1..4, as its sweep starts (fim2d.hip)
-            qpush_complete(a, act_tile, act_old);
+            qpush_complete(a, act_tile, act_old, act_k, act_kold);
             act_tile = -1;
         }
         if ((dirs >> wave) & 1u) {
@@ -415,8 +415,10 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
             else                sweep_layered<R, TH, NL, -1, -1>(Ts, lane);
         }
         __syncthreads();
-        // ---- write back changed cells, collect side flags
+        // ---- write back changed cells, collect side flags (priority bands: and the entering keys,
+        // the smallest improved value per side and overall, as fim2d.hip's write-back)
         unsigned fl = 0;
+        R kmin_self = INF, kmin[4] = {INF, INF, INF, INF};
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             const int ry = wave + 4 * j;
@@ -430,16 +432,23 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
                 if (in && nv < told[j][z]) T.st(gi + z * lzs, nv);
                 if (nv < told[j][z] * R(keep)) {
                     fl |= 128u;
+                    kmin_self = min_nn(kmin_self, nv);
                     // a neighbour can improve only if this edge value undercuts its adjacent cell
-                    if (ry == 0 && nv < Ts[lane + 1].get(z)) fl |= 1u;
-                    if (ry == TH - 1 && nv < Ts[(TH + 1) * kLds + lane + 1].get(z)) fl |= 2u;
-                    if (lane == 0 && nv < Ts[(ry + 1) * kLds].get(z)) fl |= 4u;
-                    if (lane == kTile - 1 && nv < Ts[(ry + 1) * kLds + kLds - 1].get(z)) fl |= 8u;
+                    if (ry == 0 && nv < Ts[lane + 1].get(z)) { fl |= 1u; kmin[0] = min_nn(kmin[0], nv); }
+                    if (ry == TH - 1 && nv < Ts[(TH + 1) * kLds + lane + 1].get(z)) { fl |= 2u; kmin[1] = min_nn(kmin[1], nv); }
+                    if (lane == 0 && nv < Ts[(ry + 1) * kLds].get(z)) { fl |= 4u; kmin[2] = min_nn(kmin[2], nv); }
+                    if (lane == kTile - 1 && nv < Ts[(ry + 1) * kLds + kLds - 1].get(z)) { fl |= 8u; kmin[3] = min_nn(kmin[3], nv); }
                 }
                 told[j][z] = nv;  // what memory holds now
             }
         }
         if (fl) atomicOr(&L.flags, fl);
+        if (a.bctl) {  // priority bands: the entering keys (f32 bits: T >= 0)
+            if (kmin_self < INF) atomicMin(&L.key[0], __float_as_uint((float)kmin_self));
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (kmin[q] < INF) atomicMin(&L.key[q + 1], __float_as_uint((float)kmin[q]));
+        }
         if constexpr (COH) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
         __syncthreads();
         const unsigned f = L.flags;  // uniform
@@ -480,7 +489,10 @@ __global__ __launch_bounds__(kThreads) void fim2dl_persist_kernel(Fim2dArgs a) {
             if (tile >= 0) {
                 const unsigned f = L.flags;
                 activate_neighbours(a, tile, f, L.key, 0, 0u);
-                if (threadIdx.x == 0 && (f & 128u)) atomicOr(&a.qstate[tile], kPending | kSelf);
+                if (threadIdx.x == 0 && (f & 128u)) {
+                    if (a.bctl) atomicMin(&a.key[tile], 0u);  // priority mode: a self re-queue goes first
+                    atomicOr(&a.qstate[tile], kPending | kSelf);
+                }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (threadIdx.x == 0) {
                     qfinish(a, tile);
@@ -490,12 +502,15 @@ __global__ __launch_bounds__(kThreads) void fim2dl_persist_kernel(Fim2dArgs a) {
                     }
                 }
             }
-        } else if (threadIdx.x == 64) {
+        } else if (threadIdx.x < 128 && (a.bctl || threadIdx.x == 64)) {
+            // wave 1 takes the next tile (priority bands: the whole wave; else lane 64)
             unsigned trig = 0;
-            const int t = qgrab(a, trig);
-            L.tile = t;
-            L.dirs = sweep_dirs(trig);
-            L.fresh = !(trig & kVisited);
+            const int t = a.bctl ? qgrab_prio(a, trig) : qgrab(a, trig);
+            if (threadIdx.x == 64) {
+                L.tile = t;
+                L.dirs = sweep_dirs(trig);
+                L.fresh = !(trig & kVisited);
+            }
         }
         __syncthreads();
         tile = __builtin_amdgcn_readfirstlane(L.tile);

@@ -136,6 +136,31 @@ def ctx_volume():
     c.close()
 
 
+@pytest.mark.parametrize("opts", [{"PRIO": 0.0}, {"PRIO": 1.0}, {"PRIO": 0.05}, {"PRIO": 1.0, "LAYER_PLANAR": 0},
+                                  {"PRIO": 1.0, "PRIO_RING": 8}])
+@pytest.mark.parametrize("shape,seed,pad,switch", [((300, 257, 3), 15, False, True), ((90, 140, 3), 14, True, True),
+                                                     ((64, 64, 4), 13, False, True)])
+def test_layered_priority_bands(shape, seed, pad, switch, opts):
+    """EIK_OPT_PRIO on the layered solver (fim2dl.hip: the entering keys of the write-back, the
+    whole-wave band grab): a different visit order, the same fields against the oracle in both dtypes,
+    incl. bands a few cells wide, the volume layout and a ring forced to overflow (qerror bit 4: the
+    solve runs again on the FIFO, no error raised)."""
+    import eikonal
+
+    c, goal = _layered_case(shape, seed, pad, switch)
+    O.set_strict(False)
+    try:
+        R = O.fmm3d(c, goal, None)
+    finally:
+        O.set_strict(True)
+    cx = eikonal.Context(0, options=opts)
+    try:
+        for f64 in (False, True):
+            check(cx.tmap3d(c, goal, dtype=np.float64 if f64 else np.float32), R, f64)
+    finally:
+        cx.close()
+
+
 @pytest.mark.parametrize("shape,seed,pad,switch", [((130, 150, 2), 11, False, True), ((90, 140, 3), 14, True, True),
                                                      ((300, 257, 3), 15, False, True), ((70, 65, 1), 16, False, False),
                                                      ((5, 3, 2), 42, False, False), ((39, 65, 3), 43, True, False)])
