@@ -142,12 +142,13 @@ struct eik_ctx {
     int sched = 1;               // EIK_OPT_SCHED: in-place scheduling of persistent visits
     int live_pack = 0;           // EIK_OPT_LIVE_PACK: the halo agent packs only idle tiles' edges
     // EIK_OPT_PRIO: the priority bands' width in units of 64 x the cost's geometric mean (0: the
-    // plain FIFO; < 0, the default: 1 in fp64, 0 in fp32).  fp64 at 1: C2 2.44-2.50 -> 2.37 ms, C4 at
+    // plain FIFO; < 0, the default: default_prio() in fp64 and on the layered solver, 0 in fp32 2D;
+    // round 5's first default was 1 in fp64).  fp64 at 1: C2 2.44-2.50 -> 2.37 ms, C4 at
     // one GPU 10.5 -> 13.8 Gcells/s; 0.5 / 2 lose on C4 (6.9 / 12.9; profiles/r05i_prio_ab.log).  fp32
     // solves are twice as fast per pass and the one-dispatcher bands held them back: C2 fp32 1.6 ->
     // 1.9 ms, C4 fp32 18.7 -> 10.8 Gcells/s (profiles/r05j_bench.json).  Batches of > 2 maps: FIFO.
-    // The layered solver's default (both dtypes) is kLayeredPrio: C5 fp64 1.92 -> 3.65, fp32 4.73 ->
-    // 6.2 Gcells/s (profiles/r05ac_layered_prio_ab.json.log, r05ad_prio_width_ab.log).
+    // The layered solver's bands (both dtypes, default_prio()): C5 fp64 1.92 -> 3.65, fp32 4.73 -> 6.2
+    // Gcells/s (profiles/r05ac_layered_prio_ab.json.log, r05ad_prio_width_ab.json.log).
     double prio = -1.0;
     int prio_ring = 0;           // EIK_OPT_PRIO_RING: slots per priority band (0: pow2 >= 2 x the tiles)
     int prio_dispatch = 0;       // EIK_OPT_PRIO_DISPATCH: band entries per dispatch (0: 64 on maps of >= kWideTiles, else 16)
@@ -415,6 +416,18 @@ int eik_get_stats(const eik_ctx* c, eik_stats* out) {
 
 // ------------------------------------------------------------------------------ fim2d
 // th: tile rows (64; the fp64 layered solver's tiles have fim2dl_rows(true) = 40)
+// The default priority-band width (EIK_OPT_PRIO < 0; fp64 2D solves and the layered solver): 0.25 on
+// a 4096^2 raster, growing with the raster's side -- the front's T range grows with it, and bands too
+// narrow for it leave the queue to the open-ended last band.  Band-width A/B, 0.25 / 0.5 / 1:
+//   C2 4096^2 fp64 2.14-2.16 / 2.15-2.19 / 2.17-2.20 ms; C4 16384^2 fp64 3.9-4.0 / 9.0-9.1 / 16.3-16.7
+//   Gcells/s (profiles/r05ad_prio_width_ab.json.log, r05ae_c4_width_ab.json.log);
+//   layered (C5's volume, tools/layered_scale_probe.py) fp64 4096^2 3.79 / 3.75 / 3.61, 8192^2 4.16 /
+//   4.33 / 4.19, 16384^2 1.65 / 3.95 / 4.30; fp32 6.80 / 6.83 / 6.79, 7.78 / 8.02 / 7.86, 4.84 / 8.13 /
+//   8.50 Gcells/s (the FIFO: fp64 2.89, 1.77, 1.29; fp32 6.63, 4.62, 3.11; profiles/r05af_*, r05ah_*).
+static double default_prio(int64_t H, int64_t W) {
+    return 0.25 * std::max(1.0, std::sqrt((double)H * (double)W) / 4096.0);
+}
+
 static int fim2d_create_rows(eik_ctx* c, int64_t B, int64_t H, int64_t W, int dtype, int th, eik_fim2d** out) {
     if (!c || !out) return EIK_ERR_ARG;
     *out = nullptr;
@@ -566,7 +579,7 @@ int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
     // with the queue before the seed kernel pushes the goal's tile
     f->a.bctl = nullptr;
     // (one map or a few: a batch of independent maps keeps the FIFO -- their keys do not compare)
-    const double prio = c->prio < 0 ? (f->f64 ? 1.0 : 0.0) : c->prio;
+    const double prio = c->prio < 0 ? (f->f64 ? default_prio(f->H, f->W) : 0.0) : c->prio;
     if (prio > 0 && f->a.mode == kModePersistent && f->B <= 2 && !f->no_bands) {
         uint64_t bc = 1024;
         while (bc < 2 * (uint64_t)f->a.capacity) bc <<= 1;
@@ -1422,9 +1435,6 @@ int eik_path2d_f64(eik_ctx* c, const double* T, int64_t H, int64_t W, const doub
 // ------------------------------------------------------------------------------ 3D
 // Few-layer fp32 volumes (the rover's (x, y, mode) costmaps) on the layered 2D-tile solver:
 // layers z0 .. z0+nl-1 of a [H][W][L] volume, one persistent launch.
-// the layered solver's default band width (EIK_OPT_PRIO < 0): C5 A/B 0.125 / 0.25 / 0.5 / 1 = fp64 3.61 /
-// 3.65 / 3.58 / 3.40, fp32 6.20 / 6.22 / 6.21 / 6.07 Gcells/s, FIFO 1.92 / 4.73 (profiles/r05ad_prio_width_ab.log)
-constexpr double kLayeredPrio = 0.25;
 static int solve_layered(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, int64_t W, int64_t L, int z0, int nl,
                          const int64_t goal[3], int dtype, hipStream_t st) {
     const bool f64 = dtype == EIK_F64;
@@ -1479,7 +1489,7 @@ static int solve_layered(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, i
     if (planar) HIPCHK(c, layer_planar(d_cost, c->lp_cost.p, f64, H * W, L, z0, nl, true, st));
     // priority bands (fim_engine.hpp), as eik_fim2d_start sets them up: on an explicit EIK_OPT_PRIO
     a.bctl = nullptr;
-    const double prio = c->prio < 0 ? kLayeredPrio : c->prio;
+    const double prio = c->prio < 0 ? default_prio(H, W) : c->prio;
     if (prio > 0 && attempt == 0) {
         uint64_t bc = 1024;
         while (bc < 2 * (uint64_t)a.capacity) bc <<= 1;
@@ -1735,8 +1745,9 @@ static int fim3d_solve_one(eik_ctx* c, const void* d_cost, void* d_T, int64_t H,
     const int64_t esz = dtype == EIK_F64 ? 8 : 4;
     // (an fp64 early-exit solve stays on fim3d.hip: its solve3_ref keeps the reference's exact ties,
     // which decide FM3D's closed set)
-    if (c->mode == kModePersistent && c->max_rounds == 1 && H * W * L * esz < (int64_t)UINT32_MAX &&
-        !(stop_off >= 0 && dtype == EIK_F64)) {
+    // (the layered kernel addresses T per tile and layer: (rows + 2) x W x L elements under 4 GiB)
+    if (c->mode == kModePersistent && c->max_rounds == 1 &&
+        (fim2dl_rows(dtype == EIK_F64) + 2) * W * L * esz < (int64_t)UINT32_MAX && !(stop_off >= 0 && dtype == EIK_F64)) {
         int z0 = 0, nl = 0;
         int rc = layered_plan(c, d_cost, H, W, L, dtype, st, &z0, &nl);
         if (rc) return rc;

@@ -284,8 +284,18 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
     // lzs = 1) or its layer-planar copy (ls = 1, z0 = 0, lzs = H * W; solve_layered)
     const int64_t ls = a.ls, lzs = a.lzs, plane = a.H * a.W * (lzs > 1 ? NL : ls);
     const R* __restrict__ cost = static_cast<const R*>(a.cost) + map * plane;
-    const TMem<R, COH> T(static_cast<R*>(a.T) + map * plane, plane);
     const int64_t y0 = (int64_t)ty * TH, x0 = (int64_t)tx * kTile;
+    // T through one buffer resource per solved layer, based at the tile's first halo row: T[i + z *
+    // lzs] is Tz[z] at i - b0, and a resource's 32-bit offsets span the TH + 2 rows of one layer the
+    // visit touches, whatever the volume's size.  (One resource over the whole T capped the layered
+    // solver at 4 GiB: a 16384^2 x 5 fp32 volume went to fim3d.hip at 0.3 Gcells/s,
+    // tools/layered_scale_probe.py.)  Indices of out-of-range cells (0, selected away) wrap to
+    // offsets past the range: the buffer returns 0 for them.
+    const int64_t b0 = (y0 > 0 ? (y0 - 1) * a.W : 0) * ls + a.z0;
+    const int64_t span = (TH + 2) * a.W * ls;
+    TMem<R, COH> Tz[NL];
+#pragma unroll
+    for (int z = 0; z < NL; ++z) Tz[z] = TMem<R, COH>(static_cast<R*>(a.T) + map * plane + b0 + z * lzs, span);
 
     if (tid == 0) L.flags = 0;
     if (tid < 5) L.key[tid] = 0x7f800000u;
@@ -315,7 +325,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
     auto load_halo = [&]() {  // unconditional loads (an in-range index), then the +inf select
         R v[4] = {INF, INF, INF, INF};
 #pragma unroll
-        for (int z = 0; z < NL; ++z) v[z] = T.ld(hgi + z * lzs);
+        for (int z = 0; z < NL; ++z) v[z] = Tz[z].ld(hgi - b0);
 #pragma unroll
         for (int z = 0; z < NL; ++z) v[z] = hin ? v[z] : (hg ? hg[hgo + z] : INF);
         return LCell<R>::make(v);
@@ -364,7 +374,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
             const int64_t gi = ((y0 + wave + 4 * j) * a.W + x0 + lane) * ls + a.z0;
 #pragma unroll
             for (int z = 0; z < NL; ++z) {
-                told[j][z] = T.ld(gi + z * lzs);
+                told[j][z] = Tz[z].ld(gi - b0);
                 cc[j][z] = scost(cost[gi + z * lzs]);
             }
         }
@@ -383,7 +393,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
             const int64_t go = (gy == a.H ? gx : gy) * NL;
 #pragma unroll
             for (int z = 0; z < NL; ++z) {
-                const R t = T.ld(gi + z * lzs), c = cost[gi + z * lzs];
+                const R t = Tz[z].ld(gi - b0), c = cost[gi + z * lzs];
                 told[j][z] = in ? t : (gc ? gc[go + z] : INF);
                 cc[j][z] = in ? scost(c) : INF;
             }
@@ -429,7 +439,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
 #pragma unroll
             for (int z = 0; z < NL; ++z) {
                 const R nv = nv4.get(z);
-                if (in && nv < told[j][z]) T.st(gi + z * lzs, nv);
+                if (in && nv < told[j][z]) Tz[z].st(gi - b0, nv);
                 if (nv < told[j][z] * R(keep)) {
                     fl |= 128u;
                     kmin_self = min_nn(kmin_self, nv);

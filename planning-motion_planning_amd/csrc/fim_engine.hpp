@@ -59,6 +59,7 @@ struct TMem;
 template <typename R>
 struct TMem<R, false> {
     R* p;
+    TMem() = default;
     __device__ TMem(R* base, int64_t) : p(base) {}
     __device__ R ld(int64_t i) const { return p[i]; }
     __device__ void ld4(int64_t i, R (&v)[4]) const {
@@ -89,7 +90,9 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 template <typename R>
 struct TMem<R, true> {
     __amdgpu_buffer_rsrc_t rs;
-    // n * sizeof(R) < 2^32 is checked by the host before it selects this mode
+    // n * sizeof(R) < 2^32 is checked by the host before it selects this mode (fim2dl.hip: one
+    // resource per layer and tile)
+    TMem() = default;
     __device__ TMem(R* base, int64_t n)
         : rs(__builtin_amdgcn_make_buffer_rsrc(base, 0, (int)(uint32_t)(n * (int64_t)sizeof(R)), 0x00020000)) {}
     __device__ R ld(int64_t i) const {

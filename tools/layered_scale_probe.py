@@ -17,13 +17,15 @@ dev = torch.device("cuda", 0)
 stream = torch.cuda.current_stream(dev)
 widths = os.environ.get("WIDTHS", "0,0.25,0.5,1,2").split(",")
 for N in sizes:
-    cost = terrain.cost_block(0, 0, N, N, N, N, seed=7, device=dev).to(tdt).contiguous()
+    seed = int(os.environ.get("SEED", "7"))
+    cost = terrain.cost_block(0, 0, N, N, N, N, seed=seed, device=dev).to(tdt).contiguous()
     goal = (N // 2, N // 2)
     for w in widths:
         ctx = eikonal.Context(0, options={"PRIO": float(w)})
         try:
             r = bench.bench_layers(ctx, dev, stream, cost, goal, 3)
-            print(f"{dt} N={N} PRIO={w}: {r['value']} Gcells/s {r['ms_per_step']} ms vis {r.get('tile_visits_per_solve')}",
+            print(f"{dt} N={N} PRIO={w}: {r['value']} Gcells/s {r['ms_per_step']} ms vis {r.get('tile_visits_per_solve')} "
+                  f"inpl {r['roofline'].get('inplace_passes_per_solve')} reach {r['reached_fraction']} seed {seed}",
                   flush=True)
         finally:
             ctx.close()
