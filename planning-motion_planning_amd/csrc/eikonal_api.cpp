@@ -1508,7 +1508,9 @@ static int solve_layered(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, i
         float* pd = (float*)((char*)f->bctl.p + 128 * kBands);
         HIPCHK(c, fim2d_prio_delta(a.cost, f64, planar ? (int64_t)nl * H * W : H * W * L, (float)prio, pd, st));
         a.pdelta = pd;
-        a.disp = c->prio_dispatch > 0 ? (unsigned)c->prio_dispatch : a.tiles_per_map >= kWideTiles ? 64u : 16u;
+        // the dispatch batch: 32 below kWideTiles tiles (C5 16 / 32 / 48 / 64: fp64 3.61 / 3.67-3.69 / 3.65 /
+        // 3.58, fp32 6.30-6.33 / 6.37-6.38 / 6.27 / 6.08-6.12 Gcells/s, profiles/r05ak_layered_dispatch_ab.json.log)
+        a.disp = c->prio_dispatch > 0 ? (unsigned)c->prio_dispatch : a.tiles_per_map >= kWideTiles ? 64u : 32u;
     }
     HIPCHK(c, fim2dl_init(a, f64, goal[0], goal[1], goal[2] - z0, nT, st));
     HIPCHK(c, fim2dl_persist(a, nl, f64, grid, st));
