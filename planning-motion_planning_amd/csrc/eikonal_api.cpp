@@ -148,7 +148,7 @@ struct eik_ctx {
     // solves are twice as fast per pass and the one-dispatcher bands held them back: C2 fp32 1.6 ->
     // 1.9 ms, C4 fp32 18.7 -> 10.8 Gcells/s (profiles/r05j_bench.json).  Batches of > 2 maps: FIFO.
     // The layered solver's bands (both dtypes, default_prio()): C5 fp64 1.92 -> 3.65, fp32 4.73 -> 6.2
-    // Gcells/s (profiles/r05ac_layered_prio_ab.json.log, r05ad_prio_width_ab.json.log).
+    // Gcells/s (profiles/r05ac_layered_prio_ab.log, r05ad_prio_width_ab.log).
     double prio = -1.0;
     int prio_ring = 0;           // EIK_OPT_PRIO_RING: slots per priority band (0: pow2 >= 2 x the tiles)
     int prio_dispatch = 0;       // EIK_OPT_PRIO_DISPATCH: band entries per dispatch (0: 64 on maps of >= kWideTiles, else 16)
@@ -420,7 +420,7 @@ int eik_get_stats(const eik_ctx* c, eik_stats* out) {
 // a 4096^2 raster, growing with the raster's side -- the front's T range grows with it, and bands too
 // narrow for it leave the queue to the open-ended last band.  Band-width A/B, 0.25 / 0.5 / 1:
 //   C2 4096^2 fp64 2.14-2.16 / 2.15-2.19 / 2.17-2.20 ms; C4 16384^2 fp64 3.9-4.0 / 9.0-9.1 / 16.3-16.7
-//   Gcells/s (profiles/r05ad_prio_width_ab.json.log, r05ae_c4_width_ab.json.log);
+//   Gcells/s (profiles/r05ad_prio_width_ab.log, r05ae_c4_width_ab.log);
 //   layered (C5's volume, tools/layered_scale_probe.py) fp64 4096^2 3.79 / 3.75 / 3.61, 8192^2 4.16 /
 //   4.33 / 4.19, 16384^2 1.65 / 3.95 / 4.30; fp32 6.80 / 6.83 / 6.79, 7.78 / 8.02 / 7.86, 4.84 / 8.13 /
 //   8.50 Gcells/s (the FIFO: fp64 2.89, 1.77, 1.29; fp32 6.63, 4.62, 3.11; profiles/r05af_*, r05ah_*).
@@ -1509,7 +1509,7 @@ static int solve_layered(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, i
         HIPCHK(c, fim2d_prio_delta(a.cost, f64, planar ? (int64_t)nl * H * W : H * W * L, (float)prio, pd, st));
         a.pdelta = pd;
         // the dispatch batch: 32 below kWideTiles tiles (C5 16 / 32 / 48 / 64: fp64 3.61 / 3.67-3.69 / 3.65 /
-        // 3.58, fp32 6.30-6.33 / 6.37-6.38 / 6.27 / 6.08-6.12 Gcells/s, profiles/r05ak_layered_dispatch_ab.json.log)
+        // 3.58, fp32 6.30-6.33 / 6.37-6.38 / 6.27 / 6.08-6.12 Gcells/s, profiles/r05ak_layered_dispatch_ab.log)
         a.disp = c->prio_dispatch > 0 ? (unsigned)c->prio_dispatch : a.tiles_per_map >= kWideTiles ? 64u : 32u;
     }
     HIPCHK(c, fim2dl_init(a, f64, goal[0], goal[1], goal[2] - z0, nT, st));
