@@ -111,10 +111,12 @@ typedef enum {
                                 of tiles that are neither pending nor busy (converged edges), so a
                                 neighbour is not re-activated by every intermediate refinement
                                 (a round whose snapshot had no tile pending or busy packs all)   */
-    EIK_OPT_PRIO = 15,       /* 2D persistent solves of one or two maps: v > 0 serves waiting tiles
-                                lowest entering T first, in 64 bands of width v x 64 x the geometric
-                                mean of the finite costs (fim_engine.hpp "priority bands"); 0 =
-                                the FIFO; < 0 (default) = 1 for fp64 solves, 0 for fp32          */
+    EIK_OPT_PRIO = 15,       /* 2D persistent solves of one or two maps and the layered 3D solver:
+                                v > 0 serves waiting tiles lowest entering T first, in 64 bands of
+                                width v x 64 x the geometric mean of the finite costs
+                                (fim_engine.hpp "priority bands"); 0 = the FIFO; < 0 (default) =
+                                0.25 x max(1, sqrt(H W) / 4096) for fp64 2D solves and layered
+                                solves of either dtype, the FIFO for fp32 2D solves               */
     EIK_OPT_LAYER_PLANAR = 16, /* few-layer 3D volumes (the layered solver): 1 (default) solves on
                                 layer-planar copies [nl][H][W] of the solved layers (one copy in,
                                 one out per solve; every tile-row access one contiguous run per
