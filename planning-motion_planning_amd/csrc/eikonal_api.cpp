@@ -424,8 +424,16 @@ int eik_get_stats(const eik_ctx* c, eik_stats* out) {
 //   layered (C5's volume, tools/layered_scale_probe.py) fp64 4096^2 3.79 / 3.75 / 3.61, 8192^2 4.16 /
 //   4.33 / 4.19, 16384^2 1.65 / 3.95 / 4.30; fp32 6.80 / 6.83 / 6.79, 7.78 / 8.02 / 7.86, 4.84 / 8.13 /
 //   8.50 Gcells/s (the FIFO: fp64 2.89, 1.77, 1.29; fp32 6.63, 4.62, 3.11; profiles/r05af_*, r05ah_*).
-static double default_prio(int64_t H, int64_t W) {
-    return 0.25 * std::max(1.0, std::sqrt((double)H * (double)W) / 4096.0);
+// Below a side of min_side the FIFO is the default: the bands' dispatch latency outweighs the order on
+// small rasters.  fp64 2D FIFO vs bands (0.25), ms: 1024^2 0.48 / 0.57, 2048^2 0.79 / 0.92, 2560^2 1.06 /
+// 1.20, 3072^2 1.22 / 1.37, 3584^2 1.43 / 1.58, the C4 DEM at 4096^2 1.79 / 1.85 but C2's raster 2.35 /
+// 2.15 (profiles/r05an_prio_size_2d.log, r05ao_prio_crossover.log, r05ap_c2_prio_vs_fifo_ab.log): 2D
+// min_side 4096.  Layered (C5's volume) fp64 / fp32 FIFO vs bands, ms: 1024^2 2.34 / 2.55, 1.55 / 1.70;
+// 2048^2 4.37 / 4.46, 2.61 / 2.86; 3072^2 8.49 / 7.75, 4.29 / 4.35: layered min_side 3072.
+static double default_prio(int64_t H, int64_t W, double min_side) {
+    const double side = std::sqrt((double)H * (double)W);
+    if (side < min_side) return 0.0;
+    return 0.25 * std::max(1.0, side / 4096.0);
 }
 
 static int fim2d_create_rows(eik_ctx* c, int64_t B, int64_t H, int64_t W, int dtype, int th, eik_fim2d** out) {
@@ -579,7 +587,10 @@ int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
     // with the queue before the seed kernel pushes the goal's tile
     f->a.bctl = nullptr;
     // (one map or a few: a batch of independent maps keeps the FIFO -- their keys do not compare)
-    const double prio = c->prio < 0 ? (f->f64 ? default_prio(f->H, f->W) : 0.0) : c->prio;
+    // (a domain-decomposition block -- ghost strips bound -- keeps the bands at any size: they order
+    // the ghosts' arrivals, the 4 x 2 rehearsal's work 3.7x -> 0.96x the single domain's, §6)
+    const bool dd_block = f->a.ghost[0] || f->a.ghost[1] || f->a.ghost[2] || f->a.ghost[3];
+    const double prio = c->prio < 0 ? (f->f64 ? default_prio(f->H, f->W, dd_block ? 0.0 : 4096.0) : 0.0) : c->prio;
     if (prio > 0 && f->a.mode == kModePersistent && f->B <= 2 && !f->no_bands) {
         uint64_t bc = 1024;
         while (bc < 2 * (uint64_t)f->a.capacity) bc <<= 1;
@@ -1489,7 +1500,7 @@ static int solve_layered(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, i
     if (planar) HIPCHK(c, layer_planar(d_cost, c->lp_cost.p, f64, H * W, L, z0, nl, true, st));
     // priority bands (fim_engine.hpp), as eik_fim2d_start sets them up: on an explicit EIK_OPT_PRIO
     a.bctl = nullptr;
-    const double prio = c->prio < 0 ? default_prio(H, W) : c->prio;
+    const double prio = c->prio < 0 ? default_prio(H, W, 3072.0) : c->prio;
     if (prio > 0 && attempt == 0) {
         uint64_t bc = 1024;
         while (bc < 2 * (uint64_t)a.capacity) bc <<= 1;
