@@ -587,10 +587,15 @@ int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
     // with the queue before the seed kernel pushes the goal's tile
     f->a.bctl = nullptr;
     // (one map or a few: a batch of independent maps keeps the FIFO -- their keys do not compare)
-    // (a domain-decomposition block -- ghost strips bound -- keeps the bands at any size: they order
-    // the ghosts' arrivals, the 4 x 2 rehearsal's work 3.7x -> 0.96x the single domain's, §6)
+    // (a domain-decomposition block -- ghost strips bound -- keeps the bands at any size, at width >= 1:
+    // they order the ghosts' arrivals, whose T spans the whole raster's range, not the block's.  The
+    // 16384^2 4 x 2 rehearsal: FIFO 3.7x the single domain's visits, width 1 0.96x (22 ms), the
+    // block-sized 0.35 2.96x (61 ms), profiles/r05d_c4_rehearsal_n8_*.json, r05h_c4_rehearsal_n8.log)
     const bool dd_block = f->a.ghost[0] || f->a.ghost[1] || f->a.ghost[2] || f->a.ghost[3];
-    const double prio = c->prio < 0 ? (f->f64 ? default_prio(f->H, f->W, dd_block ? 0.0 : 4096.0) : 0.0) : c->prio;
+    const double prio = c->prio >= 0 ? c->prio
+                        : !f->f64  ? 0.0
+                        : dd_block ? std::max(1.0, default_prio(f->H, f->W, 0.0))
+                                   : default_prio(f->H, f->W, 4096.0);
     if (prio > 0 && f->a.mode == kModePersistent && f->B <= 2 && !f->no_bands) {
         uint64_t bc = 1024;
         while (bc < 2 * (uint64_t)f->a.capacity) bc <<= 1;
