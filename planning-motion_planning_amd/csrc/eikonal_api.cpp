@@ -597,8 +597,11 @@ int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
                         : dd_block ? std::max(1.0, default_prio(f->H, f->W, 0.0))
                                    : default_prio(f->H, f->W, 4096.0);
     if (prio > 0 && f->a.mode == kModePersistent && f->B <= 2 && !f->no_bands) {
+        // a decomposition block's launch lives through many halo rounds and has no FIFO re-solve to
+        // fall back on: stale entries of its many episodes get 16 x the tiles per band (a 4 x 2 live
+        // solve filled the 2 x ring once in a GPU suite run, profiles/r05as_tests.log)
         uint64_t bc = 1024;
-        while (bc < 2 * (uint64_t)f->a.capacity) bc <<= 1;
+        while (bc < (dd_block ? 16u : 2u) * (uint64_t)f->a.capacity) bc <<= 1;
         if (c->prio_ring > 0) {  // (tests: a small ring forces the overflow fallback)
             bc = 1;
             while (bc < (uint64_t)c->prio_ring) bc <<= 1;
@@ -703,6 +706,9 @@ int eik_fim3dl_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t 
     f->host_syncs = 0;
     f->sweep_ms = f->solve_ms = 0.0;
     HIPCHK(c, hipMemsetAsync((void*)a.visits, 0, 3 * sizeof(unsigned long long), f->stream));
+    // (the FIFO: priority bands on these blocks were measured slower -- 2048^2 x 3 in 2 x 2 blocks, fp64
+    // 99 -> 108 ms, fp32 40 -> 44 ms, the same visits; the relaunch schedule has no work inflation for
+    // them to remove, profiles/r05as_dd_layered_prio_probe.log)
     const bool in = goal[0] >= 0 && goal[1] >= 0 && goal[0] < f->W && goal[1] < f->H;
     if (in && (goal[2] < f->lz0 || goal[2] >= f->lz0 + f->lnl))
         return set_err(c, EIK_ERR_ARG, "goal layer %ld outside the solved layers", (long)goal[2]);
@@ -943,8 +949,12 @@ static int live_cmd(eik_fim2d* f, unsigned op, unsigned par) {
                 return set_err(c, EIK_ERR_HIP, "live solve: the halo agent did not answer within %.1f s", el);
             if (__atomic_load_n(&b->error, __ATOMIC_RELAXED) & 1u) break;
             // the launch ended early (fault, or every workgroup left): nothing will answer
-            if (hipStreamQuery(f->stream) == hipSuccess)
-                return set_err(c, EIK_ERR_HIP, "live solve: the persistent launch is no longer running");
+            if (hipStreamQuery(f->stream) == hipSuccess) {
+                unsigned qerr = 0;  // the queue's error word (bit 4: a priority band's ring filled)
+                (void)hipMemcpy(&qerr, (const char*)f->qctl.p + 192, sizeof qerr, hipMemcpyDeviceToHost);
+                return set_err(c, EIK_ERR_HIP, "live solve: the persistent launch is no longer running (queue error %u)",
+                               qerr);
+            }
         }
         __builtin_ia32_pause();
     }
