@@ -116,7 +116,7 @@ def main():
     ctx = eikonal.Context(local_rank, options=eikonal._lib.options_from_env())  # A/B hook, opt-in
     ctx.set_option(L.OPT_SYNC_EVERY, args.sync_every)
     if shared and world > 1:
-        ctx.set_option(L.OPT_GRID, max(2, 2 * torch.cuda.get_device_properties(dev).multi_processor_count // world))
+        ctx.set_option(L.OPT_GRID, max(2, 3 * torch.cuda.get_device_properties(dev).multi_processor_count // (2 * world)))
     fim = eikonal.Fim2d(ctx, 1, blk.h, blk.w, edt)
     lgoal = blk.local_goal(*goal_g)
 
@@ -143,26 +143,32 @@ def main():
         local = dd.GpuLocal(fim, ghost)
 
         dd_rounds = []
+        live_fail = {}  # a live solve that failed: its step index and error (then rounds for the rest)
+        nstep = [0]
 
         def step():
+            nonlocal dd_mode
+            nstep[0] += 1
             if dd_mode == "live":
-                live_local.start(cost, T, lgoal, stream.cuda_stream)
-                dd_rounds.append(dd.solve_live(live_local, blk, halo, group=ctrl, vote=vote))
-            else:
-                local.start(cost, T, lgoal, stream.cuda_stream)
-                dd_rounds.append(dd.solve(local, blk, send, recv, exchange_every=args.exchange_every))
+                try:
+                    live_local.start(cost, T, lgoal, stream.cuda_stream)
+                    dd_rounds.append(dd.solve_live(live_local, blk, halo, group=ctrl, vote=vote))
+                    return
+                except Exception as e:  # raised on every rank alike (dd.solve_live's error carry and
+                    # release vote): every rank takes the relaunch schedule from here on, this step too
+                    live_fail.update(step=nstep[0], error=repr(e)[:200])
+                    dd_mode = "rounds"
+                    ctx.set_option(L.OPT_QTIMEOUT, 30.0)
+                    torch.cuda.synchronize()
+            local.start(cost, T, lgoal, stream.cuda_stream)
+            dd_rounds.append(dd.solve(local, blk, send, recv, exchange_every=args.exchange_every))
     else:
         def step():
             fim.solve(cost.data_ptr(), T.data_ptr(), [lgoal], stream.cuda_stream)
 
     if dd_mode == "live":
         ctx.set_option(L.OPT_QTIMEOUT, 5.0)  # a stuck live round ends in an error, not a hang
-        try:
-            step()
-        except Exception as e:  # raised on every rank alike (dd.solve_live's error carry)
-            live_err = repr(e)
-            dd_mode = "rounds"
-            ctx.set_option(L.OPT_QTIMEOUT, 30.0)
+    step()  # (N > 1, live: a failure here falls back before the warmup)
     for _ in range(args.warmup):
         step()
 
@@ -298,16 +304,29 @@ def main():
         rr = dd_rounds[-args.steps:]
         out["config"]["dd_rounds_per_solve"] = round(sum(rr) / max(len(rr), 1), 1)
         out["config"]["dd_us_per_round"] = round(ms_per_step * 1e3 / max(sum(rr) / max(len(rr), 1), 1), 1)
-        if live_err:
+        if live_err:  # the live transport could not be set up: rounds from the start
             out["config"]["dd_live_error"] = live_err[:200]
+        if live_fail:  # a live solve failed at step k (1 = the first, untimed): rounds from there on
+            out["config"]["dd_live_error"] = live_fail["error"]
+            out["config"]["dd_live_failed_at_step"] = live_fail["step"]
+            out["config"]["dd_live_failed_in_timed_region"] = live_fail["step"] > 1 + args.warmup
 
     if rank == 0 and world == 1 and not args.no_path:
         out.update(ms_to_path(cost, ctx, fim, dev, stream, goal_g, edt))
 
-    if world > 1 and not args.no_extra:  # configs[2] sharded: 128 / N maps per rank, no collective
-        c3 = bench_batch(ctx, dev, stream, args.extra_steps, tdt, edt, rank=rank, world=world, group=ctrl)
+    if world > 1 and not args.no_extra:
+        del T
+        torch.cuda.empty_cache()
+        xs = {}
+        # configs[2] sharded: 128 / N maps per rank, no collective
+        xs["C3_sharded"] = bench_batch(ctx, dev, stream, args.extra_steps, tdt, edt, rank=rank, world=world, group=ctrl)
+        # configs[4] split in x-y: blocks of the layered volume, RCCL relaunch rounds
+        try:
+            xs["C5_split"] = bench_c5_split(ctx, dev, stream, args.extra_steps, tdt, edt, rank, world, ctrl, shared)
+        except Exception as e:  # report; the measured line stands
+            xs["C5_split"] = {"error": repr(e)[:200]}
         if rank == 0:
-            out["extra_configs"] = {"C3_sharded": c3}
+            out["extra_configs"] = xs
 
     if rank == 0 and world == 1 and not args.no_extra:
         del T
@@ -671,6 +690,105 @@ def bench_arm(ctx, steps, half=30, m=40, K=16, res=0.05):
             f"ms_{K}_single_fm3d": round(sec_s * 1e3, 3)}
 
 
+def c5_volume(c0, dev):
+    """configs[4]'s [H][W][5] volume from a 2D raster c0: mode 0 = c0, mode 1 = 1.6 x it and
+    impassable above cost 100, mode 2 = 0.8 x it with 1-in-5 impassable 64 x 64 blocks, between two
+    +inf padding layers (Coupled_motion_planner.py:355-356)."""
+    H, W = c0.shape
+    inf = torch.full_like(c0, float("inf"))
+    c1 = torch.where(c0 > 100, inf, 1.6 * c0)
+    yy = torch.arange(H, device=dev)[:, None] // 64
+    xx = torch.arange(W, device=dev)[None, :] // 64
+    c2 = torch.where(((yy + 2 * xx) % 5) == 0, inf, 0.8 * c0)
+    return torch.stack([inf, c0, c1, c2, inf], dim=-1).contiguous()
+
+
+def bench_c5_split(ctx, dev, stream, steps, tdt, edt, rank, world, group, shared, N=4096):
+    """SURVEY §8(e) "C5: split x-y only, layers stay together" at N > 1: configs[4]'s 4096 x 4096 x 3
+    volume (bench_layers' volume of the C2 raster) split into dd.SPLITS[world] blocks, one per rank,
+    each solved by the layered solver (eik_fim3dl_*) with ghost strips of 3 values per edge cell, on
+    the relaunch schedule (dd.solve: local solve to convergence, pack, RCCL batch_isend_irecv,
+    merge, all_reduce of the active count; the shared-GPU rehearsal stages the strips through host
+    memory over gloo).  A step = one solve of the whole volume; the time is the max over ranks.
+    Checked against the single-domain layered solve (eik_fim3d_solve) of the same volume on every
+    rank: masks equal and <= 1e-11 (fp64) / 1e-5 (fp32) relative (dd_field_ok), with every rank's
+    tile visits beside the single domain's."""
+    px, py = dd.SPLITS[world]
+    blk = dd.Block(N, N, px, py, rank)
+    vol = c5_volume(terrain.cost_block(0, 0, N, N, N, N, seed=42, device=dev).to(tdt), dev)
+    cb = vol[blk.y0:blk.y1, blk.x0:blk.x1].contiguous()
+    T = torch.empty_like(cb)
+    nl, Lm = 3, 5
+    fim = eikonal.Fim3dLayered(ctx, blk.h, blk.w, Lm, 1, nl, edt)
+    dsend, drecv, ghost = dd.make_strips(blk, tdt, dev, float("inf"), per_cell=nl)
+    loc = dd.GpuLocalLayered(fim, ghost)
+    if shared:  # gloo between processes on one GPU: host-staged strips
+        hsend, hrecv, _ = dd.make_strips(blk, tdt, "cpu", float("inf"), per_cell=nl)
+        drv, send, recv, cdev = dd.HostStaged(loc, dsend, drecv), hsend, hrecv, "cpu"
+    else:  # RCCL over xGMI, device strips
+        drv, send, recv, cdev = loc, dsend, drecv, None
+    lg = blk.local_goal(N // 2, N // 2)
+    goal = (lg[0], lg[1], 1)
+    rounds, vis, pas = [], [], []
+
+    def solve():
+        loc.start(cb, T, goal, stream.cuda_stream)
+        rounds.append(dd.solve(drv, blk, send, recv, exchange_every=1, count_device=cdev))
+        st = fim.stats()
+        vis.append(st["tile_visits"])
+        pas.append(st["inplace_passes"])
+
+    solve()  # warmup
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        solve()
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = time.perf_counter() - t0
+    tt = torch.tensor([el], dtype=torch.float64)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=group)
+    sec = tt.item() / steps
+    # the single-domain layered solve of the same volume (every rank its own; no gather)
+    Tf = torch.empty_like(vol)
+    g3 = np.array([N // 2, N // 2, 1], np.int64)
+    ctx._chk(L.lib().eik_fim3d_solve(ctx._h, vol.data_ptr(), Tf.data_ptr(), N, N, Lm, edt, g3, stream.cuda_stream))
+    torch.cuda.synchronize()
+    sd = ctx.stats()
+    ref = Tf[blk.y0:blk.y1, blk.x0:blk.x1, 1:1 + nl]
+    Tb = T[:, :, 1:1 + nl]
+    fin = torch.isfinite(ref)
+    if not torch.equal(fin, torch.isfinite(Tb)):
+        err = float("inf")
+    elif bool(fin.any()):
+        err = float(((Tb[fin].double() - ref[fin].double()).abs() / ref[fin].double().clamp(min=1e-30)).max())
+    else:
+        err = 0.0
+    mine = torch.tensor([err, float(np.mean(vis[1:])), float(np.mean(pas[1:])), float(np.mean(rounds[1:]))],
+                        dtype=torch.float64)
+    allr = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allr, mine, group=group)
+    pr = torch.stack(allr)
+    tol = 1e-11 if edt == L.EIK_F64 else 1e-5
+    fim.close()
+    del vol, cb, T, Tf
+    torch.cuda.empty_cache()
+    return {"workload": f"configs[4] split: {N}x{N}x3 layered costmap (bench_layers' volume, z padded to 5), "
+                        f"{px}x{py} x-y blocks over {world} GPUs, layers together; layered solver per block, "
+                        "relaunch schedule (" + ("host-staged gloo rehearsal" if shared else
+                                                 "RCCL batch_isend_irecv + all_reduce") + ")",
+            "dtype": "f64" if edt == L.EIK_F64 else "f32", "value": round(N * N * 3 / sec / 1e9, 4),
+            "unit": "Gcells/s", "ms_per_step": round(sec * 1e3, 4), "steps": steps,
+            "dd_field_ok": bool(float(pr[:, 0].max()) <= tol), "dd_field_max_rel": float(pr[:, 0].max()),
+            "dd_rounds_per_solve": round(float(pr[0, 3]), 1),
+            "dd_per_rank": {"tile_visits": [round(v, 1) for v in pr[:, 1].tolist()],
+                            "inplace_passes": [round(v, 1) for v in pr[:, 2].tolist()],
+                            "total_tile_visits": round(float(pr[:, 1].sum()), 1),
+                            "visits_vs_single_domain": round(float(pr[:, 1].sum()) / max(sd["tile_visits"], 1), 3)},
+            "single_domain_tile_visits": int(sd["tile_visits"])}
+
+
 def bench_layers(ctx, dev, stream, cost2d, goal, steps, Lz=3):
     """configs[4]: coupled (x, y, locomotion-mode) 4096 x 4096 x 3 costmap, [y][x][z] (FM3D
     layout), unit spacing between layers (FastMarching3D semantics): mode 0 = the C2 raster,
@@ -680,13 +798,7 @@ def bench_layers(ctx, dev, stream, cost2d, goal, steps, Lz=3):
     fim2dl.hip).  Solve from (goal, mode 0); then the FM3D path from (256, 256, mode 0).
     Gcells/s counts the 3 real layers."""
     H, W = cost2d.shape
-    c0 = cost2d
-    inf = torch.full_like(c0, float("inf"))
-    c1 = torch.where(c0 > 100, inf, 1.6 * c0)
-    yy = torch.arange(H, device=dev)[:, None] // 64
-    xx = torch.arange(W, device=dev)[None, :] // 64
-    c2 = torch.where(((yy + 2 * xx) % 5) == 0, inf, 0.8 * c0)
-    cost = torch.stack([inf, c0, c1, c2, inf], dim=-1).contiguous()
+    cost = c5_volume(cost2d, dev)
     T = torch.empty_like(cost)
     Lm = Lz + 2
     g3 = np.array([goal[0], goal[1], 1], np.int64)

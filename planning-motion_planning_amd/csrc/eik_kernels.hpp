@@ -50,7 +50,7 @@ struct Fim2dArgs {
     int z0;                // offset of the first solved layer in a cell (the volume: its index; planar: 0)
     int64_t lzs;           // layer stride: 1 in the [y][x][L] volume, H * W in a layer-planar copy
     // live domain decomposition (eik_fim2d_launch with live != 0): the persistent launch stays up
-    // -- its last workgroup is the halo agent serving the host's commands -- and ends when
+    // -- its workgroup 0 is the halo agent serving the host's commands -- and ends when
     // *qhold != 0
     unsigned* qhold;       // nullptr: end when no tile is pending or busy
     struct LiveBox* live;  // pinned host mailbox of the halo agent (live launches only)
@@ -59,6 +59,10 @@ struct Fim2dArgs {
     // (band = T / pdelta, the last band open-ended) and are taken lowest band first; nullptr bctl: off
     unsigned* bslot;            // [kBands][bmask + 1]: tile + 1, 0 = empty
     unsigned bmask;
+    // per tile: bit b set while an entry of the tile sits in band b's ring or on its way from there
+    // through the FIFO (fim_engine.hpp band_put): at most one entry per (tile, band), so a ring of
+    // >= tiles slots can never lap
+    unsigned long long* bmem;
     unsigned long long* bctl;   // band b: head at bctl[16 b], tail at bctl[16 b + 8] (own 64-B lines)
     const float* pdelta;        // band width in units of T (device word: prio_delta_kernel sets it per solve)
     unsigned disp;              // band entries moved per dispatch (fim_engine.hpp band_dispatch; 0: kDispatch)
@@ -84,6 +88,10 @@ constexpr int kModeList = 0, kModePersistent = 1;
 // grab -- with the in-place passes' atomics cost C2 ~20 %)
 constexpr size_t kQueueCtlBytes = 384;
 constexpr int kBands = 64;  // priority bands (EIK_OPT_PRIO): one band per lane of the grabbing wave
+// a FIFO entry moved there from band b carries b + 1 in its top bits (the claimer clears the tile's
+// band-membership bit); the low bits hold tile + 1
+constexpr unsigned kBandTagShift = 25;
+constexpr unsigned kSlotTileMask = (1u << kBandTagShift) - 1u;
 constexpr size_t kVisitsOff = 256;
 
 // T = inf, queue / list / visit / edge words cleared, goals seeded

@@ -436,6 +436,33 @@ static double default_prio(int64_t H, int64_t W, double min_side) {
     return 0.25 * std::max(1.0, side / 4096.0);
 }
 
+// Priority bands' buffers for a solve of `tiles` tiles (fim_engine.hpp): kBands rings of a power of
+// two >= 2 x the tiles (EIK_OPT_PRIO_RING: any power of two, tests), the per-tile band-membership
+// words (at most one entry per (tile, band): a ring of >= tiles slots cannot lap) and the head /
+// tail words, all cleared on the stream.  Fills a.bslot / bmask / bmem / bctl.  (The band-tagged
+// FIFO entries hold tile + 1 in kBandTagShift bits: bands need tiles < 2^25 - 1.)
+static hipError_t setup_bands(eik_ctx* c, DevBuf& bslot, DevBuf& bctl, int64_t tiles, Fim2dArgs& a, hipStream_t st) {
+    uint64_t bc = 1024;
+    while (bc < 2 * (uint64_t)tiles) bc <<= 1;
+    if (c->prio_ring > 0) {  // (tests: a ring below the tile count can lap -> qerror bit 4 -> FIFO re-solve)
+        bc = 1;
+        while (bc < (uint64_t)c->prio_ring) bc <<= 1;
+    }
+    const size_t ring_bytes = sizeof(unsigned) * kBands * bc;
+    const size_t mem_off = (ring_bytes + 255) & ~(size_t)255;
+    const size_t bytes = mem_off + sizeof(unsigned long long) * (size_t)tiles;
+    hipError_t e = bslot.ensure(bytes);
+    if (e == hipSuccess) e = bctl.ensure(128 * kBands + 128);  // + the band width's word
+    if (e == hipSuccess) e = hipMemsetAsync(bslot.p, 0, bytes, st);
+    if (e == hipSuccess) e = hipMemsetAsync(bctl.p, 0, 128 * kBands, st);
+    if (e != hipSuccess) return e;
+    a.bslot = (unsigned*)bslot.p;
+    a.bmask = (unsigned)(bc - 1);
+    a.bmem = (unsigned long long*)((char*)bslot.p + mem_off);
+    a.bctl = (unsigned long long*)bctl.p;
+    return hipSuccess;
+}
+
 static int fim2d_create_rows(eik_ctx* c, int64_t B, int64_t H, int64_t W, int dtype, int th, eik_fim2d** out) {
     if (!c || !out) return EIK_ERR_ARG;
     *out = nullptr;
@@ -596,23 +623,11 @@ int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
                         : !f->f64  ? 0.0
                         : dd_block ? std::max(1.0, default_prio(f->H, f->W, 0.0))
                                    : default_prio(f->H, f->W, 4096.0);
-    if (prio > 0 && f->a.mode == kModePersistent && f->B <= 2 && !f->no_bands) {
-        // a decomposition block's launch lives through many halo rounds and has no FIFO re-solve to
-        // fall back on: stale entries of its many episodes get 16 x the tiles per band (a 4 x 2 live
-        // solve filled the 2 x ring once in a GPU suite run, profiles/r05as_tests.log)
-        uint64_t bc = 1024;
-        while (bc < (dd_block ? 16u : 2u) * (uint64_t)f->a.capacity) bc <<= 1;
-        if (c->prio_ring > 0) {  // (tests: a small ring forces the overflow fallback)
-            bc = 1;
-            while (bc < (uint64_t)c->prio_ring) bc <<= 1;
-        }
-        HIPCHK(c, f->bslot.ensure(sizeof(unsigned) * kBands * bc));
-        HIPCHK(c, f->bctl.ensure(128 * kBands + 128));  // + the band width's word
-        HIPCHK(c, hipMemsetAsync(f->bslot.p, 0, sizeof(unsigned) * kBands * bc, f->stream));
-        HIPCHK(c, hipMemsetAsync(f->bctl.p, 0, 128 * kBands, f->stream));
-        f->a.bslot = (unsigned*)f->bslot.p;
-        f->a.bmask = (unsigned)(bc - 1);
-        f->a.bctl = (unsigned long long*)f->bctl.p;
+    if (prio > 0 && f->a.mode == kModePersistent && f->B <= 2 && !f->no_bands && f->a.capacity < (1 << kBandTagShift) - 1) {
+        // (a decomposition block's launch lives through many halo rounds: the band-membership bits
+        // bound every band to one entry per tile however many pending episodes its tiles go through;
+        // round 5 gave blocks 16 x the tiles per ring instead, which only moved the threshold)
+        HIPCHK(c, setup_bands(c, f->bslot, f->bctl, f->a.capacity, f->a, f->stream));
         float* pd = (float*)((char*)f->bctl.p + 128 * kBands);
         HIPCHK(c, fim2d_prio_delta(d_cost, f->f64, f->H * f->W, (float)prio, pd, f->stream));
         f->a.pdelta = pd;
@@ -671,6 +686,11 @@ int eik_fim3dl_create(eik_ctx* c, int64_t H, int64_t W, int64_t L, int z0, int n
     const int kmax = dtype == EIK_F64 ? 3 : 4;
     if (nl < 1 || nl > kmax || z0 < 0 || z0 + nl > L)
         return set_err(c, EIK_ERR_ARG, "layered block: nl=%d z0=%d L=%ld (nl <= %d)", nl, z0, (long)L, kmax);
+    // the layered kernel addresses T through one buffer resource per tile row band and layer: 32-bit
+    // byte offsets over (rows + 2) raster rows of W cells of L values (fim3d_solve_one's gate)
+    const int64_t esz = dtype == EIK_F64 ? 8 : 4;
+    if (W < 1 || L < 1 || (fim2dl_rows(dtype == EIK_F64) + 2) * W * L * esz >= (int64_t)UINT32_MAX)
+        return set_err(c, EIK_ERR_ARG, "layered block: a tile row band of W=%ld x L=%ld exceeds 4 GiB", (long)W, (long)L);
     const int rc = fim2d_create_rows(c, 1, H, W, dtype, fim2dl_rows(dtype == EIK_F64), out);
     if (rc) return rc;
     (*out)->lnl = nl;
@@ -950,10 +970,27 @@ static int live_cmd(eik_fim2d* f, unsigned op, unsigned par) {
             if (__atomic_load_n(&b->error, __ATOMIC_RELAXED) & 1u) break;
             // the launch ended early (fault, or every workgroup left): nothing will answer
             if (hipStreamQuery(f->stream) == hipSuccess) {
-                unsigned qerr = 0;  // the queue's error word (bit 4: a priority band's ring filled)
-                (void)hipMemcpy(&qerr, (const char*)f->qctl.p + 192, sizeof qerr, hipMemcpyDeviceToHost);
-                return set_err(c, EIK_ERR_HIP, "live solve: the persistent launch is no longer running (queue error %u)",
-                               qerr);
+                // the queue's words (error bits: 1 a wait timed out, 2 the visit budget, 4 a priority
+                // band's ring lapped), the visit counters and the fullest band (tail - head)
+                unsigned q[kQueueCtlBytes / 4] = {};
+                (void)hipMemcpy(q, f->qctl.p, kQueueCtlBytes, hipMemcpyDeviceToHost);
+                unsigned long long vis[2] = {};
+                memcpy(vis, (const char*)q + kVisitsOff, sizeof vis);
+                long long band_max = -1;
+                if (f->a.bctl) {
+                    std::vector<unsigned long long> bw(16 * kBands);
+                    if (hipMemcpy(bw.data(), f->a.bctl, 128 * kBands, hipMemcpyDeviceToHost) == hipSuccess)
+                        for (int b = 0; b < kBands; ++b)
+                            band_max = std::max(band_max, (long long)(bw[16 * b + 8] - bw[16 * b]));
+                }
+                unsigned long long qh = 0, qt = 0;
+                memcpy(&qh, q, 8);
+                memcpy(&qt, (const char*)q + 64, 8);
+                return set_err(c, EIK_ERR_HIP,
+                               "live solve: the persistent launch is no longer running (queue error %u, active %d, "
+                               "visits %llu, passes %llu, fifo head-tail %lld, fullest band %lld of %u slots)",
+                               q[192 / 4], (int)q[128 / 4], vis[0], vis[1], (long long)(qh - qt), band_max,
+                               f->a.bctl ? f->a.bmask + 1u : 0u);
             }
         }
         __builtin_ia32_pause();
@@ -1000,7 +1037,7 @@ int eik_fim2d_launch(eik_fim2d* f, int live) {
         }
         HIPCHK(c, hipEventRecord(f->ev_pool[f->ev_used++], f->stream));
     }
-    // live: the last workgroup is the halo agent; all must be co-resident (grid <= resident)
+    // live: workgroup 0 is the halo agent (dispatched first); the others should be co-resident (grid <= resident)
     const int g = std::max(live ? 2 : 1, std::min(grid, f->persist_grid));
     a.fresh_first = c->fresh_first;
     a.sched = c->sched;
@@ -1516,21 +1553,9 @@ static int solve_layered(eik_ctx* c, const void* d_cost, void* d_T, int64_t H, i
     // priority bands (fim_engine.hpp), as eik_fim2d_start sets them up: on an explicit EIK_OPT_PRIO
     a.bctl = nullptr;
     const double prio = c->prio < 0 ? default_prio(H, W, 3072.0) : c->prio;
-    if (prio > 0 && attempt == 0) {
-        uint64_t bc = 1024;
-        while (bc < 2 * (uint64_t)a.capacity) bc <<= 1;
-        if (c->prio_ring > 0) {  // (tests: a small ring forces the overflow fallback)
-            bc = 1;
-            while (bc < (uint64_t)c->prio_ring) bc <<= 1;
-        }
-        HIPCHK(c, f->bslot.ensure(sizeof(unsigned) * kBands * bc));
-        HIPCHK(c, f->bctl.ensure(128 * kBands + 128));
-        HIPCHK(c, hipMemsetAsync(f->bslot.p, 0, sizeof(unsigned) * kBands * bc, st));
-        HIPCHK(c, hipMemsetAsync(f->bctl.p, 0, 128 * kBands, st));
+    if (prio > 0 && attempt == 0 && a.capacity < (1 << kBandTagShift) - 1) {
+        HIPCHK(c, setup_bands(c, f->bslot, f->bctl, a.capacity, a, st));
         HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)a.key, 0x7f800000u, (size_t)a.capacity, st));  // keys: +inf
-        a.bslot = (unsigned*)f->bslot.p;
-        a.bmask = (unsigned)(bc - 1);
-        a.bctl = (unsigned long long*)f->bctl.p;
         float* pd = (float*)((char*)f->bctl.p + 128 * kBands);
         HIPCHK(c, fim2d_prio_delta(a.cost, f64, planar ? (int64_t)nl * H * W : H * W * L, (float)prio, pd, st));
         a.pdelta = pd;

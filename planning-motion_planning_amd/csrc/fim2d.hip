@@ -710,13 +710,52 @@ __global__ __launch_bounds__(kThreads) void fim2d_sweep_kernel(Fim2dArgs a) {
     }
 }
 
-// Live DD halo agent: the last workgroup of a live launch.  It serves the host's mailbox while
+// Min-merge of 64 received strip cells (one wave, all lanes: cell i, valid when i < len) into a
+// ghost strip: every cell that drops is stored (made visible, agent scope) and the edge tile beside
+// the wave's cells is activated ONCE, with the smallest dropped value as its key -- the wave's 64
+// cells are one 64-aligned run, i.e. one tile's edge.  (Round 5 queued one activation per dropped
+// cell; on the priority bands each could add a decrease-key entry.)  `count`: dropped cells are
+// added there (nullable).
+template <typename R>
+__device__ __forceinline__ void merge_strip_cells(const Fim2dArgs& a, int side, const R* rv, R* g, int64_t i,
+                                                  int64_t len, unsigned* count) {
+    R v = Real<R>::inf();
+    bool drop = false;
+    if (i < len) {
+        v = ld_system(rv + i);
+        drop = v < ld_agent(g + i);
+        if (drop) st_scoped(g + i, v, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const unsigned long long m = __ballot(drop);
+    if (!m) return;  // wave-uniform
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the wave's ghost stores before the activation
+    // the key is f32 (the bands' entering-T words): reduce in f32, as unsigned bits (T >= 0)
+    unsigned k = drop ? __float_as_uint((float)v) : 0x7f800000u;
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) k = min(k, (unsigned)__shfl_xor((int)k, d));
+    if ((threadIdx.x & 63) == (unsigned)__builtin_ctzll(m)) {
+        if (count) atomicAdd(count, (unsigned)__popcll(m));
+        int ty, tx;
+        if (side < 2) {
+            tx = (int)(i / kTile);
+            ty = side == 0 ? 0 : a.nty - 1;
+        } else {
+            ty = (int)(i / kTile);
+            tx = side == 2 ? 0 : a.ntx - 1;
+        }
+        activate(a, ty * a.ntx + tx, a.iter % 3, a.iter + 1, __uint_as_float(k), kFromN << side);
+    }
+}
+
+// Live DD halo agent: workgroup 0 of a live launch -- the first one dispatched, so it runs even when
+// other work on the device keeps some of the launch's workgroups from being resident (those start
+// late and find the solve over).  It serves the host's mailbox while
 // the other workgroups solve: PACK (snapshot the queue's activity, then store the four edges of T
 // into the neighbours' receive strips -- peer memory over xGMI), MERGE (min-merge the received
 // strips into the ghosts, queue the edge tiles whose ghost dropped) and RELEASE (end the launch).
 // One command in flight; every wait is bounded by qtimeout.
 template <typename R>
-__device__ void live_agent(const Fim2dArgs& a, unsigned* sh) {
+__device__ __forceinline__ void live_agent(const Fim2dArgs& a, unsigned* sh) {
     LiveBox* box = a.live;
     const int tid = threadIdx.x;
     unsigned last = 0;
@@ -780,23 +819,8 @@ __device__ void live_agent(const Fim2dArgs& a, unsigned* sh) {
                 R* g = static_cast<R*>(const_cast<void*>(a.ghost[side]));
                 if (!rv || !g) continue;
                 const int64_t len = side < 2 ? a.W : a.H;
-                for (int64_t i = tid; i < len; i += blockDim.x) {
-                    const R v = ld_system(rv + i);
-                    if (v < ld_agent(g + i)) {
-                        st_scoped(g + i, v, __HIP_MEMORY_SCOPE_AGENT);
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                        atomicAdd(&sh[3], 1u);
-                        int ty, tx;
-                        if (side < 2) {
-                            tx = (int)(i / kTile);
-                            ty = side == 0 ? 0 : a.nty - 1;
-                        } else {
-                            ty = (int)(i / kTile);
-                            tx = side == 2 ? 0 : a.ntx - 1;
-                        }
-                        qpush(a, ty * a.ntx + tx, kFromN << side, (float)v);
-                    }
-                }
+                for (int64_t i0 = 0; i0 < len; i0 += blockDim.x)
+                    merge_strip_cells<R>(a, side, rv, g, i0 + tid, len, &sh[3]);
             }
         }
         __syncthreads();
@@ -820,7 +844,7 @@ __device__ void live_agent(const Fim2dArgs& a, unsigned* sh) {
 template <typename R, int WPS, bool CAP = false>
 __global__ __launch_bounds__(kThreads, WPS) void fim2d_persist_kernel(Fim2dArgs a) {
     __shared__ TileLds<R> L;
-    if (a.live && blockIdx.x == gridDim.x - 1) {
+    if (a.live && blockIdx.x == 0) {
         __shared__ unsigned sh[4];
         live_agent<R>(a, sh);
         return;
@@ -976,32 +1000,39 @@ hipError_t fim2d_prio_delta(const void* cost, bool f64, int64_t n, float mult, f
 }
 
 // After each persistent launch: the tickets of its idle waiters ran ahead of the tail --
-// restart the ticket counter at the tail (every slot is empty when the launch ends).
-__global__ void fim2d_qrewind_kernel(Fim2dArgs a) { *a.qhead = *a.qtail; }
+// restart the ticket counter at the tail.  On the FIFO every slot is empty when a launch ends.
+// With priority bands a dispatch may still move (stale) band entries into slots whose ticket
+// holders have already left on qactive == 0: those entries are dropped here and their tiles'
+// band-membership bits cleared (the relaunch schedule's next launch would otherwise read a
+// leftover entry one ring lap later, and the bit would keep the tile out of its band).
+__global__ void fim2d_qrewind_kernel(Fim2dArgs a) {
+    if (a.bctl) {
+        const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= (int64_t)a.qmask; i += stride) {
+            const unsigned v = a.qslot[i];
+            if (v == 0u) continue;
+            const unsigned tag = v >> kBandTagShift;
+            if (tag) atomicAnd(&a.bmem[(v & kSlotTileMask) - 1u], ~(1ull << (tag - 1u)));
+            a.qslot[i] = 0u;
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a.qhead = *a.qtail;
+}
+static void launch_qrewind(const Fim2dArgs& a, hipStream_t st) {
+    const int grid = a.bctl ? (int)std::min<int64_t>(256, ((int64_t)a.qmask + 256) / 256) : 1;
+    hipLaunchKernelGGL(fim2d_qrewind_kernel, dim3(grid), dim3(a.bctl ? 256 : 1), 0, st, a);
+}
 
 // Domain decomposition: ghost = min(ghost, recv) and activate every edge tile next to a ghost
 // cell that decreased (for list iteration `iter`, or into the FIFO).  side: 0 N 1 S 2 W 3 E.
 // The strip may have been written by a peer GPU (system-scope loads); during a live launch the
 // ghost store is made visible (agent scope, released) before the tile is queued.
+// (Blocks of 256: each wave's cells are one 64-aligned run, merge_strip_cells.)
 template <typename R>
-__global__ void fim2d_merge_ghost_kernel(Fim2dArgs a, int side, const R* __restrict__ recv, int64_t len) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= len) return;
+__global__ __launch_bounds__(256) void fim2d_merge_ghost_kernel(Fim2dArgs a, int side, const R* __restrict__ recv,
+                                                                int64_t len) {
     R* g = static_cast<R*>(const_cast<void*>(a.ghost[side]));
-    const R v = ld_system(recv + i);
-    if (v < g[i]) {
-        st_scoped(g + i, v, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        int ty, tx;
-        if (side < 2) {
-            tx = (int)(i / kTile);
-            ty = side == 0 ? 0 : a.nty - 1;
-        } else {
-            ty = (int)(i / kTile);
-            tx = side == 2 ? 0 : a.ntx - 1;
-        }
-        activate(a, ty * a.ntx + tx, a.iter % 3, a.iter + 1, (float)v, kFromN << side);
-    }
+    merge_strip_cells<R>(a, side, recv, g, (int64_t)blockIdx.x * blockDim.x + threadIdx.x, len, nullptr);
 }
 
 // Copy this subdomain's edge rows/columns of T into contiguous send strips -- local buffers or a
@@ -1054,12 +1085,12 @@ hipError_t fim2d_persist(const Fim2dArgs& a, bool f64, int grid, hipStream_t st,
     else
         hipLaunchKernelGGL((fim2d_persist_kernel<float, 1>), dim3(grid), dim3(kThreads), 0, st, a);
     // before anything (merge kernel, next launch) appends again
-    if (rewind) hipLaunchKernelGGL(fim2d_qrewind_kernel, dim3(1), dim3(1), 0, st, a);
+    if (rewind) launch_qrewind(a, st);
     return hipGetLastError();
 }
 
 hipError_t fim2d_qrewind(const Fim2dArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL(fim2d_qrewind_kernel, dim3(1), dim3(1), 0, st, a);
+    launch_qrewind(a, st);
     return hipGetLastError();
 }
 

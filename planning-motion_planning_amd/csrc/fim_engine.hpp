@@ -283,35 +283,65 @@ __device__ __forceinline__ unsigned band_of(const Fim2dArgs& a, float k) {
 __device__ __forceinline__ void qcount(const Fim2dArgs& a, int i) {
     if (EIK_QDEBUG) atomicAdd(a.visits + 3 + i, 1ull);
 }
-// A band is a ring of bmask + 1 slots (eikonal_api.cpp: >= 2 x the tiles, EIK_OPT_PRIO_RING).  A
-// tile has at most one live entry per band per pending episode, but stale entries of earlier
-// episodes wait in their band until dispatched; a put that would lap an undispatched entry flags
-// qerror bit 4 (its head is loaded beside the tail's add, so no extra round trip; an older head
-// only errs on the safe side) and the host re-solves with the FIFO (eik_fim2d_solve).
-__device__ __forceinline__ void band_put(const Fim2dArgs& a, unsigned b, int tile) {
-    qcount(a, 7);
+// A band is a ring of bmask + 1 slots (eikonal_api.cpp: a power of two >= 2 x the tiles,
+// EIK_OPT_PRIO_RING).  At most ONE entry per (tile, band) exists at any time: a.bmem[tile] bit b is
+// set by the put (an atomicOr whose old value says whether an entry is already there) and cleared
+// by the workgroup that takes the entry from the FIFO, before its claim (qgrab_prio).  A put that
+// finds the bit set is dropped -- the tile's entry already waiting in band b (stale from an earlier
+// pending episode, or this episode's) is taken in its place, and since the put made the tile
+// PENDING before its bit test, that entry's claim, which clears the bit before its CAS, serves it.
+// So a band holds at most `tiles` entries and its ring cannot lap.  (Round 5 without the bits:
+// stale entries of a long live DD launch's many episodes piled up in the bands until a ring of 2 x
+// the tiles lapped -- the 4 x 2 live test's launch ended on qerror bit 4, profiles/
+// r05as_tests_live_4x2_fail.log)  The lap check stays for a ring forced below the
+// tile count (EIK_OPT_PRIO_RING, tests): qerror bit 4, and eik_fim2d_solve re-solves on the FIFO.
+__device__ __forceinline__ void band_put_slot(const Fim2dArgs& a, unsigned b, int tile) {
     const unsigned long long hd = __hip_atomic_load(&a.bctl[16 * b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long pos = atomicAdd(&a.bctl[16 * b + 8], 1ull);
     if (pos > hd + a.bmask) atomicOr(a.qerror, 4u);
     __hip_atomic_store(&a.bslot[(size_t)b * (a.bmask + 1ull) + (pos & a.bmask)], (unsigned)tile + 1u, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
 }
-// a workgroup waits on the FIFO (a ticket past the filled slots)
-__device__ __forceinline__ bool fifo_waiters(const Fim2dArgs& a) {
+__device__ __forceinline__ void band_put(const Fim2dArgs& a, unsigned b, int tile) {
+    const unsigned long long bit = 1ull << b;
+    if (atomicOr(&a.bmem[tile], bit) & bit) return;  // the tile's entry in band b serves this put
+    qcount(a, 7);
+    band_put_slot(a, b, tile);
+}
+// a newly pending tile with key k (priority mode): to a waiting workgroup (a ticket past the
+// filled slots), else to its band.
+__device__ __forceinline__ void prio_put(const Fim2dArgs& a, int tile, float k) {
     const unsigned long long h = __hip_atomic_load(a.qhead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long t = __hip_atomic_load(a.qtail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return h > t;
-}
-// a newly pending tile with key k (priority mode): to a waiting workgroup, else to its band
-__device__ __forceinline__ void prio_put(const Fim2dArgs& a, int tile, float k) {
-    if (fifo_waiters(a))
+    if (h > t)
         qslot_put(a, tile);
     else
         band_put(a, band_of(a, k), tile);
 }
+// The same with the membership bit set beside the head / tail loads (one round trip for both), given
+// back when the tile goes to the FIFO instead -- meanwhile another put of this pending tile to band b
+// is dropped, which is safe: the FIFO entry serves it.  For qfinish (a visit's retirement, off the
+// sweeps' register peak); inside a sweep (qpush_complete in the split activations) the serial form
+// above keeps the fp64 kernel at two workgroups per CU.
+__device__ __forceinline__ void prio_put_overlap(const Fim2dArgs& a, int tile, float k) {
+    const unsigned b = band_of(a, k);
+    const unsigned long long bit = 1ull << b;
+    const unsigned long long had = atomicOr(&a.bmem[tile], bit) & bit;
+    const unsigned long long h = __hip_atomic_load(a.qhead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long t = __hip_atomic_load(a.qtail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (h > t) {
+        if (!had) atomicAnd(&a.bmem[tile], ~bit);
+        qslot_put(a, tile);
+    } else if (!had) {
+        qcount(a, 7);
+        band_put_slot(a, b, tile);
+    }
+}
 // claim a taken entry: pending -> busy (stale entries -- the tile busy, or no longer pending -- fail)
 __device__ __forceinline__ bool prio_claim(const Fim2dArgs& a, int tile, unsigned& trig) {
     unsigned old = __hip_atomic_load(&a.qstate[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // (qgrab_prio's membership-bit clear, in flight beside the load above, completes before the CAS)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     for (;;) {
         if ((old & kBusy) || !(old & kPending)) return false;
         const unsigned prev = atomicCAS(&a.qstate[tile], old, kBusy | kVisited);
@@ -493,7 +523,7 @@ __device__ __forceinline__ void qfinish(const Fim2dArgs& a, int tile) {
     const unsigned old = atomicAnd(&a.qstate[tile], ~kBusy);
     if (old & kPending) {
         if (a.bctl)  // its key: the smallest activation since its claim (0 for a self re-queue)
-            prio_put(a, tile, __uint_as_float(__hip_atomic_load(&a.key[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+            prio_put_overlap(a, tile, __uint_as_float(__hip_atomic_load(&a.key[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
         else
             qslot_put(a, tile);
     } else {
@@ -578,7 +608,9 @@ __device__ __forceinline__ bool band_dispatch(const Fim2dArgs& a) {
             __builtin_amdgcn_s_sleep(1);
         }
         __hip_atomic_store(slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&a.qslot[(base + lane) & a.qmask], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // tagged with its band: the taker clears the tile's membership bit (qgrab_prio)
+        __hip_atomic_store(&a.qslot[(base + lane) & a.qmask], v | ((unsigned)b + 1u) << kBandTagShift, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     }
     return true;
 }
@@ -611,7 +643,14 @@ __device__ __forceinline__ int qgrab_prio(const Fim2dArgs& a, unsigned& trig) {
                 unsigned tg = 0u;
                 if (lane == 0) {
                     __hip_atomic_store(slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    got = prio_claim(a, (int)(v - 1u), tg) ? (int)(v - 1u) : -1;
+                    const int tl = (int)((v & kSlotTileMask) - 1u);
+                    const unsigned tag = v >> kBandTagShift;
+                    // an entry from band tag - 1: its membership bit is cleared BEFORE the claim's
+                    // CAS (a put that still saw the bit made the tile pending first, so this claim
+                    // serves it; a put after the clear makes a new entry).  Issued beside the
+                    // claim's state load, both awaited before the CAS (prio_claim).
+                    if (tag) atomicAnd(&a.bmem[tl], ~(1ull << (tag - 1u)));
+                    got = prio_claim(a, tl, tg) ? tl : -1;
                     qcount(a, got >= 0 ? 3 : 4);
                 }
                 got = __shfl(got, 0);

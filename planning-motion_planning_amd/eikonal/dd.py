@@ -150,6 +150,32 @@ class GpuLocalLayered(GpuLocal):
         self.last_active = 1
 
 
+class HostStaged:
+    """dd.solve adapter for a gloo group between processes that share one GPU (the shared-GPU
+    rehearsals and tests): the device strips of a block solver are staged through host tensors
+    (gloo moves CPU tensors; RCCL cannot put two ranks on one device -- on a node the strips go over
+    RCCL directly).  dsend / drecv: the device strips; dd.solve is handed the host ones."""
+
+    def __init__(self, loc, dsend, drecv):
+        self.loc, self.dsend, self.drecv = loc, dsend, drecv
+
+    def iterate(self, k):
+        self.loc.iterate(k)
+
+    def pack_edges(self, *hsend):
+        self.loc.pack_edges(*self.dsend)
+        for h, d in zip(hsend, self.dsend):
+            if h is not None:
+                h.copy_(d)
+
+    def merge_ghost(self, side, hrecv):
+        self.drecv[side].copy_(hrecv)
+        self.loc.merge_ghost(side, self.drecv[side])
+
+    def active(self):
+        return self.loc.active()
+
+
 # ------------------------------------------------------------------------- live schedule
 OPP = {N_: S_, S_: N_, W_: E_, E_: W_}
 ERR_MARK = 1 << 40  # carried through the all-reduce when a rank's solve failed
@@ -205,6 +231,13 @@ def solve_live(local, block, halo, group=None, max_rounds=1000000, vote=None):
     edges were packed, and merging them lowered no ghost -- T was frozen from that snapshot on,
     so it is the global fixed point.  Stores of parity p land only after every rank has merged
     parity p of round r-2 (it has passed the all-reduce of round r-1)."""
+    def total(v):
+        if vote is not None:
+            return vote(v)
+        t = torch.tensor([v], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        return int(t.item())
+
     local.launch(halo)
     carry, rounds, ok, err = 1, 0, False, None
     try:
@@ -216,12 +249,7 @@ def solve_live(local, block, halo, group=None, max_rounds=1000000, vote=None):
                     halo.send(local, par)
                 except Exception as e:  # keep the collective schedule: the others must learn of it
                     err, carry = e, ERR_MARK
-            if vote is not None:
-                tot = vote(carry)
-            else:
-                t = torch.tensor([carry], dtype=torch.int64)
-                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
-                tot = int(t.item())
+            tot = total(carry)
             if tot >= ERR_MARK:
                 raise RuntimeError("live domain-decomposed solve failed on a rank") from err
             if tot == 0:
@@ -234,9 +262,19 @@ def solve_live(local, block, halo, group=None, max_rounds=1000000, vote=None):
                 err, carry = e, ERR_MARK
         raise RuntimeError("live domain-decomposed solve did not converge")
     finally:
-        left = local.release()
-        if ok and left != 0:
-            raise RuntimeError(f"live solve released with {left} tiles still active")
+        rel_err = None
+        try:
+            left = local.release()
+            if ok and left != 0:
+                rel_err = RuntimeError(f"live solve released with {left} tiles still active")
+        except Exception as e:
+            rel_err = e
+        if ok:
+            # every rank left the round loop on the same vote; one more vote makes a release that
+            # failed on ONE rank fail the solve on all of them (a caller that falls back -- bench.py --
+            # must take the same branch everywhere)
+            if total(ERR_MARK if rel_err is not None else 0) >= ERR_MARK:
+                raise RuntimeError("live domain-decomposed solve: a rank's release failed") from rel_err
 
 
 class P2PHalo:

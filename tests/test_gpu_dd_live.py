@@ -109,6 +109,17 @@ def test_live_single_block_full_grid():
     ctx.close()
 
 
+def _why(rank, e):
+    """a worker's failure with its cause chain (dd.solve_live raises on every rank alike; the
+    cause -- the eikonal error of the rank that failed, with its queue error word -- rides below)"""
+    parts = [f"rank {rank}: {e!r}"]
+    c = e.__cause__ or e.__context__
+    while c is not None and len(parts) < 4:
+        parts.append(repr(c))
+        c = c.__cause__ or c.__context__
+    return " <- ".join(parts)
+
+
 def _port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -159,7 +170,7 @@ def _ipc_worker(rank, world, port, H, W, goal, seed, q, f64):
         halo.close()
         q.put((rank, blk.y0, blk.y1, blk.x0, blk.x1, res, rounds, None))
     except Exception as e:  # report instead of hanging the parent
-        q.put((rank, 0, 0, 0, 0, None, 0, repr(e)))
+        q.put((rank, 0, 0, 0, 0, None, 0, _why(rank, e)))
     finally:
         dist.destroy_process_group()
 
@@ -185,7 +196,7 @@ def test_live_ipc_processes(world, f64):
             if p.is_alive():
                 p.kill()
     errs = [x[-1] for x in parts if x[-1]]
-    assert not errs, errs
+    assert not errs, "\n".join(errs)
     cost = _cost(H, W, seed, goal)
     if not f64:
         cost = cost.astype(np.float32).astype(np.float64)
@@ -198,9 +209,10 @@ def test_live_ipc_processes(world, f64):
         _check(T, R, f64, cost)
 
 
-def _terrain_worker(rank, world, port, N, q):
+def _terrain_worker(rank, world, port, N, q, ring=0):
     """One rank of bench.py's N > 1 configuration (configs[3] scaled to N^2): its block of the seed-7
-    terrain raster generated on the device, fp64, the live schedule over IPC strips + the node vote."""
+    terrain raster generated on the device, fp64, the live schedule over IPC strips + the node vote.
+    ring > 0: EIK_OPT_PRIO_RING, slots per priority band."""
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -221,8 +233,10 @@ def _terrain_worker(rank, world, port, N, q):
         c = terrain.cost_block(blk.y0, blk.x0, blk.h, blk.w, N, N, seed=7, device=dev).double().contiguous()
         T = torch.empty_like(c)
         ctx = eikonal.Context(0)
-        ctx.set_option(L.OPT_GRID, max(2, 2 * torch.cuda.get_device_properties(dev).multi_processor_count // world))
+        ctx.set_option(L.OPT_GRID, max(2, 3 * torch.cuda.get_device_properties(dev).multi_processor_count // (2 * world)))
         ctx.set_option(L.OPT_QTIMEOUT, 20.0)
+        if ring:
+            ctx.set_option(L.OPT_PRIO_RING, ring)
         fim = eikonal.Fim2d(ctx, 1, blk.h, blk.w, L.EIK_F64)
         _, _, ghost = dd.make_strips(blk, torch.float64, dev, float("inf"))
         loc = dd.LiveGpuLocal(fim, ghost)
@@ -237,17 +251,26 @@ def _terrain_worker(rank, world, port, N, q):
         vote.close()
         q.put((rank, blk.y0, blk.y1, blk.x0, blk.x1, T.cpu().numpy(), rounds, ok, None))
     except Exception as e:  # report instead of hanging the parent
-        q.put((rank, 0, 0, 0, 0, None, 0, False, repr(e)))
+        q.put((rank, 0, 0, 0, 0, None, 0, False, _why(rank, e)))
     finally:
         dist.destroy_process_group()
 
 
-def test_c4_split_4x2_assembled_field():
+@pytest.mark.parametrize("ring", [0, 64])
+def test_c4_split_4x2_assembled_field(ring):
     """configs[3]'s 4 x 2 split at a real size: a 4096^2 fp64 raster of the bench's terrain (seed 7,
-    goal at the centre) over 8 processes sharing cuda:0 (the bench's EIK_BENCH_SHARED_GPU grids),
-    the live schedule (IPC peer stores + shared-memory vote).  The assembled blocks are compared
-    with the single-domain solve of the same raster: masks equal, <= 1e-11 relative, and every
-    reached cell a fixed point of its own neighbours (<= 1e-9 relative residual)."""
+    goal at the centre) over 8 processes sharing cuda:0 (the bench's EIK_BENCH_SHARED_GPU grids, 3/4 of
+    the co-resident workgroups), the live schedule (IPC peer stores + shared-memory vote).  The
+    assembled blocks are compared with the single-domain solve of the same raster: masks equal,
+    <= 1e-11 relative, and every reached cell a fixed point of its own neighbours (<= 1e-9 relative
+    residual).
+    ring=64: every priority band's ring forced to 64 slots, 1/8 of a block's 512 tiles (16 x 32 tiles
+    of 1024 x 2048).  The band-membership bits (fim_engine.hpp band_put) bound a band to one entry per
+    tile, so the default ring (>= 2 x the tiles) cannot lap; this case checks a long live launch on
+    rings far below that (profiles/r06c_ring_probe.log: 512 / 256 / 128 / 64 slots, both the round-5
+    and this library, no lap).  Round 5's failure of this test was not a ring lap but residency: 8
+    launches of exactly the co-resident grid each, and one rank's halo agent -- then its LAST
+    workgroup -- could not start while another rank's small kernels held a slot."""
     import torch.multiprocessing as mp
 
     import eikonal
@@ -258,7 +281,7 @@ def test_c4_split_4x2_assembled_field():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_terrain_worker, args=(r, world, port, N, q)) for r in range(world)]
+    procs = [ctx.Process(target=_terrain_worker, args=(r, world, port, N, q, ring)) for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -269,7 +292,7 @@ def test_c4_split_4x2_assembled_field():
             if p.is_alive():
                 p.kill()
     errs = [x[-1] for x in parts if x[-1]]
-    assert not errs, errs
+    assert not errs, "\n".join(errs)
     assert all(x[7] for x in parts), "halo strips differ from the neighbours' final edges"
     Tdd = np.full((N, N), np.nan)
     for _, y0, y1, x0, x1, Tb, rounds, _, _ in parts:
@@ -292,31 +315,6 @@ def test_c4_split_4x2_assembled_field():
     assert rel.max() <= 1e-11, rel.max()
     res = _residual(Tdd, cost)
     assert res <= 1e-9, res
-
-
-class _HostStaged:
-    """dd.solve adapter for gloo between processes on one GPU: the device strips of a block solver
-    are staged through host tensors (RCCL cannot put two ranks on one device; on a node the strips
-    go over RCCL directly)."""
-
-    def __init__(self, loc, dsend, drecv):
-        self.loc, self.dsend, self.drecv = loc, dsend, drecv
-
-    def iterate(self, k):
-        self.loc.iterate(k)
-
-    def pack_edges(self, *hsend):
-        self.loc.pack_edges(*self.dsend)
-        for h, d in zip(hsend, self.dsend):
-            if h is not None:
-                h.copy_(d)
-
-    def merge_ghost(self, side, hrecv):
-        self.drecv[side].copy_(hrecv)
-        self.loc.merge_ghost(side, self.drecv[side])
-
-    def active(self):
-        return self.loc.active()
 
 
 def _layered_worker(rank, world, port, H, W, goal, q):
@@ -343,7 +341,7 @@ def _layered_worker(rank, world, port, H, W, goal, q):
         c = torch.from_numpy(np.ascontiguousarray(vol[blk.y0:blk.y1, blk.x0:blk.x1])).to(dev)
         T = torch.empty_like(c)
         ctx = eikonal.Context(0)
-        ctx.set_option(L.OPT_GRID, max(2, 2 * torch.cuda.get_device_properties(dev).multi_processor_count // world))
+        ctx.set_option(L.OPT_GRID, max(2, 3 * torch.cuda.get_device_properties(dev).multi_processor_count // (2 * world)))
         nl = 3
         dsend, drecv, ghost = dd.make_strips(blk, torch.float64, dev, float("inf"), per_cell=nl)
         hsend, hrecv, _ = dd.make_strips(blk, torch.float64, "cpu", float("inf"), per_cell=nl)
@@ -351,14 +349,14 @@ def _layered_worker(rank, world, port, H, W, goal, q):
         loc = dd.GpuLocalLayered(fim, ghost)
         lg = blk.local_goal(goal[0], goal[1])
         loc.start(c, T, (lg[0], lg[1], goal[2]), torch.cuda.current_stream(dev).cuda_stream)
-        rounds = dd.solve(_HostStaged(loc, dsend, drecv), blk, hsend, hrecv, exchange_every=4,
+        rounds = dd.solve(dd.HostStaged(loc, dsend, drecv), blk, hsend, hrecv, exchange_every=4,
                           count_device="cpu")
         torch.cuda.synchronize()
         q.put((rank, blk.y0, blk.y1, blk.x0, blk.x1, T.cpu().numpy(), rounds, None))
         fim.close()
         ctx.close()
     except Exception as e:  # report instead of hanging the parent
-        q.put((rank, 0, 0, 0, 0, None, 0, repr(e)))
+        q.put((rank, 0, 0, 0, 0, None, 0, _why(rank, e)))
     finally:
         dist.destroy_process_group()
 
@@ -401,7 +399,7 @@ def test_c5_split_2x1_processes():
             if p.is_alive():
                 p.kill()
     errs = [x[-1] for x in parts if x[-1]]
-    assert not errs, errs
+    assert not errs, "\n".join(errs)
     Tdd = np.full((H, W, 5), np.nan)
     for _, y0, y1, x0, x1, Tb, rounds, _ in parts:
         Tdd[y0:y1, x0:x1] = Tb
