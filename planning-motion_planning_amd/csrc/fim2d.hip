@@ -51,6 +51,9 @@ __device__ __forceinline__ R stage_cost(R c) {
 // and fp32 (profiles/r03l_edge_first_ab.log), and C3 / C4 3-8 % slower (round 4,
 // profiles/r04u_edge_first_throughput_ab.log): the drain before the activations is latency, not the
 // number of stores, and the extra per-visit barrier and edge-column stores cost more than it saves.
+#ifndef EIK_WB_LINE
+#define EIK_WB_LINE 0
+#endif
 #ifndef EIK_EDGE_FIRST
 #define EIK_EDGE_FIRST 0
 #endif
@@ -557,6 +560,13 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
                     if (gx == a.W - 1 && cx + e != kTile - 1) fl |= 64u;
                 }
             }
+#if EIK_WB_LINE
+            // (A/B, round 6: store whole 128-B lines -- every chunk of a line whose any chunk changed)
+            if (full) {
+#pragma unroll
+                for (int m = 1; m < 128 / (4 * (int)sizeof(R)); m <<= 1) any |= __shfl_xor((int)any, m) != 0;
+            }
+#endif
             if (any) {
                 if (COH && EIK_EDGE_FIRST && full && ry != 0 && ry != kTile - 1) {
                     if (cx == 0 && nv[0] < told[4 * k]) T.st(gy * a.W + x0, nv[0]);

@@ -279,7 +279,9 @@ __device__ __forceinline__ unsigned band_of(const Fim2dArgs& a, float k) {
 #ifndef EIK_QDEBUG
 #define EIK_QDEBUG 0
 #endif
-// queue counters for tools (eik_fim2d_qcount): a.visits[3 + i]
+// queue counters for tools (eik_fim2d_qcount): a.visits[3 + i] -- 0 FIFO slot polls, 1 tail polls
+// (priority mode), 2 band dispatch attempts, 3 / 4 claims won / stale entries dropped, 5 dispatches
+// that moved entries, 6 decrease-key entries, 7 band entries put
 __device__ __forceinline__ void qcount(const Fim2dArgs& a, int i) {
     if (EIK_QDEBUG) atomicAdd(a.visits + 3 + i, 1ull);
 }
@@ -468,6 +470,7 @@ __device__ __forceinline__ int qgrab(const Fim2dArgs& a, unsigned& trig) {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     for (unsigned spin = 0;; ++spin) {
         const unsigned v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        qcount(a, 0);
         if (v != 0u) {
             // free the slot BEFORE the tile can be re-queued (slot reuse).  Only fresh-first
             // producers write a filled slot (their CAS): then the entry is taken with an exchange.
@@ -564,6 +567,7 @@ __device__ __forceinline__ bool band_dispatch(const Fim2dArgs& a) {
         h = __hip_atomic_load(&a.bctl[16 * lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         t = __hip_atomic_load(&a.bctl[16 * lane + 8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (lane == 0) qcount(a, 2);  // (EIK_QDEBUG: dispatch attempts, 2 x 64 band words read each)
     const unsigned lim = a.disp ? (a.disp < 64u ? a.disp : 64u) : kDispatch;
     const unsigned avail = t > h ? (unsigned)(t - h < lim ? t - h : lim) : 0u;
     if (!__ballot(avail != 0u)) return false;
@@ -576,7 +580,7 @@ __device__ __forceinline__ bool band_dispatch(const Fim2dArgs& a) {
     const unsigned end = wave_incl_sum(got), start = end - got;
     const unsigned total = __shfl(end, 63);
     if (total == 0u) return false;  // another dispatcher moved first: look again at the next poll
-    qcount(a, 5);
+    if (lane == 0) qcount(a, 5);
     unsigned long long base = 0;
     if (lane == 0) base = atomicAdd(a.qtail, (unsigned long long)total);
     base = __shfl(base, 0);
@@ -635,7 +639,11 @@ __device__ __forceinline__ int qgrab_prio(const Fim2dArgs& a, unsigned& trig) {
             int oldest = 0;
             if (lane == 0) {
                 v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (!v) oldest = __hip_atomic_load(a.qtail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == pos;
+                qcount(a, 0);  // (EIK_QDEBUG: the polls' sc1 loads -- slot, then tail)
+                if (!v) {
+                    oldest = __hip_atomic_load(a.qtail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == pos;
+                    qcount(a, 1);
+                }
             }
             v = __shfl(v, 0);
             if (v != 0u) {

@@ -24,9 +24,13 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     stream = torch.cuda.Stream(dev)
-    ctx = eikonal.Context(0)
+    ctx = eikonal.Context(0, options=L.options_from_env())  # EIK_OPTIONS A/B hook
     tdt, edt = (torch.float64, L.EIK_F64) if dt == "f64" else (torch.float32, L.EIK_F32)
-    if cfg == "C3":
+    if cfg == "C2":  # configs[1], the headline raster
+        from eikonal import terrain
+        cost = terrain.cost_block(0, 0, 4096, 4096, 4096, 4096, seed=42, device=dev).to(tdt).contiguous()
+        out = bench.bench_c2(ctx, dev, stream, cost, (2048, 2048), steps, dt)
+    elif cfg == "C3":
         out = bench.bench_batch(ctx, dev, stream, steps, tdt, edt)
     elif cfg == "C4":
         out = bench.bench_c4(ctx, dev, stream, steps, tdt, edt)
