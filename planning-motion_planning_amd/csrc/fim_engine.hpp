@@ -370,8 +370,8 @@ __device__ __forceinline__ void qpush_complete(const Fim2dArgs& a, int tile, uns
                                                unsigned kold = 0x7f800000u) {
     if ((old & (kPending | kBusy)) == 0u) {
         atomicAdd(a.qactive, 1);  // before the slot store: a waiter never sees "empty and idle"
-        if (a.bctl)
-            prio_put(a, tile, fminf(k, __uint_as_float(kold)));
+        if (a.bctl)  // (EIK_OPT_FRESH_FIRST on the bands: a fresh tile -- the front advancing -- keyed 0)
+            prio_put(a, tile, a.fresh_first && !(old & kVisited) ? 0.f : fminf(k, __uint_as_float(kold)));
         else if (!(old & kVisited) && a.fresh_first)
             qslot_put_front(a, tile);
         else
