@@ -715,6 +715,8 @@ def bench_c5_split(ctx, dev, stream, steps, tdt, edt, rank, world, group, shared
     tile visits beside the single domain's."""
     px, py = dd.SPLITS[world]
     blk = dd.Block(N, N, px, py, rank)
+    if shared:  # the layered kernel holds one workgroup per CU: 3/4 of those, split between the ranks
+        ctx.set_option(L.OPT_GRID, max(2, 3 * torch.cuda.get_device_properties(dev).multi_processor_count // (4 * world)))
     vol = c5_volume(terrain.cost_block(0, 0, N, N, N, N, seed=42, device=dev).to(tdt), dev)
     cb = vol[blk.y0:blk.y1, blk.x0:blk.x1].contiguous()
     T = torch.empty_like(cb)
@@ -730,10 +732,31 @@ def bench_c5_split(ctx, dev, stream, steps, tdt, edt, rank, world, group, shared
     lg = blk.local_goal(N // 2, N // 2)
     goal = (lg[0], lg[1], 1)
     rounds, vis, pas = [], [], []
+    # the live schedule (round 6: the layered kernel's halo agent, hipIpc strips of nl values per edge
+    # cell, the node vote), agreed by every rank, else the relaunch rounds above
+    live, live_err, halo, vote = None, None, None, None
+    try:
+        halo = dd.IpcHalo(ctx, blk, (8 if edt == L.EIK_F64 else 4) * nl, group=group)
+        if env_int("LOCAL_WORLD_SIZE", world) == world:
+            vote = dd.NodeVote(group=group)
+    except Exception as e:
+        live_err = repr(e)
+    ok = torch.tensor([0 if live_err else 1], dtype=torch.int64)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+    if ok.item() == 1:
+        live = dd.LiveGpuLocalLayered(fim, ghost)
 
     def solve():
-        loc.start(cb, T, goal, stream.cuda_stream)
-        rounds.append(dd.solve(drv, blk, send, recv, exchange_every=1, count_device=cdev))
+        nonlocal live, live_err
+        if live is not None:
+            try:
+                live.start(cb, T, goal, stream.cuda_stream)
+                rounds.append(dd.solve_live(live, blk, halo, group=group, vote=vote))
+            except Exception as e:  # every rank alike (dd.solve_live's error carry): rounds from here on
+                live, live_err = None, repr(e)
+        if live is None:
+            loc.start(cb, T, goal, stream.cuda_stream)
+            rounds.append(dd.solve(drv, blk, send, recv, exchange_every=1, count_device=cdev))
         st = fim.stats()
         vis.append(st["tile_visits"])
         pas.append(st["inplace_passes"])
@@ -772,12 +795,18 @@ def bench_c5_split(ctx, dev, stream, steps, tdt, edt, rank, world, group, shared
     pr = torch.stack(allr)
     tol = 1e-11 if edt == L.EIK_F64 else 1e-5
     fim.close()
+    if halo is not None:
+        halo.close()
+    if vote is not None:
+        vote.close()
     del vol, cb, T, Tf
     torch.cuda.empty_cache()
+    sched = ("live schedule: persistent layered launches + halo agents, hipIpc strips (xGMI) + node vote"
+             if live is not None else "relaunch schedule (" + ("host-staged gloo rehearsal" if shared else
+                                                               "RCCL batch_isend_irecv + all_reduce") + ")")
     return {"workload": f"configs[4] split: {N}x{N}x3 layered costmap (bench_layers' volume, z padded to 5), "
-                        f"{px}x{py} x-y blocks over {world} GPUs, layers together; layered solver per block, "
-                        "relaunch schedule (" + ("host-staged gloo rehearsal" if shared else
-                                                 "RCCL batch_isend_irecv + all_reduce") + ")",
+                        f"{px}x{py} x-y blocks over {world} GPUs, layers together; layered solver per block, " + sched,
+            "dd_mode": "live" if live is not None else "rounds", **({"dd_live_error": live_err[:200]} if live_err else {}),
             "dtype": "f64" if edt == L.EIK_F64 else "f32", "value": round(N * N * 3 / sec / 1e9, 4),
             "unit": "Gcells/s", "ms_per_step": round(sec * 1e3, 4), "steps": steps,
             "dd_field_ok": bool(float(pr[:, 0].max()) <= tol), "dd_field_max_rel": float(pr[:, 0].max()),

@@ -1016,7 +1016,13 @@ int eik_fim2d_launch(eik_fim2d* f, int live) {
     HIPCHK(c, hipSetDevice(c->device));
     const int grid = c->grid > 0 ? c->grid : 4 * c->cu_count;
     const bool wide = !f->f64 && f->a.tiles_per_map >= kWideTiles;  // one large raster (a batch of small maps: no gain)
-    if (f->persist_grid == 0) f->persist_grid = fim2d_persist_resident(f->f64, c->cu_count, wide);
+    if (f->lnl) {  // a layered block (eik_fim3dl_create): the layered kernel's co-resident count
+        int& res = c->resident_l[f->f64 ? 1 : 0][f->lnl];
+        if (res == 0) res = fim2dl_persist_resident(f->lnl, f->f64, c->cu_count);
+        f->persist_grid = res;
+    } else if (f->persist_grid == 0) {
+        f->persist_grid = fim2d_persist_resident(f->f64, c->cu_count, wide);
+    }
     Fim2dArgs a = f->a;
     if (live) {
         int rc = live_box(f);
@@ -1041,8 +1047,26 @@ int eik_fim2d_launch(eik_fim2d* f, int live) {
     const int g = std::max(live ? 2 : 1, std::min(grid, f->persist_grid));
     a.fresh_first = c->fresh_first;
     a.sched = c->sched;
-    HIPCHK(c, rewind_if_needed(f));
-    HIPCHK(c, fim2d_persist(a, f->f64, g, f->stream, wide));
+    if (f->lnl) {  // (its launches rewind their queue themselves)
+        // a live layered block orders its waiting tiles on the priority bands at width >= 1, as the 2D
+        // blocks do (§3.2): on the FIFO the blocks re-solved their interiors as the ghosts' corrections
+        // arrived (C5 split 4 x 2: 4.5 x the single domain's visits, profiles/r06i_c4_rehearsal_n8.log).
+        // (The relaunch schedule keeps the FIFO: its launches run to local convergence either way.)
+        const double prio = c->prio >= 0 ? c->prio : std::max(1.0, default_prio(f->H, f->W, 0.0));
+        a.bctl = nullptr;
+        if (live && prio > 0 && a.capacity < (1 << kBandTagShift) - 1) {
+            HIPCHK(c, setup_bands(c, f->bslot, f->bctl, a.capacity, a, f->stream));
+            HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)a.key, 0x7f800000u, (size_t)a.capacity, f->stream));  // keys: +inf
+            float* pd = (float*)((char*)f->bctl.p + 128 * kBands);
+            HIPCHK(c, fim2d_prio_delta(a.cost, f->f64, f->H * f->W * f->lL, (float)prio, pd, f->stream));
+            a.pdelta = pd;
+            a.disp = c->prio_dispatch > 0 ? (unsigned)c->prio_dispatch : 32u;
+        }
+        HIPCHK(c, fim2dl_persist(a, f->lnl, f->f64, g, f->stream));
+    } else {
+        HIPCHK(c, rewind_if_needed(f));
+        HIPCHK(c, fim2d_persist(a, f->f64, g, f->stream, wide));
+    }
     if (c->timing) HIPCHK(c, hipEventRecord(f->ev_pool[f->ev_used++], f->stream));
     f->live_on = live != 0;
     ++f->iterations;

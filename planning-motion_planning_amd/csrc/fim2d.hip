@@ -757,94 +757,47 @@ __device__ __forceinline__ void merge_strip_cells(const Fim2dArgs& a, int side, 
     }
 }
 
-// Live DD halo agent: workgroup 0 of a live launch -- the first one dispatched, so it runs even when
-// other work on the device keeps some of the launch's workgroups from being resident (those start
-// late and find the solve over).  It serves the host's mailbox while
-// the other workgroups solve: PACK (snapshot the queue's activity, then store the four edges of T
-// into the neighbours' receive strips -- peer memory over xGMI), MERGE (min-merge the received
-// strips into the ghosts, queue the edge tiles whose ghost dropped) and RELEASE (end the launch).
-// One command in flight; every wait is bounded by qtimeout.
+// Live DD halo agent of the 2D solver (fim_engine.hpp live_agent_loop: workgroup 0 of a live launch
+// serves the host's mailbox).  PACK: the four edges of T into the neighbours' receive strips (peer
+// memory over xGMI); MERGE: the received strips min-merged into the ghosts, one activation per edge
+// tile and side (merge_strip_cells).
 template <typename R>
 __device__ __forceinline__ void live_agent(const Fim2dArgs& a, unsigned* sh) {
-    LiveBox* box = a.live;
     const int tid = threadIdx.x;
-    unsigned last = 0;
-    for (;;) {
-        if (tid == 0) {
-            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-            unsigned s;
-            for (;;) {
-                s = __hip_atomic_load(&box->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-                if (s != last) break;
-                if (__hip_atomic_load(a.qerror, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
-                    __builtin_amdgcn_s_memrealtime() - t0 > a.qtimeout) {
-                    atomicOr(a.qerror, 1u);
-                    s = ~0u;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(4);
-            }
-            sh[0] = s;
-            sh[1] = s == ~0u ? 0u : __hip_atomic_load(&box->cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            sh[2] = (unsigned)__hip_atomic_load(a.qactive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            sh[3] = 0u;
+    auto pack = [&](unsigned par, bool skip_busy) {
+        const R* T = static_cast<const R*>(a.T);
+        R* tg[4];
+        for (int k = 0; k < 4; ++k) tg[k] = static_cast<R*>(a.live->send[par][k]);
+        // EIK_OPT_LIVE_PACK 1 (skip_busy): a cell of a tile that is pending or busy is not packed -- the
+        // receiver's strip of this parity keeps an older (larger) value, which the min-merge ignores; a
+        // round whose snapshot saw no tile pending or busy packs every cell, so the convergence vote's
+        // proof (dd.solve_live) is unchanged
+        auto idle = [&](int64_t ty, int64_t tx) {
+            return !skip_busy ||
+                   (__hip_atomic_load(&a.qstate[ty * a.ntx + tx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &
+                    (kPending | kBusy)) == 0u;
+        };
+        for (int64_t i = tid; i < a.W; i += blockDim.x) {
+            if (tg[0] && idle(0, i / kTile)) st_scoped(tg[0] + i, ld_agent(T + i), __HIP_MEMORY_SCOPE_SYSTEM);
+            if (tg[1] && idle(a.nty - 1, i / kTile))
+                st_scoped(tg[1] + i, ld_agent(T + (a.H - 1) * a.W + i), __HIP_MEMORY_SCOPE_SYSTEM);
         }
-        __syncthreads();
-        const unsigned s = sh[0], op = sh[1] & 0xffu, par = (sh[1] >> 8) & 1u;
-        if (s == ~0u) {  // timed out: make the solvers leave too
-            if (tid == 0) __hip_atomic_store(a.qhold, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return;
+        for (int64_t i = tid; i < a.H; i += blockDim.x) {
+            if (tg[2] && idle(i / kTile, 0)) st_scoped(tg[2] + i, ld_agent(T + i * a.W), __HIP_MEMORY_SCOPE_SYSTEM);
+            if (tg[3] && idle(i / kTile, a.ntx - 1))
+                st_scoped(tg[3] + i, ld_agent(T + i * a.W + a.W - 1), __HIP_MEMORY_SCOPE_SYSTEM);
         }
-        last = s;
-        if (op == kLivePack) {  // the snapshot (sh[2]) was taken before any T load below
-            const R* T = static_cast<const R*>(a.T);
-            R* tg[4];
-            for (int k = 0; k < 4; ++k) tg[k] = static_cast<R*>(box->send[par][k]);
-            // EIK_OPT_LIVE_PACK 1: a cell of a tile that is pending or busy is not packed -- the
-            // receiver's strip of this parity keeps an older (larger) value, which the min-merge
-            // ignores; a round whose snapshot saw no tile pending or busy packs every cell, so the
-            // convergence vote's proof (dd.solve_live) is unchanged
-            const bool skip_busy = a.live_pack && sh[2] != 0u;
-            auto idle = [&](int64_t ty, int64_t tx) {
-                return !skip_busy ||
-                       (__hip_atomic_load(&a.qstate[ty * a.ntx + tx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &
-                        (kPending | kBusy)) == 0u;
-            };
-            for (int64_t i = tid; i < a.W; i += blockDim.x) {
-                if (tg[0] && idle(0, i / kTile)) st_scoped(tg[0] + i, ld_agent(T + i), __HIP_MEMORY_SCOPE_SYSTEM);
-                if (tg[1] && idle(a.nty - 1, i / kTile))
-                    st_scoped(tg[1] + i, ld_agent(T + (a.H - 1) * a.W + i), __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-            for (int64_t i = tid; i < a.H; i += blockDim.x) {
-                if (tg[2] && idle(i / kTile, 0)) st_scoped(tg[2] + i, ld_agent(T + i * a.W), __HIP_MEMORY_SCOPE_SYSTEM);
-                if (tg[3] && idle(i / kTile, a.ntx - 1))
-                    st_scoped(tg[3] + i, ld_agent(T + i * a.W + a.W - 1), __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: peer stores complete
-        } else if (op == kLiveMerge) {
-            // the strips were stored by peer GPUs: drop any stale cached copy before reading
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-            for (int side = 0; side < 4; ++side) {
-                const R* rv = static_cast<const R*>(box->recv[par][side]);
-                R* g = static_cast<R*>(const_cast<void*>(a.ghost[side]));
-                if (!rv || !g) continue;
-                const int64_t len = side < 2 ? a.W : a.H;
-                for (int64_t i0 = 0; i0 < len; i0 += blockDim.x)
-                    merge_strip_cells<R>(a, side, rv, g, i0 + tid, len, &sh[3]);
-            }
+    };
+    auto merge = [&](unsigned par, unsigned* count) {
+        for (int side = 0; side < 4; ++side) {
+            const R* rv = static_cast<const R*>(a.live->recv[par][side]);
+            R* g = static_cast<R*>(const_cast<void*>(a.ghost[side]));
+            if (!rv || !g) continue;
+            const int64_t len = side < 2 ? a.W : a.H;
+            for (int64_t i0 = 0; i0 < len; i0 += blockDim.x) merge_strip_cells<R>(a, side, rv, g, i0 + tid, len, count);
         }
-        __syncthreads();
-        if (tid == 0) {
-            if (op == kLivePack) __hip_atomic_store(&box->active, sh[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            if (op == kLiveMerge) __hip_atomic_store(&box->changed, sh[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            if (op == kLiveRelease) __hip_atomic_store(a.qhold, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&box->error, __hip_atomic_load(a.qerror, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&box->done, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-        if (op == kLiveRelease) return;
-        __syncthreads();  // sh[] is rewritten by the next command
-    }
+    };
+    live_agent_loop(a, sh, pack, merge);
 }
 
 // WPS: the launch-bounds occupancy target in waves per SIMD (1: the compiler's choice, 159

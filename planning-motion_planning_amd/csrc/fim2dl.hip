@@ -48,7 +48,12 @@ template <> struct LCell<double> {
 #ifndef EIK_L64_ROWS
 #define EIK_L64_ROWS 40
 #endif
-template <typename R> constexpr int kRowsOf = sizeof(R) == 4 ? kTile : EIK_L64_ROWS;
+// EIK_L32_ROWS: the fp32 tile's rows (64; round 6 probed 24 / 32 for a second workgroup per CU --
+// DESIGN.md §3.3)
+#ifndef EIK_L32_ROWS
+#define EIK_L32_ROWS 64
+#endif
+template <typename R> constexpr int kRowsOf = sizeof(R) == 4 ? EIK_L32_ROWS : EIK_L64_ROWS;
 
 // EIK_FRESH_SKIP_L: a full tile's first visit stages only the cost -- its T layers are still the init
 // kernel's +inf (the seed kernel queues the goal's tile as visited), as fim2d.hip's kFreshSkip
@@ -310,9 +315,11 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
     const bool hcell = wave < 2 || lane < TH;
     const bool hin = hcell && hy >= 0 && hy < a.H && hx >= 0 && hx < a.W;
     const int64_t hgi = hin ? (hy * a.W + hx) * ls + a.z0 : 0;
-    // domain decomposition (relaunch schedule, eik_fim3dl_start: the ghosts change only between
-    // launches): the halo cell just outside the block comes from the side's ghost strip, nl values
-    // per edge cell ([i][z], as fim2dl_pack_edges_kernel writes them)
+    // domain decomposition: the halo cell just outside the block comes from the side's ghost strip, nl
+    // values per edge cell ([i][z], as fim2dl_pack_edges_kernel writes them); agent-scope loads -- a
+    // live launch's halo agent lowers the ghosts while the block solves (a cut tile's ghost row /
+    // column inside the tile is read at staging only: the agent's activation of a busy tile re-queues
+    // it, and the next visit stages the new value)
     const R* hg = nullptr;
     int64_t hgo = 0;
     if (hcell && !hin) {
@@ -327,7 +334,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
 #pragma unroll
         for (int z = 0; z < NL; ++z) v[z] = Tz[z].ld(hgi - b0);
 #pragma unroll
-        for (int z = 0; z < NL; ++z) v[z] = hin ? v[z] : (hg ? hg[hgo + z] : INF);
+        for (int z = 0; z < NL; ++z) v[z] = hin ? v[z] : (hg ? (COH ? ld_agent(hg + hgo + z) : hg[hgo + z]) : INF);
         return LCell<R>::make(v);
     };
     // ---- stage: every global load of the visit (T, cost, halo) is issued before the first LDS
@@ -394,7 +401,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
 #pragma unroll
             for (int z = 0; z < NL; ++z) {
                 const R t = Tz[z].ld(gi - b0), c = cost[gi + z * lzs];
-                told[j][z] = in ? t : (gc ? gc[go + z] : INF);
+                told[j][z] = in ? t : (gc ? (COH ? ld_agent(gc + go + z) : gc[go + z]) : INF);
                 cc[j][z] = in ? scost(c) : INF;
             }
         }
@@ -478,11 +485,74 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
     }
 }
 
-// Persistent driver (cf. fim2d_persist_kernel): one launch per solve, device FIFO of tiles.
+// Live DD halo agent of the layered solver (a block of a few-layer volume, SURVEY §8(e) C5: split in
+// x-y, layers together; fim_engine.hpp live_agent_loop serves the mailbox): PACK stores this block's
+// edges, NL values per edge cell ([i][z], fim2dl_pack_edges_kernel's layout), into the neighbours'
+// receive strips; MERGE min-merges the received strips into the ghosts and queues the edge tile of
+// every cell that dropped in any layer (FIFO blocks: a tile already pending costs one atomic).
+template <typename R, int NL>
+__device__ __forceinline__ void live_agent_layered(const Fim2dArgs& a, unsigned* sh) {
+    constexpr int TH = kRowsOf<R>;
+    const int tid = threadIdx.x;
+    const R* T = static_cast<const R*>(a.T);
+    auto at = [&](int64_t y, int64_t x, int z) { return ld_agent(T + (y * a.W + x) * a.ls + a.z0 + z * a.lzs); };
+    auto pack = [&](unsigned par, bool) {
+        R* tg[4];
+        for (int k = 0; k < 4; ++k) tg[k] = static_cast<R*>(a.live->send[par][k]);
+        for (int64_t i = tid; i < a.W; i += blockDim.x)
+#pragma unroll
+            for (int z = 0; z < NL; ++z) {
+                if (tg[0]) st_scoped(tg[0] + i * NL + z, at(0, i, z), __HIP_MEMORY_SCOPE_SYSTEM);
+                if (tg[1]) st_scoped(tg[1] + i * NL + z, at(a.H - 1, i, z), __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        for (int64_t i = tid; i < a.H; i += blockDim.x)
+#pragma unroll
+            for (int z = 0; z < NL; ++z) {
+                if (tg[2]) st_scoped(tg[2] + i * NL + z, at(i, 0, z), __HIP_MEMORY_SCOPE_SYSTEM);
+                if (tg[3]) st_scoped(tg[3] + i * NL + z, at(i, a.W - 1, z), __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+    };
+    auto merge = [&](unsigned par, unsigned* count) {
+        for (int side = 0; side < 4; ++side) {
+            const R* rv = static_cast<const R*>(a.live->recv[par][side]);
+            R* g = static_cast<R*>(const_cast<void*>(a.ghost[side]));
+            if (!rv || !g) continue;
+            const int64_t len = side < 2 ? a.W : a.H;
+            for (int64_t i = tid; i < len; i += blockDim.x) {
+                bool dropped = false;
+                float k = __builtin_inff();
+#pragma unroll
+                for (int z = 0; z < NL; ++z) {
+                    const R v = ld_system(rv + i * NL + z);
+                    if (v < ld_agent(g + i * NL + z)) {
+                        st_scoped(g + i * NL + z, v, __HIP_MEMORY_SCOPE_AGENT);
+                        dropped = true;
+                        k = fminf(k, (float)v);
+                    }
+                }
+                if (!dropped) continue;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the ghost before the activation
+                atomicAdd(count, 1u);
+                const int ty = side < 2 ? (side == 0 ? 0 : a.nty - 1) : (int)(i / TH);
+                const int tx = side < 2 ? (int)(i / kTile) : (side == 2 ? 0 : a.ntx - 1);
+                qpush(a, ty * a.ntx + tx, kFromN << side, k);
+            }
+        }
+    };
+    live_agent_loop(a, sh, pack, merge);
+}
+
+// Persistent driver (cf. fim2d_persist_kernel): one launch per solve, device FIFO of tiles.  A live
+// launch (a.live: a decomposition block on dd.solve_live) keeps workgroup 0 as its halo agent.
 template <typename R, int NL>
 __global__ __launch_bounds__(kThreads) void fim2dl_persist_kernel(Fim2dArgs a) {
     constexpr int TH = kRowsOf<R>;
     __shared__ TileLdsL<R, TH> L;
+    if (a.live && blockIdx.x == 0) {
+        __shared__ unsigned sh[4];
+        live_agent_layered<R, NL>(a, sh);
+        return;
+    }
     constexpr R INF = Real<R>::inf();
     const R INFS[4] = {INF, INF, INF, INF};
     for (int i = threadIdx.x; i < kGuard * kLds; i += kThreads) {  // guard rows: read by sweeps, never lowered
@@ -547,7 +617,6 @@ __global__ void fim2dl_seed_kernel(Fim2dArgs a, int64_t gx, int64_t gy, int64_t 
     qpush(a, (int)(gy / th) * a.ntx + (int)(gx / kTile), kSelf | kVisited);  // T not all +inf
 }
 
-__global__ void fim2dl_rewind_kernel(Fim2dArgs a) { *a.qhead = *a.qtail; }
 
 // flag |= 1 if layer z of the [HW][L] volume holds a finite cost
 template <typename R>
@@ -735,8 +804,8 @@ hipError_t fim2dl_persist(const Fim2dArgs& a, int nl, bool f64, int grid, hipStr
             default: return hipErrorInvalidValue;
         }
     }
-    hipLaunchKernelGGL(fim2dl_rewind_kernel, dim3(1), dim3(1), 0, st, a);
-    return hipGetLastError();
+    // the queue rewind of fim2d.hip (with bands: FIFO leftovers of the last dispatch dropped, bits cleared)
+    return fim2d_qrewind(a, st);
 }
 
 hipError_t layer_finite(const void* cost, bool f64, int64_t hw, int64_t L, int64_t z, int* d_flag, hipStream_t st) {

@@ -339,11 +339,17 @@ __device__ __forceinline__ void prio_put_overlap(const Fim2dArgs& a, int tile, f
         band_put_slot(a, b, tile);
     }
 }
-// claim a taken entry: pending -> busy (stale entries -- the tile busy, or no longer pending -- fail)
-__device__ __forceinline__ bool prio_claim(const Fim2dArgs& a, int tile, unsigned& trig) {
+// claim a taken entry: pending -> busy (stale entries -- the tile busy, or no longer pending -- fail).
+// cleared: the entry came from a band and its membership bit was just cleared (qgrab_prio) -- that
+// clear is in flight beside the state load below, which may have been served before it.  A put that
+// still saw the bit made the tile pending before it (and returned), so when the load says "not
+// claimable" the state is loaded again once the clear has completed: a pending tile whose put was
+// dropped for this entry is served by this claim, never left without an entry.
+__device__ __forceinline__ bool prio_claim(const Fim2dArgs& a, int tile, unsigned& trig, bool cleared = false) {
     unsigned old = __hip_atomic_load(&a.qstate[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // (qgrab_prio's membership-bit clear, in flight beside the load above, completes before the CAS)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the clear, too)
+    if (cleared && ((old & kBusy) || !(old & kPending)))
+        old = __hip_atomic_load(&a.qstate[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (;;) {
         if ((old & kBusy) || !(old & kPending)) return false;
         const unsigned prev = atomicCAS(&a.qstate[tile], old, kBusy | kVisited);
@@ -653,12 +659,12 @@ __device__ __forceinline__ int qgrab_prio(const Fim2dArgs& a, unsigned& trig) {
                     __hip_atomic_store(slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     const int tl = (int)((v & kSlotTileMask) - 1u);
                     const unsigned tag = v >> kBandTagShift;
-                    // an entry from band tag - 1: its membership bit is cleared BEFORE the claim's
-                    // CAS (a put that still saw the bit made the tile pending first, so this claim
-                    // serves it; a put after the clear makes a new entry).  Issued beside the
-                    // claim's state load, both awaited before the CAS (prio_claim).
+                    // an entry from band tag - 1: its membership bit is cleared before the claim
+                    // decides (a put that still saw the bit made the tile pending first, so this
+                    // claim serves it; a put after the clear makes a new entry).  Issued beside the
+                    // claim's state load (prio_claim re-loads the state when that load came first).
                     if (tag) atomicAnd(&a.bmem[tl], ~(1ull << (tag - 1u)));
-                    got = prio_claim(a, tl, tg) ? tl : -1;
+                    got = prio_claim(a, tl, tg, tag != 0u) ? tl : -1;
                     qcount(a, got >= 0 ? 3 : 4);
                 }
                 got = __shfl(got, 0);
@@ -685,6 +691,70 @@ __device__ __forceinline__ int qgrab_prio(const Fim2dArgs& a, unsigned& trig) {
             }
             __builtin_amdgcn_s_sleep(EIK_PRIO_SLEEP);
         }
+    }
+}
+
+// ------------------------------------------------------------------ live DD halo agent
+// The mailbox protocol of a live launch's halo agent (workgroup 0 -- the first one dispatched, so it
+// runs even when other work on the device keeps some of the launch's workgroups from being resident;
+// those start late and find the solve over).  The host posts one command at a time in pinned memory
+// (LiveBox, eik_kernels.hpp): PACK (snapshot the tiles pending or busy, then `pack(par, skip_busy)`
+// stores this block's edges into the neighbours' receive strips of parity par, system-scope stores
+// and a system release fence), MERGE (system acquire, then `merge(par, count)` min-merges the
+// received strips into the ghosts, queues the edge tiles whose ghost dropped and adds the dropped
+// cells to *count) and RELEASE (end the launch).  Every wait is bounded by qtimeout.  The solver
+// supplies pack / merge (fim2d.hip: one value per edge cell; fim2dl.hip: nl values).
+template <class Pack, class Merge>
+__device__ __forceinline__ void live_agent_loop(const Fim2dArgs& a, unsigned* sh, Pack&& pack, Merge&& merge) {
+    LiveBox* box = a.live;
+    const int tid = threadIdx.x;
+    unsigned last = 0;
+    for (;;) {
+        if (tid == 0) {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            unsigned s;
+            for (;;) {
+                s = __hip_atomic_load(&box->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (s != last) break;
+                if (__hip_atomic_load(a.qerror, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
+                    __builtin_amdgcn_s_memrealtime() - t0 > a.qtimeout) {
+                    atomicOr(a.qerror, 1u);
+                    s = ~0u;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(4);
+            }
+            sh[0] = s;
+            sh[1] = s == ~0u ? 0u : __hip_atomic_load(&box->cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            sh[2] = (unsigned)__hip_atomic_load(a.qactive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sh[3] = 0u;
+        }
+        __syncthreads();
+        const unsigned s = sh[0], op = sh[1] & 0xffu, par = (sh[1] >> 8) & 1u;
+        if (s == ~0u) {  // timed out: make the solvers leave too
+            if (tid == 0) __hip_atomic_store(a.qhold, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        last = s;
+        if (op == kLivePack) {  // the snapshot (sh[2]) was taken before any T load
+            pack(par, a.live_pack && sh[2] != 0u);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: peer stores complete
+        } else if (op == kLiveMerge) {
+            // the strips were stored by peer GPUs: drop any stale cached copy before reading
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            merge(par, &sh[3]);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            if (op == kLivePack) __hip_atomic_store(&box->active, sh[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (op == kLiveMerge) __hip_atomic_store(&box->changed, sh[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (op == kLiveRelease) __hip_atomic_store(a.qhold, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&box->error, __hip_atomic_load(a.qerror, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&box->done, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        if (op == kLiveRelease) return;
+        __syncthreads();  // sh[] is rewritten by the next command
     }
 }
 

@@ -363,6 +363,16 @@ class LiveGpuLocal(GpuLocal):
         return self.fim.release()
 
 
+class LiveGpuLocalLayered(LiveGpuLocal):
+    """solve_live adapter over eikonal.Fim3dLayered: a block of a few-layer 3D volume
+    on the live schedule -- the layered kernel's workgroup 0 is the halo agent, strips of nl values per
+    edge cell (IpcHalo with elem_bytes = nl x the element size).  goal: the block-local (x, y, z) or
+    x < 0."""
+
+    def start(self, cost, T, goal, stream):
+        GpuLocalLayered.start(self, cost, T, goal, stream)
+
+
 def halo_consistent(block, T, ghosts, group=None):
     """After a converged solve every ghost strip equals the neighbour's final edge of T exactly
     (the last round packed the final edges and merged them).  Checks the halo transport end to

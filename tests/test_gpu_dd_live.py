@@ -417,3 +417,108 @@ def test_c5_split_2x1_processes():
     assert np.array_equal(np.isfinite(Tdd), fin)
     rel = np.abs(Tdd[fin] - ref[fin]) / np.maximum(ref[fin], 1e-30)
     assert rel.max() <= 1e-11, rel.max()
+
+
+def _layered_live_worker(rank, world, port, H, W, goal, q, f64):
+    """One rank of a C5-style volume split in x-y on the LIVE schedule: eikonal.Fim3dLayered on its
+    block, the layered kernel's halo agent storing nl values per edge cell into the neighbours'
+    hipIpc strips (dd.IpcHalo with nl x the element size), the per-round vote over shared memory."""
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "planning-motion_planning_amd"))
+    import torch.distributed as dist
+
+    import eikonal
+    from eikonal import _lib as L
+    from eikonal import dd
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        px, py = dd.SPLITS[world]
+        blk = dd.Block(H, W, px, py, rank)
+        dt = torch.float64 if f64 else torch.float32
+        vol = _volume5(H, W, goal)
+        c = torch.from_numpy(np.ascontiguousarray(vol[blk.y0:blk.y1, blk.x0:blk.x1])).to(dev, dt)
+        T = torch.empty_like(c)
+        ctx = eikonal.Context(0)
+        ctx.set_option(L.OPT_GRID, max(2, 3 * torch.cuda.get_device_properties(dev).multi_processor_count // (4 * world)))
+        ctx.set_option(L.OPT_QTIMEOUT, 20.0)
+        nl = 3
+        _, _, ghost = dd.make_strips(blk, dt, dev, float("inf"), per_cell=nl)
+        fim = eikonal.Fim3dLayered(ctx, blk.h, blk.w, 5, 1, nl, L.EIK_F64 if f64 else L.EIK_F32)
+        loc = dd.LiveGpuLocalLayered(fim, ghost)
+        halo = dd.IpcHalo(ctx, blk, (8 if f64 else 4) * nl)
+        vote = dd.NodeVote() if world > 2 else None
+        lg = blk.local_goal(goal[0], goal[1])
+        res = []
+        for _ in range(2):  # twice: the strips and the solver are reused
+            loc.start(c, T, (lg[0], lg[1], goal[2]), torch.cuda.current_stream(dev).cuda_stream)
+            rounds = dd.solve_live(loc, blk, halo, vote=vote)
+            torch.cuda.synchronize()
+            res.append(T.cpu().double().numpy())
+        dist.barrier()
+        halo.close()
+        if vote is not None:
+            vote.close()
+        q.put((rank, blk.y0, blk.y1, blk.x0, blk.x1, res, rounds, None))
+        fim.close()
+        ctx.close()
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, 0, 0, 0, 0, None, 0, _why(rank, e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,f64", [(2, True), (4, True), (4, False)])
+def test_c5_split_live_processes(world, f64):
+    """SURVEY §8(e), C5 across GPUs on the LIVE schedule (round 6): a 768 x 1024 x 3 volume (z-padded
+    to 5) split 2 x 1 / 2 x 2 over processes sharing cuda:0, one persistent layered launch per block
+    whose halo agent exchanges nl values per edge cell while the block solves.  The assembled field
+    equals the single-domain layered solve (eik_tmap3d): masks equal, <= 1e-11 (fp64) / 1e-5 (fp32)
+    relative, twice in a row on the same solvers and strips."""
+    import torch.multiprocessing as mp
+
+    import eikonal
+
+    H, W = 768, 1024
+    goal = (W // 3, H // 2, 2)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_layered_live_worker, args=(r, world, port, H, W, goal, q, f64)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        parts = [q.get(timeout=240) for _ in range(world)]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    errs = [x[-1] for x in parts if x[-1]]
+    assert not errs, "\n".join(errs)
+    vol = _volume5(H, W, goal)
+    if not f64:
+        vol = vol.astype(np.float32).astype(np.float64)
+    ectx = eikonal.Context(0)
+    try:
+        ref = ectx.tmap3d(vol if f64 else vol.astype(np.float32), np.array(goal),
+                          dtype=np.float64 if f64 else np.float32).astype(np.float64)
+    finally:
+        ectx.close()
+    inner = (slice(None), slice(None), slice(1, 4))
+    for k in range(2):
+        Tdd = np.full((H, W, 5), np.nan)
+        for _, y0, y1, x0, x1, res, rounds, _ in parts:
+            Tdd[y0:y1, x0:x1] = res[k]
+            assert rounds >= 2
+        Tk, R = Tdd[inner], ref[inner]
+        fin = np.isfinite(R)
+        assert fin.mean() > 0.5
+        assert np.array_equal(np.isfinite(Tk), fin)
+        rel = np.abs(Tk[fin] - R[fin]) / np.maximum(R[fin], 1e-30)
+        assert rel.max() <= (1e-11 if f64 else 1e-5), rel.max()

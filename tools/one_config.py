@@ -23,7 +23,7 @@ def main():
     steps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    stream = torch.cuda.Stream(dev)
+    stream = torch.cuda.current_stream(dev)  # the stream the inputs are generated on (a side stream raced them)
     ctx = eikonal.Context(0, options=L.options_from_env())  # EIK_OPTIONS A/B hook
     tdt, edt = (torch.float64, L.EIK_F64) if dt == "f64" else (torch.float32, L.EIK_F32)
     if cfg == "C2":  # configs[1], the headline raster
