@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 O=gpurun_out
 LIBS=${LIBS:-"lib_alt lib"}
 for v in $LIBS; do
-  EIKONAL_LIB=planning-motion_planning_amd/$v/libeikonal.so timeout -k 10 300 python -u -m pytest tests/test_gpu_fim2d.py -x -q --timeout 120 --timeout-method thread > $O/ab_tests_$v.log 2>&1 || { echo "tests $v rc=$?"; tail -n 30 $O/ab_tests_$v.log; exit 1; }
+  EIKONAL_LIB=planning-motion_planning_amd/$v/libeikonal.so timeout -k 10 300 python -u -m pytest ${AB_TESTS:-tests/test_gpu_fim2d.py} -x -q --timeout 120 --timeout-method thread > $O/ab_tests_$v.log 2>&1 || { echo "tests $v rc=$?"; tail -n 30 $O/ab_tests_$v.log; exit 1; }
   echo "$v: $(tail -n 1 $O/ab_tests_$v.log)"
 done
 for i in 1 2; do

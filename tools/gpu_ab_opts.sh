@@ -1,11 +1,11 @@
 # A/B of solver options (EIK_OPTIONS strings) on one library, alternating, 2 rounds:
-#   OPTS="|FRESH_FIRST=1" bash tools/gpu_ab_opts.sh [bench args...]     ('|'-separated; empty = defaults)
+#   OPTS="-|FRESH_FIRST=1" bash tools/gpu_ab_opts.sh [bench args...]     ('|'-separated; "-" = the defaults)
 export TMPDIR=/tmp
 O=gpurun_out; mkdir -p $O
-IFS='|' read -ra VARIANTS <<< "${OPTS:-|}"
+IFS='|' read -ra VARIANTS <<< "${OPTS:--}"
 for i in 1 2; do
   for j in "${!VARIANTS[@]}"; do
-    v="${VARIANTS[$j]}"
+    v="${VARIANTS[$j]}"; [ "$v" = "-" ] && v=""
     EIK_OPTIONS="$v" timeout -k 10 300 python bench.py --no-cpu-baseline "$@" > $O/abo_$j.json 2> $O/abo_$j.err || { echo "bench [$v] rc=$?"; tail -n 20 $O/abo_$j.err; exit 1; }
     python - "$j" "$v" <<'PY'
 import json, sys
