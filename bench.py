@@ -932,6 +932,17 @@ def bench_costmap(ctx, dev, stream, steps, goal, N=4096, res=0.05):
         rp["r"] = ctx.rover_path(Zh, q)
 
     sec3 = timed_loop(step1, max(2, steps // 2))
+    default_join = [int(v) for v in rp["r"][2]]
+    # the same step with the reference's own band and LIFO ties (EIK_OPT_EXACT_BAND, bidir_exact.hip)
+    ctx.set_option(L.OPT_EXACT_BAND, 1)
+    try:
+        sec4 = timed_loop(step1, max(2, steps // 2))
+        xi = ctx.exact_info()
+    finally:
+        ctx.set_option(L.OPT_EXACT_BAND, 0)
+    exact = {"ms": round(sec4 * 1e3, 3), "replay_ms": round(xi["ms"], 3), "passes": xi["passes"],
+             "sweeps": xi["sweeps"], "tie_launches": xi["tie_launches"], "node_join": [int(v) for v in rp["r"][2]],
+             "join_equals_default": [int(v) for v in rp["r"][2]] == default_join}
     return {"workload": f"cost raster of the planner (Coupled_motion_planner.py:1101-1216) from a {N}x{N} DEM "
                         f"(terrain seed 42, res {res} m), f64",
             "value": round(N * N / sec / 1e9, 4), "unit": "Gcells/s", "ms_per_step": round(sec * 1e3, 3),
@@ -941,7 +952,7 @@ def bench_costmap(ctx, dev, stream, steps, goal, N=4096, res=0.05):
             "planner_step1": {"workload": "Coupled_motion_planner.py:1097-1258 via eik_rover_path_f64: host DEM -> "
                                           "cost raster -> biComputeTmap (2 x fp64 fronts) -> 2 GDM paths -> roverPath",
                               "ms": round(sec3 * 1e3, 3), "waypoints": int(len(rp["r"][0])),
-                              "node_join": [int(v) for v in rp["r"][2]]}}
+                              "node_join": default_join, "exact_band": exact}}
 
 
 def host_cpu():

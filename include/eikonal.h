@@ -125,8 +125,14 @@ typedef enum {
     EIK_OPT_PRIO_RING = 17,  /* slots per priority band (rounded up to a power of two; 0, the
                                 default: >= 2 x the tiles).  A band whose ring fills stops the
                                 launch; eik_fim2d_solve then solves again with the FIFO.         */
-    EIK_OPT_PRIO_DISPATCH = 18 /* band entries moved to the FIFO per dispatch, 1..64 (0, the
+    EIK_OPT_PRIO_DISPATCH = 18, /* band entries moved to the FIFO per dispatch, 1..64 (0, the
                                 default: 64 on maps of >= 16384 tiles, else 16)                 */
+    EIK_OPT_EXACT_BAND = 19  /* biComputeTmap / rover path: 1 replays the reference's sequential
+                                narrow band in pop order from the converged fields (csrc/
+                                bidir_exact.hip): its tentative band values, its LIFO order of
+                                equal T and so its nodeJoin, bit for bit; 0 (default) = band cells
+                                at their relaxed values (GPU <= reference <= 1.03 x GPU), ties
+                                by node index                                                   */
 } eik_option;
 
 typedef enum { EIK_MODE_LIST = 0, EIK_MODE_PERSISTENT = 1 } eik_mode;
@@ -153,7 +159,8 @@ int eik_tmap2d_f64(eik_ctx* ctx, const double* cost, int64_t H, int64_t W, int64
  * evaluated on the device from the two fields' pop ranks (the meeting iteration k).  TmapG/TmapS
  * are the fronts' PARTIAL fields at that iteration, as the reference returns them: the source and
  * its k first pops (rank <= k) and the narrow band around them at their values, +inf elsewhere
- * (fp64; exact ties of T are ranked by node index, the reference pops them LIFO). */
+ * (fp64; band values relaxed and exact ties of T ranked by node index, or with EIK_OPT_EXACT_BAND
+ * the reference's own band values, LIFO ties and nodeJoin). */
 int eik_tmap2d_bidir_f64(eik_ctx* ctx, const double* cost, int64_t H, int64_t W, int64_t gx, int64_t gy,
                          int64_t sx, int64_t sy, double* TG, double* TS, uint32_t join[2]);
 
@@ -171,6 +178,11 @@ int eik_bidir_join_f64(eik_ctx* ctx, const double* TG, const double* TS, int64_t
  * start front), out[4..5] cells the join ranked per front, out[6..7] band cells relaxed per front,
  * out[8..9] the band relaxation's sweeps per front. */
 int eik_fronts_info(const eik_ctx* ctx, int64_t out[10]);
+
+/* The last biComputeTmap / rover path's exact band replay (EIK_OPT_EXACT_BAND): out[0] re-ranking
+ * passes, out[1..2] relaxation sweeps (goal, start front), out[3] tie-run launches, out[4] its
+ * device time in microseconds; all 0 when it did not run. */
+int eik_exact_info(const eik_ctx* ctx, int64_t out[5]);
 
 /* B independent maps (goal sweep / terrain Monte-Carlo): cost, T: B*H*W; goals: B x (x, y). */
 int eik_tmap2d_batch_f32(eik_ctx* ctx, const float* cost, int64_t B, int64_t H, int64_t W, const int64_t* goals,

@@ -831,6 +831,21 @@ hipError_t fronts_clean(double* d_T, int64_t n, FrontsCheck* chk, hipStream_t st
 
 size_t bidir_join_work_bytes(int64_t n) { return layout(nullptr, n).total; }
 
+// the join's pop ranks per front (after bidir_join on d_work): UINT_MAX for cells not ranked
+void bidir_join_ranks(const void* d_work, int64_t n, const unsigned** rg, const unsigned** rs) {
+    const JoinLayout L = layout(const_cast<void*>(d_work), n);
+    *rg = L.rg;
+    *rs = L.rs;
+}
+
+// the packed join of two rank arrays (join_min_kernel) into *d_best (set to ~0 first by the caller)
+hipError_t bidir_join_min(const unsigned* d_rg, const unsigned* d_rs, int64_t n, unsigned long long* d_best,
+                          hipStream_t st) {
+    const unsigned jgrid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(kPassBlocks, (n + 255) / 256));
+    hipLaunchKernelGGL(join_min_kernel, dim3(jgrid), dim3(256), 0, st, d_rg, d_rs, n, d_best);
+    return hipGetLastError();
+}
+
 // the band relaxation's band cells and sweeps per front (after bidir_partial with a cost)
 hipError_t bidir_band_stats(const void* d_work, int64_t n, unsigned out[4], hipStream_t st) {
     const JoinLayout L = layout(const_cast<void*>(d_work), n);

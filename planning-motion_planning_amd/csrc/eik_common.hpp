@@ -26,6 +26,19 @@ template <> struct Real<double> {
 //   both neighbours inf -> inf;  one inf -> other + c;  c < |a-b| -> min + c;
 //   else 0.5 * (a + b + sqrt(2c^2 - (a-b)^2)).
 // Branch-free: hi == inf covers the first two branches (lo + c, inf + c = inf).
+// getEikonal FastMarching.py:17-29 in its own operation order, IEEE fp64 without contraction,
+// correctly rounded sqrt (np.power(x, 2) of a numpy scalar is the exact product; the oracle's
+// orc_eikonal): the exact band replay (bidir_exact.hip) and its fronts' solve (fim2d.hip REF)
+__device__ __forceinline__ double eik_ref(double thor, double tver, double c) {
+#pragma clang fp contract(off)
+    const double inf = Real<double>::inf();
+    if (thor == inf) return tver == inf ? inf : tver + c;
+    if (tver == inf) return thor + c;
+    const double d = thor - tver;
+    if (c < __builtin_fabs(d)) return __builtin_fmin(thor, tver) + c;
+    return 0.5 * (thor + tver + __builtin_sqrt(2.0 * (c * c) - d * d));
+}
+
 template <typename R>
 __device__ __forceinline__ R godunov2(R a, R b, R c) {
     const R lo = a < b ? a : b;

@@ -42,6 +42,9 @@ struct Fim2dArgs {
     // activates no neighbour -- every cell whose converged T is <= tcap depends only on cells below
     // it, so it still converges exactly; nullptr: no cap (honoured by the fp64 persistent kernel only)
     const double* tcap;
+    // EIK_OPT_EXACT_BAND's fronts (eikonal_api.cpp solve_fronts): fp64 persistent solves step in the
+    // reference's getEikonal arithmetic (fim2d.hip sweep_quadrant REF)
+    int ref_arith;
     // every tile's west / east edge column, [tile][2][kTile] R, kept equal to T's (fim2d.hip kEcol): the
     // west / east halo of a tile visit is one contiguous 64-cell read instead of 64 rows' lines
     void* ecol;
@@ -250,6 +253,19 @@ hipError_t bidir_band_stats(const void* d_work, int64_t n, unsigned out[4], hipS
 hipError_t bidir_partial(double* d_TG, double* d_TS, int64_t H, int64_t W, const void* d_work,
                          const unsigned long long* d_best, hipStream_t st, const double* d_cost = nullptr,
                          unsigned* d_viol = nullptr);
+void bidir_join_ranks(const void* d_work, int64_t n, const unsigned** rg, const unsigned** rs);
+hipError_t bidir_join_min(const unsigned* d_rg, const unsigned* d_rs, int64_t n, unsigned long long* d_best,
+                          hipStream_t st);
+// EIK_OPT_EXACT_BAND (bidir_exact.hip): the reference's own partial fields and nodeJoin, replayed in pop
+// order from the join's ranks d_rg / d_rs (members[f] cells ranked per front) over the device cost;
+// d_TG / d_TS (the converged fields) become the partial fields, *d_best the exact join.  info
+// (accumulated): passes, relaxation sweeps G, S, tie-run launches.  hipErrorNotReady: no fixed point
+// within the caps; hipErrorNotSupported: a run of more than 4096 exactly equal T (a zero-cost region).
+size_t bidir_exact_work_bytes(int64_t n, int64_t m0, int64_t m1);
+hipError_t bidir_exact(double* d_TG, double* d_TS, const double* d_cost, int64_t H, int64_t W, int64_t gnode,
+                       int64_t snode, const unsigned* d_rg, const unsigned* d_rs, const int64_t members[2],
+                       void* d_work, size_t work_bytes, unsigned long long* d_best, hipStream_t st,
+                       unsigned long long info[4]);
 // the capped fronts' device block (eikonal_api.cpp solve_fronts)
 struct FrontsCheck {
     double caps[2];                   // per front: activation cap of the full-resolution solve

@@ -171,6 +171,9 @@ struct eik_ctx {
     DevBuf fronts;                     // capped fronts: coarse cost (2 maps) | coarse T (2 maps) | FrontsCheck
     int64_t fronts_info[10] = {};      // eik_fronts_info: capped, fallback, kept G / S, members G / S,
                                        // band cells G / S, band relaxation sweeps G / S
+    bool exact_band = false;           // EIK_OPT_EXACT_BAND: replay the reference's band (bidir_exact.hip)
+    DevBuf exact;                      // its scratch: events, ranks, sort keys
+    unsigned long long exact_info[5] = {};  // eik_exact_info: passes, sweeps G / S, tie launches, microseconds
     DevBuf cm_u8, cm_i32, cm_f32, cm_f64;  // cost-builder scratch
     DevBuf arm;                            // end-effector volume scratch (arm.hip)
     int resident_l[2][5] = {};  // co-resident workgroups of fim2dl_persist_kernel<R, nl> (f32, f64)
@@ -402,6 +405,7 @@ int eik_set_option(eik_ctx* c, int opt, double v) {
         case EIK_OPT_PRIO_DISPATCH: c->prio_dispatch = v < 0 ? 0 : (int)std::min(v, 64.0); break;
         case EIK_OPT_LAYER_PLANAR: c->layer_planar = v != 0; break;
         case EIK_OPT_PATH_LOOP: c->path_loop = std::max(0, std::min(4, (int)v)); break;
+        case EIK_OPT_EXACT_BAND: c->exact_band = v != 0; break;
         case EIK_OPT_FRONTS_CAP: c->fronts_cap = v <= 0 ? 0.0 : v == 1 ? kFrontsMargin : std::max(1.0, v); break;
         default: return set_err(c, EIK_ERR_ARG, "unknown option %d", opt);
     }
@@ -1281,13 +1285,52 @@ int eik_tmap2d_batch_f32(eik_ctx* c, const float* cost, int64_t B, int64_t H, in
 // dT[n:2n] (start front), in place; *best = the packed join (~0: the fronts never meet).  d_cost
 // (the fronts' raster): band cells by the band relaxation (bidir.hip), else at their full-field
 // values; d_chk: the capped fronts' check.  Ends with the stream synchronised on *best.
+// src (with d_cost): the goal's and the start's linear index, for EIK_OPT_EXACT_BAND's replay.
 static int join_and_partial(eik_ctx* c, double* dT, int64_t n, int64_t H, int64_t W, unsigned long long* best,
                             int64_t members[2], const double* d_cost = nullptr, FrontsCheck* d_chk = nullptr,
-                            FrontsCheck* h_chk = nullptr) {
+                            FrontsCheck* h_chk = nullptr, const int64_t* src = nullptr) {
     hipStream_t st = c->stream;
     HIPCHK(c, c->work.ensure(bidir_join_work_bytes(n)));
     HIPCHK(c, c->misc.ensure(64));
     HIPCHK(c, bidir_join(dT, dT + n, n, c->work.p, c->work.bytes, (unsigned long long*)c->misc.p, st, members));
+    if (d_cost && src && c->exact_band) {
+        // the reference's own band values, LIFO ties and nodeJoin, replayed from the join's ranks
+        const unsigned *rg = nullptr, *rs = nullptr;
+        bidir_join_ranks(c->work.p, n, &rg, &rs);
+        HIPCHK(c, c->exact.ensure(bidir_exact_work_bytes(n, members[0], members[1])));
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        HIPCHK(c, hipEventCreate(&e0));
+        HIPCHK(c, hipEventCreate(&e1));
+        HIPCHK(c, hipEventRecord(e0, st));
+        unsigned long long info[4] = {0, 0, 0, 0};
+        const hipError_t e = bidir_exact(dT, dT + n, d_cost, H, W, src[0], src[1], rg, rs, members, c->exact.p,
+                                         c->exact.bytes, (unsigned long long*)c->misc.p, st, info);
+        if (e == hipErrorNotReady || e == hipErrorNotSupported) {
+            (void)hipEventDestroy(e0);
+            (void)hipEventDestroy(e1);
+            return set_err(c, EIK_ERR_NOCONVERGE, e == hipErrorNotReady
+                                                      ? "biComputeTmap: the exact band replay did not settle"
+                                                      : "biComputeTmap: the exact band replay met a run of more than "
+                                                        "4096 cells of exactly equal T (a zero-cost region)");
+        }
+        HIPCHK(c, e);
+        HIPCHK(c, hipEventRecord(e1, st));
+        HIPCHK(c, hipMemcpyAsync(best, c->misc.p, sizeof *best, hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipStreamSynchronize(st));
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        for (int q = 0; q < 4; ++q) c->exact_info[q] = info[q];
+        c->exact_info[4] = (unsigned long long)(ms * 1000.0f);
+        for (int q = 0; q < 4; ++q) c->fronts_info[6 + q] = 0;
+        if (d_chk) {
+            HIPCHK(c, hipMemcpyAsync(h_chk, d_chk, sizeof *h_chk, hipMemcpyDeviceToHost, st));
+            HIPCHK(c, hipStreamSynchronize(st));
+            h_chk->viol = 0;  // band values come from the replay's events, not from the capped field
+        }
+        return EIK_OK;
+    }
     {
         const hipError_t e = bidir_partial(dT, dT + n, H, W, c->work.p, (const unsigned long long*)c->misc.p, st, d_cost,
                                            d_chk ? &d_chk->viol : nullptr);
@@ -1322,7 +1365,15 @@ static int solve_fronts(eik_ctx* c, eik_fim2d* f, double* dcost, double* dT, con
                         unsigned long long* best) {
     hipStream_t st = c->stream;
     const int64_t n = H * W;
+    const int64_t src[2] = {g[1] * W + g[0], g[3] * W + g[2]};
     for (int64_t& v : c->fronts_info) v = 0;  // (join_and_partial fills the band entries)
+    for (auto& v : c->exact_info) v = 0;
+    // exact band: the fronts in the reference's arithmetic, so the replay mostly confirms their values
+    struct RefArith {
+        eik_fim2d* f;
+        RefArith(eik_fim2d* f_, bool on) : f(f_) { f->a.ref_arith = on ? 1 : 0; }
+        ~RefArith() { f->a.ref_arith = 0; }
+    } ref_guard(f, c->exact_band);
     HIPCHK(c, c->work.ensure(bidir_join_work_bytes(n)));
     const bool capped = c->fronts_cap > 0 && n >= kFrontsCapCells && std::min(H, W) >= 256;
     if (capped) {
@@ -1359,7 +1410,7 @@ static int solve_fronts(eik_ctx* c, eik_fim2d* f, double* dcost, double* dT, con
         HIPCHK(c, fronts_clean(dT, n, chk, st));
         FrontsCheck h{};
         int64_t mem[2] = {0, 0};
-        rc = join_and_partial(c, dT, n, H, W, best, mem, dcost, chk, &h);
+        rc = join_and_partial(c, dT, n, H, W, best, mem, dcost, chk, &h, src);
         if (rc) return rc;
         const unsigned long long k = *best >> 30;
         const bool ok = *best != ~0ull && h.viol == 0 && k < h.kept[0] && k < h.kept[1];
@@ -1374,12 +1425,18 @@ static int solve_fronts(eik_ctx* c, eik_fim2d* f, double* dcost, double* dT, con
     int rc = eik_fim2d_solve(f, dcost, dT, g, st);
     if (rc) return rc;
     int64_t mem[2] = {0, 0};
-    rc = join_and_partial(c, dT, n, H, W, best, mem, dcost);
+    rc = join_and_partial(c, dT, n, H, W, best, mem, dcost, nullptr, nullptr, src);
     if (!capped) {
         c->fronts_info[4] = mem[0];
         c->fronts_info[5] = mem[1];
     }
     return rc;
+}
+
+int eik_exact_info(const eik_ctx* c, int64_t out[5]) {
+    if (!c || !out) return EIK_ERR_ARG;
+    for (int i = 0; i < 5; ++i) out[i] = (int64_t)c->exact_info[i];
+    return EIK_OK;
 }
 
 int eik_fronts_info(const eik_ctx* c, int64_t out[10]) {

@@ -203,7 +203,10 @@ __device__ __forceinline__ Cell<R> make_cell(R t, R c, int col) {
 #ifndef EIK_SWEEP_UNROLL_F32
 #define EIK_SWEEP_UNROLL_F32 8  // C4 fp32 +3 %, C2 / C3 within noise (profiles/r05v_sweep_unroll_f32_ab.log)
 #endif
-template <typename R, int DX, int DY, bool TRACK, class Hook>
+// REF (fp64, EIK_OPT_EXACT_BAND's fronts): the step in the reference's own getEikonal arithmetic
+// (eik_ref) instead of the chain form, so the converged field is the reference's closed values bit
+// for bit wherever its last update read the same upwind minima (bidir_exact.hip starts from it)
+template <typename R, int DX, int DY, bool TRACK, bool REF = false, class Hook>
 __device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lane, R keep, Hook&& hook) {
     constexpr int S = (int)sizeof(Cell<R>);
     constexpr int kRow = kLds * S;
@@ -269,7 +272,8 @@ __device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lan
                 // fp64: the DPP move cannot fold into a 64-bit min, so lanes 1.. take lane l-1's
                 // fresh value alone (it is at most the prefetched LDS value of the same cell, read
                 // one step earlier) and lane 0 keeps the halo column's LDS value (the DPP's old)
-                w = godunov2_chain(wave_shr1(cur, q_upx[u]), cur, q_c[u], c2x2);
+                if constexpr (REF) w = eik_ref(wave_shr1(cur, q_upx[u]), cur, q_c[u]);
+                else w = godunov2_chain(wave_shr1(cur, q_upx[u]), cur, q_c[u], c2x2);
                 lds_min(reinterpret_cast<R*>(base + gcur + off(u)), w);
                 if constexpr (TRACK) changed |= w < q_old[u] * keep;
                 cur = fmin_nn(w, q_old[u]);  // NaN (both-inf case): keeps old
@@ -287,9 +291,9 @@ __device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lan
     }
     return changed;
 }
-template <typename R, int DX, int DY, bool TRACK>
+template <typename R, int DX, int DY, bool TRACK, bool REF = false>
 __device__ __forceinline__ bool sweep_quadrant(Cell<R>* __restrict__ Ts, int lane, R keep) {
-    return sweep_quadrant<R, DX, DY, TRACK>(Ts, lane, keep, [](int) {});
+    return sweep_quadrant<R, DX, DY, TRACK, REF>(Ts, lane, keep, [](int) {});
 }
 
 // LDS of one tile visit
@@ -319,7 +323,7 @@ struct TileLds {
 // CAP: honour Fim2dArgs::tcap (the capped bidirectional fronts, eikonal_api.cpp solve_fronts) -- a
 // separate instantiation: the compare in the edge test cost the uncapped fp64 solve 4-5 % (C2 2.36
 // -> 2.47 ms, profiles/r04i_tcap_ab.log)
-template <typename R, bool COH, bool CAP = false>
+template <typename R, bool COH, bool CAP = false, bool REF = false>
 __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileLds<R>& L, R keep) {
     constexpr R INF = Real<R>::inf();
     Cell<R>* const Ts = L.Tc + kGuard * kLds;
@@ -491,10 +495,10 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
         bool last_changed = false;
         if (a.max_rounds == 1) {  // single round: "changed" is read off the write-back below
             if (sweep) {
-                if (wave == 0)      sweep_quadrant<R, +1, +1, false>(Ts, lane, keep, hook);
-                else if (wave == 1) sweep_quadrant<R, -1, +1, false>(Ts, lane, keep, hook);
-                else if (wave == 2) sweep_quadrant<R, +1, -1, false>(Ts, lane, keep, hook);
-                else                sweep_quadrant<R, -1, -1, false>(Ts, lane, keep, hook);
+                if (wave == 0)      sweep_quadrant<R, +1, +1, false, REF>(Ts, lane, keep, hook);
+                else if (wave == 1) sweep_quadrant<R, -1, +1, false, REF>(Ts, lane, keep, hook);
+                else if (wave == 2) sweep_quadrant<R, +1, -1, false, REF>(Ts, lane, keep, hook);
+                else                sweep_quadrant<R, -1, -1, false, REF>(Ts, lane, keep, hook);
             } else {  // a wave without a sweep this pass still does its duties, in step order
                 for (int st = 0; st < 2 * kTile; st += kAhead) hook(st);
             }
@@ -503,10 +507,10 @@ __device__ __forceinline__ void process_tile(const Fim2dArgs& a, int tile, TileL
             for (int round = 0;; ++round) {
                 bool ch = false;
                 if (sweep) {
-                    if (wave == 0)      ch = sweep_quadrant<R, +1, +1, true>(Ts, lane, keep);
-                    else if (wave == 1) ch = sweep_quadrant<R, -1, +1, true>(Ts, lane, keep);
-                    else if (wave == 2) ch = sweep_quadrant<R, +1, -1, true>(Ts, lane, keep);
-                    else                ch = sweep_quadrant<R, -1, -1, true>(Ts, lane, keep);
+                    if (wave == 0)      ch = sweep_quadrant<R, +1, +1, true, REF>(Ts, lane, keep);
+                    else if (wave == 1) ch = sweep_quadrant<R, -1, +1, true, REF>(Ts, lane, keep);
+                    else if (wave == 2) ch = sweep_quadrant<R, +1, -1, true, REF>(Ts, lane, keep);
+                    else                ch = sweep_quadrant<R, -1, -1, true, REF>(Ts, lane, keep);
                 }
                 if (__any(ch) && lane == 0) atomicOr(&L.round, 1u << (round & 31));
                 __syncthreads();
@@ -804,7 +808,7 @@ __device__ __forceinline__ void live_agent(const Fim2dArgs& a, unsigned* sh) {
 // VGPRs -> 3 workgroups per CU; 4: <= 128 VGPRs -> 4 per CU, a few spills).  Large rasters
 // (maps of >= kWideTiles tiles: the throughput-bound regime) run the 4-wave form -- 16384^2 on one GPU
 // +10-15 %, 4096^2 -3 % (profiles/r02r_wps_ab.log).
-template <typename R, int WPS, bool CAP = false>
+template <typename R, int WPS, bool CAP = false, bool REF = false>
 __global__ __launch_bounds__(kThreads, WPS) void fim2d_persist_kernel(Fim2dArgs a) {
     __shared__ TileLds<R> L;
     if (a.live && blockIdx.x == 0) {
@@ -854,7 +858,7 @@ __global__ __launch_bounds__(kThreads, WPS) void fim2d_persist_kernel(Fim2dArgs 
         EIK_PROBE(6);
         tile = __builtin_amdgcn_readfirstlane(L.tile);
         if (tile < 0) break;  // uniform: solve finished (or failed)
-        process_tile<R, true, CAP>(a, tile, L, keep);  // sc1 loads; sc1 stores drained + barrier
+        process_tile<R, true, CAP, REF>(a, tile, L, keep);  // sc1 loads; sc1 stores drained + barrier
     }
     if (threadIdx.x == 0 && nvis) atomicAdd(a.visits, (unsigned long long)nvis);
 }
@@ -1039,7 +1043,11 @@ int fim2d_persist_resident(bool f64, int cus, bool wide) {
 hipError_t fim2d_persist(const Fim2dArgs& a, bool f64, int grid, hipStream_t st, bool wide, bool rewind) {
     // (a.tcap: fp64 only -- the fp32 kernels and list mode solve in full, which the capped fronts'
     // clean pass and check accept as well)
-    if (f64 && a.tcap)
+    if (f64 && a.ref_arith && a.tcap)
+        hipLaunchKernelGGL((fim2d_persist_kernel<double, 1, true, true>), dim3(grid), dim3(kThreads), 0, st, a);
+    else if (f64 && a.ref_arith)
+        hipLaunchKernelGGL((fim2d_persist_kernel<double, 1, false, true>), dim3(grid), dim3(kThreads), 0, st, a);
+    else if (f64 && a.tcap)
         hipLaunchKernelGGL((fim2d_persist_kernel<double, 1, true>), dim3(grid), dim3(kThreads), 0, st, a);
     else if (f64)
         hipLaunchKernelGGL((fim2d_persist_kernel<double, 1>), dim3(grid), dim3(kThreads), 0, st, a);

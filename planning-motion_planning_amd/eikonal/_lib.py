@@ -15,6 +15,7 @@ PATH_DONE, PATH_FALLBACK, PATH_ERROR = 0, 1, 2
 OPT_MAX_ROUNDS, OPT_SYNC_EVERY, OPT_TIMING, OPT_GRID, OPT_TOL, OPT_DELTA = 0, 1, 2, 3, 4, 5
 OPT_MODE, OPT_QTIMEOUT, OPT_MAX_VISITS, OPT_PASSES, OPT_FRESH_FIRST, OPT_SCHED, OPT_PATH_LOOP = 6, 7, 8, 9, 10, 11, 12
 OPT_FRONTS_CAP, OPT_LIVE_PACK, OPT_PRIO, OPT_LAYER_PLANAR, OPT_PRIO_RING, OPT_PRIO_DISPATCH = 13, 14, 15, 16, 17, 18
+OPT_EXACT_BAND = 19
 MODE_LIST, MODE_PERSISTENT = 0, 1
 
 i64 = C.c_int64
@@ -129,6 +130,7 @@ def lib():
         L.eik_tmap2d_bidir_f64.argtypes = [vp, _f64p, i64, i64, i64, i64, i64, i64, _f64p, _f64p, _u32p]
         L.eik_bidir_join_f64.argtypes = [vp, _f64p, _f64p, i64, i64, _f64p, _f64p, _u32p, _i64p]
         L.eik_fronts_info.argtypes = [vp, _i64p]
+        L.eik_exact_info.argtypes = [vp, _i64p]
         L.eik_tmap2d_batch_f32.argtypes = [vp, _f32p, i64, i64, i64, _i64p, _f32p]
         L.eik_path2d_f64.argtypes = [vp, _f64p, i64, i64, _f64p, _f64p, C.c_double, _f64p, i64, P(i64), P(C.c_int)]
         L.eik_gradient2d_f64.argtypes = [vp, _f64p, i64, i64, _f64p, _f64p]
@@ -194,7 +196,7 @@ def lib():
 
 EXPORTED = [
     "eik_version", "eik_create", "eik_destroy", "eik_last_error", "eik_set_option", "eik_get_stats",
-    "eik_tmap2d_f32", "eik_tmap2d_f64", "eik_tmap2d_bidir_f64", "eik_bidir_join_f64", "eik_fronts_info", "eik_tmap2d_batch_f32", "eik_path2d_f64",
+    "eik_tmap2d_f32", "eik_tmap2d_f64", "eik_tmap2d_bidir_f64", "eik_bidir_join_f64", "eik_fronts_info", "eik_exact_info", "eik_tmap2d_batch_f32", "eik_path2d_f64",
     "eik_gradient2d_f64", "eik_fim2d_create", "eik_fim2d_destroy", "eik_fim2d_set_ghosts", "eik_fim2d_start",
     "eik_fim2d_iterate", "eik_fim2d_solve", "eik_fim2d_pack_edges", "eik_fim2d_merge_ghost", "eik_fim2d_active",
     "eik_fim2d_stats", "eik_path2d_dev", "eik_selftest_walker_math", "eik_tmap3d_f32", "eik_tmap3d_f64",
@@ -352,6 +354,15 @@ class Context:
         self._chk(lib().eik_fronts_info(self._h, out))
         return {"capped": bool(out[0]), "fallback": bool(out[1]), "kept": out[2:4].tolist(),
                 "members": out[4:6].tolist(), "band": out[6:8].tolist(), "band_sweeps": out[8:10].tolist()}
+
+    def exact_info(self):
+        """The last tmap2d_bidir / rover_path's exact band replay (EIK_OPT_EXACT_BAND, eik_exact_info):
+        re-ranking passes, relaxation sweeps per front, tie-run launches, device time in ms (all 0: it
+        did not run)."""
+        out = np.zeros(5, np.int64)
+        self._chk(lib().eik_exact_info(self._h, out))
+        return {"passes": int(out[0]), "sweeps": out[1:3].tolist(), "tie_launches": int(out[3]),
+                "ms": out[4] / 1000.0}
 
     def path2d(self, T, init, end, tau=0.5):
         T = np.ascontiguousarray(T, dtype=np.float64)

@@ -125,6 +125,25 @@ def test_gpu_dropin_bidir_and_rover_path(golden):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("i", [0, 4])
+def test_gpu_dropin_bidir_exact_band(golden, monkeypatch, i):
+    """EIKONAL_EXACT_BAND=1: the drop-in's biComputeTmap returns the reference's outputs bit for bit
+    (b0: a uniform raster, LIFO ties), and the switch is read per call."""
+    b = golden("fmm2d_bidir")
+    p = f"b{i}_"
+    cost = b[p + "cost"].astype(np.float64)
+    goal, start = [int(v) for v in b[p + "goal"]], [int(v) for v in b[p + "start"]]
+    monkeypatch.setenv("EIKONAL_EXACT_BAND", "1")
+    TG, TS, join = FM.biComputeTmap(cost, goal, start)
+    assert np.array_equal(join, b[p + "join"])
+    for T, R in ((TG, b[p + "TG"]), (TS, b[p + "TS"])):
+        assert np.array_equal(T.view(np.uint64), R.view(np.uint64))
+    monkeypatch.setenv("EIKONAL_EXACT_BAND", "0")
+    FM.biComputeTmap(cost, goal, start)
+    assert FM._ctx().exact_info()["passes"] == 0
+
+
+@pytest.mark.gpu
 def test_gpu_dropin_3d(golden):
     v = golden("fmm3d")
     p = "v0_"

@@ -66,6 +66,34 @@ def test_rover_path_matches_oracle_chain(n, seed):
     assert np.hypot(got_p[:, 0] - xm, got_p[:, 1] - ym).min() >= 0.1
 
 
+@pytest.mark.parametrize("n,seed", [(160, 5), (224, 11)])
+def test_rover_path_exact_band_matches_oracle_chain(n, seed):
+    """The same chain with EIK_OPT_EXACT_BAND: the fronts' partial fields are the reference's own
+    (band values and LIFO ties replayed, csrc/bidir_exact.hip), so the rover path follows the oracle
+    chain's to the path kernel's tolerance on fields whose costs agree to 1e-12 -- not 0.01 cells."""
+    import eikonal
+    from eikonal import _lib as L
+
+    Z = terrain_np.dem(n, n, seed=seed) + 3.0
+    size = RES * n
+    cref, _ = PO.CO.cost_map(Z, RES, size)
+    cT = cref.T
+    sx, sy = free_cell(cT, int(0.78 * n), int(0.72 * n))
+    rx, ry = free_cell(cT, int(0.2 * n), int(0.25 * n))
+    xm, ym, xr, yr = RES * (sx + 1), RES * (sy + 1), RES * (rx + 1), RES * (ry + 1)
+    ref_p, ref_h, ref_j, _ = PO.rover_path(Z, xm, ym, xr, yr, 0.4, RES, size)
+    c = eikonal.Context(0)
+    try:
+        c.set_option(L.OPT_EXACT_BAND, 1)
+        got_p, got_h, got_j = c.rover_path(Z, planner.query(xm, ym, xr, yr, 0.4, RES, size))
+        assert c.exact_info()["passes"] >= 1
+    finally:
+        c.close()
+    assert np.array_equal(got_j, ref_j)
+    assert got_p.shape == ref_p.shape
+    assert np.abs(got_p[:, :2] - ref_p[:, :2]).max() / RES <= 1e-6
+
+
 def test_rover_path_unreachable():
     """Rover on the corner node (0, 0): both its neighbours are +inf border cells.  The reference's
     fronts still "meet" there by popping +inf band entries and return a degenerate path; the GPU
