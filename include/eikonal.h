@@ -127,12 +127,12 @@ typedef enum {
                                 launch; eik_fim2d_solve then solves again with the FIFO.         */
     EIK_OPT_PRIO_DISPATCH = 18, /* band entries moved to the FIFO per dispatch, 1..64 (0, the
                                 default: 64 on maps of >= 16384 tiles, else 16)                 */
-    EIK_OPT_EXACT_BAND = 19  /* biComputeTmap / rover path: 1 replays the reference's sequential
-                                narrow band in pop order from the converged fields (csrc/
-                                bidir_exact.hip): its tentative band values, its LIFO order of
-                                equal T and so its nodeJoin, bit for bit; 0 (default) = band cells
-                                at their relaxed values (GPU <= reference <= 1.03 x GPU), ties
-                                by node index                                                   */
+    EIK_OPT_EXACT_BAND = 19  /* biComputeTmap / rover path and fp64 FM3D early exits: 1 replays the
+                                reference's sequential narrow band in pop order from the converged
+                                fields (csrc/bidir_exact.hip): its tentative band values, its LIFO
+                                order of equal T and so its nodeJoin / closed set, bit for bit; 0
+                                (default) = band cells at their final (2D: relaxed) values (GPU <=
+                                reference <= 1.03 x GPU), ties by node index / strict < T[start] */
 } eik_option;
 
 typedef enum { EIK_MODE_LIST = 0, EIK_MODE_PERSISTENT = 1 } eik_mode;
@@ -179,7 +179,7 @@ int eik_bidir_join_f64(eik_ctx* ctx, const double* TG, const double* TS, int64_t
  * out[8..9] the band relaxation's sweeps per front. */
 int eik_fronts_info(const eik_ctx* ctx, int64_t out[10]);
 
-/* The last biComputeTmap / rover path's exact band replay (EIK_OPT_EXACT_BAND): out[0] re-ranking
+/* The last biComputeTmap / rover path's / FM3D early exit's exact band replay (EIK_OPT_EXACT_BAND): out[0] re-ranking
  * passes, out[1..2] relaxation sweeps (goal, start front), out[3] tie-run launches, out[4] its
  * device time in microseconds; all 0 when it did not run. */
 int eik_exact_info(const eik_ctx* ctx, int64_t out[5]);
@@ -210,7 +210,8 @@ int eik_tmap3d_f64(eik_ctx* ctx, const double* cost, int64_t H, int64_t W, int64
  * PARTIAL field -- cells popped before `start` (T < T[start]) and `start` at their final values,
  * the narrow band (finite cost, a closed 6-neighbour) at its converged full-field value -- <= the
  * reference's tentative value, which depends on its sequential update order --
- * and +inf elsewhere (eik_fim3d_early_exit).
+ * and +inf elsewhere (eik_fim3d_early_exit).  fp64 with EIK_OPT_EXACT_BAND: the reference's own
+ * closed set and band values, replayed in pop order (masks identical, values within 1e-11).
  * start == goal, a start outside the volume or an unreachable start -> the full field, as in the
  * reference (it never pops such a start). */
 int eik_tmap3d_early_f32(eik_ctx* ctx, const float* cost, int64_t H, int64_t W, int64_t L, const int64_t goal[3],

@@ -21,6 +21,7 @@ import numpy as np
 from numpy import array
 
 from eikonal import default_context, PATH_ERROR
+from eikonal._lib import OPT_EXACT_BAND
 
 _DTYPE = np.float32 if os.environ.get("EIKONAL_DTYPE", "float64") in ("float32", "f32") else np.float64
 
@@ -121,11 +122,15 @@ def interpolatePoint(point, mapI):
 
 def computeTmap(costMap, goal, start=None):
     """FastMarching3D.py:126-145 -> T[y, x, z] (float64, inf = unreached), early exit at `start`
-    (:141); start=None (no reference counterpart) returns the full field."""
+    (:141); start=None (no reference counterpart) returns the full field.  EIKONAL_EXACT_BAND=1 (fp64):
+    the early-exit field's band values and ties exactly as the reference's sequential band
+    (EIK_OPT_EXACT_BAND, csrc/bidir_exact.hip)."""
     cost = np.ascontiguousarray(costMap, dtype=_DTYPE)
     g = np.asarray(goal, dtype=np.int64).reshape(-1)[:3]
     s = None if start is None else np.asarray(start, dtype=np.int64).reshape(-1)[:3]
-    return _ctx().tmap3d(cost, g, dtype=_DTYPE, start=s).astype(np.float64, copy=False)
+    c = _ctx()
+    c.set_option(OPT_EXACT_BAND, 1 if os.environ.get("EIKONAL_EXACT_BAND", "0") not in ("", "0") else 0)
+    return c.tmap3d(cost, g, dtype=_DTYPE, start=s).astype(np.float64, copy=False)
 
 
 def getPathGDM(totalCostMap, initWaypoint, endWaypoint, tau):

@@ -55,14 +55,14 @@ constexpr int kTieBatch = 16;
 constexpr unsigned kMaxTieBatches = 1u << 16;
 
 struct Front {
-    const double* cost;  // H*W
-    double* T;           // the converged field on entry (init values); the partial field on exit
-    unsigned* rank;      // H*W: pop rank, kNoRank = not among the m ranked cells
+    const double* cost;  // the raster / volume
+    double* T;           // the converged field on entry (init values); the partial field on exit (2D)
+    unsigned* rank;      // per cell: pop rank, kNoRank = not among the m ranked cells
     unsigned* ord;       // m: the cell of each rank
-    double* ev;          // 4*H*W: events [cell][d], d = the direction of the popping neighbour
-    int64_t src;         // the front's source (closed before the first pop, :120 / :123)
+    double* ev;          // K per cell: events [cell][d], d = the direction of the popping neighbour
+    int64_t src;         // the front's source (closed before the first pop)
     unsigned m;
-    unsigned from;       // this pass: first rank re-initialised / re-keyed
+    unsigned from;       // this pass: first rank relaxed / re-keyed
 };
 
 struct Ctl {
@@ -71,56 +71,112 @@ struct Ctl {
     unsigned first_bad[2];  // this pass: first rank that moved against the relaxation's order
     unsigned stuck[2];      // a group did not settle within kGroupSweepCap sweeps
     unsigned longrun;       // a run of equal T too long for exact_ties_kernel (1), or not closed (2)
+    unsigned msel;          // FM3D: cells selected for ranking
+    double thr;             // FM3D: the selection's bound on T
 };
 
-// children / neighbours in the reference's order (:46-54): y - 1, y + 1, x - 1, x + 1
-__device__ __forceinline__ int64_t nb_of(int64_t i, int64_t x, int64_t y, int d, int64_t H, int64_t W) {
-    switch (d) {
-        case 0: return y > 0 ? i - W : -1;
-        case 1: return y + 1 < H ? i + W : -1;
-        case 2: return x > 0 ? i - 1 : -1;
-        default: return x + 1 < W ? i + 1 : -1;
+// The grids.  Children (= neighbours) in the reference's updateNode order, opposite directions
+// paired (d ^ 1); `solve` is its local update over the K neighbours' values as of a pop.
+// 2D, FastMarching.py:46-63: y - 1, y + 1, x - 1, x + 1; getEikonal(min(T[x+1], T[x-1]),
+// min(T[y+1], T[y-1]), cost).  Cells [y][x].
+struct Geo2 {
+    int64_t H, W;
+    static constexpr int K = 4;
+    struct Co {
+        int64_t x, y;
+    };
+    __device__ Co co(int64_t i) const {
+        const int64_t y = (unsigned)i / (unsigned)W;
+        return {i - y * W, y};
     }
-}
-__device__ __forceinline__ int64_t dx_of(int d) { return d < 2 ? 0 : (d == 2 ? -1 : 1); }
-__device__ __forceinline__ int64_t dy_of(int d) { return d >= 2 ? 0 : (d == 0 ? -1 : 1); }
+    __device__ int64_t nb(int64_t i, Co c, int d) const {
+        switch (d) {
+            case 0: return c.y > 0 ? i - W : -1;
+            case 1: return c.y + 1 < H ? i + W : -1;
+            case 2: return c.x > 0 ? i - 1 : -1;
+            default: return c.x + 1 < W ? i + 1 : -1;
+        }
+    }
+    __device__ Co step(Co c, int d) const {
+        return d < 2 ? Co{c.x, c.y + (d == 0 ? -1 : 1)} : Co{c.x + (d == 2 ? -1 : 1), c.y};
+    }
+    __device__ double solve(const double* v, double cost) const {
+        return eik_ref(__builtin_fmin(v[3], v[2]), __builtin_fmin(v[1], v[0]), cost);
+    }
+};
+// 3D, FastMarching3D.py:21-75: z - 1, z + 1, x - 1, x + 1, y + 1, y - 1 (node = [x, y, z]); Tx = Tx1 <
+// Tx2 ? Tx1 : Tx2 with Tx1 = T[x-1] (likewise y, z), then the n-D update solve3_ref(Tx, Ty, Tz, C).
+// Cells [y][x][z].
+struct Geo3 {
+    int64_t H, W, L;
+    static constexpr int K = 6;
+    struct Co {
+        int64_t x, y, z;
+    };
+    __device__ Co co(int64_t i) const {
+        const int64_t xy = (unsigned)i / (unsigned)L, y = (unsigned)xy / (unsigned)W;
+        return {xy - y * W, y, i - xy * L};
+    }
+    __device__ int64_t nb(int64_t i, Co c, int d) const {
+        switch (d) {
+            case 0: return c.z > 0 ? i - 1 : -1;
+            case 1: return c.z + 1 < L ? i + 1 : -1;
+            case 2: return c.x > 0 ? i - L : -1;
+            case 3: return c.x + 1 < W ? i + L : -1;
+            case 4: return c.y + 1 < H ? i + W * L : -1;
+            default: return c.y > 0 ? i - W * L : -1;
+        }
+    }
+    __device__ Co step(Co c, int d) const {
+        switch (d) {
+            case 0: return {c.x, c.y, c.z - 1};
+            case 1: return {c.x, c.y, c.z + 1};
+            case 2: return {c.x - 1, c.y, c.z};
+            case 3: return {c.x + 1, c.y, c.z};
+            case 4: return {c.x, c.y + 1, c.z};
+            default: return {c.x, c.y - 1, c.z};
+        }
+    }
+    __device__ double solve(const double* v, double cost) const {
+        const double tx = v[2] < v[3] ? v[2] : v[3], ty = v[5] < v[4] ? v[5] : v[4], tz = v[0] < v[1] ? v[0] : v[1];
+        return solve3_ref(tx, ty, tz, cost);
+    }
+};
 
 // the min over z's events whose time (the popping neighbour's rank) is below lim
-__device__ __forceinline__ double events_below(const Front& F, int64_t z, int64_t x, int64_t y, unsigned lim,
-                                               int64_t H, int64_t W) {
+template <class G>
+__device__ __forceinline__ double events_below(const G& g, const Front& F, int64_t z, typename G::Co c, unsigned lim) {
     double v = Real<double>::inf();
-    for (int d = 0; d < 4; ++d) {
-        const int64_t j = nb_of(z, x, y, d, H, W);
-        if (j >= 0 && F.rank[j] < lim) v = __builtin_fmin(v, F.ev[4 * z + d]);
+    for (int d = 0; d < G::K; ++d) {
+        const int64_t j = g.nb(z, c, d);
+        if (j >= 0 && F.rank[j] < lim) v = __builtin_fmin(v, F.ev[G::K * z + d]);
     }
     return v;
 }
 
 // V(z, t): what cell z holds when the t-th pop updates its neighbours
-__device__ __forceinline__ double value_at(const Front& F, int64_t z, int64_t x, int64_t y, unsigned t, int64_t H,
-                                           int64_t W) {
-    if (z == F.src) return 0.0;                                      // :132 / :135
-    if (!(F.cost[z] < Real<double>::inf())) return Real<double>::inf();  // closed from the start (:121 / :124)
+template <class G>
+__device__ __forceinline__ double value_at(const G& g, const Front& F, int64_t z, typename G::Co c, unsigned t) {
+    if (z == F.src) return 0.0;                                          // the source: 0, closed
+    if (!(F.cost[z] < Real<double>::inf())) return Real<double>::inf();  // closed from the start, never updated
     const unsigned rz = F.rank[z];
-    return events_below(F, z, x, y, rz < t ? rz : t, H, W);
+    return events_below(g, F, z, c, rz < t ? rz : t);
 }
 
-// the update of y made by the t-th pop (updateNode :56-63): Thor = min(T[x+1], T[x-1]), Tver =
-// min(T[y+1], T[y-1]) as of that pop
-__device__ __forceinline__ double event_value(const Front& F, int64_t y, int64_t x, int64_t yy, unsigned t, double cy,
-                                              int64_t H, int64_t W) {
-    const double inf = Real<double>::inf();
-    double v[4];
+// the update of y made by the t-th pop, over y's neighbours as of that pop
+template <class G>
+__device__ __forceinline__ double event_value(const G& g, const Front& F, int64_t y, typename G::Co c, unsigned t,
+                                              double cy) {
+    double v[G::K];
 #pragma unroll
-    for (int d = 0; d < 4; ++d) {
-        const int64_t j = nb_of(y, x, yy, d, H, W);
-        v[d] = j < 0 ? inf : value_at(F, j, x + dx_of(d), yy + dy_of(d), t, H, W);
+    for (int d = 0; d < G::K; ++d) {
+        const int64_t j = g.nb(y, c, d);
+        v[d] = j < 0 ? Real<double>::inf() : value_at(g, F, j, g.step(c, d), t);
     }
-    return eik_ref(__builtin_fmin(v[3], v[2]), __builtin_fmin(v[1], v[0]), cy);
+    return g.solve(v, cy);
 }
 
-// is y updated by the pop of rank r (y = child k of that pop)?  open (:56): not popped before, not
-// +inf cost, not the source
+// is y updated by the pop of rank r?  open: not popped before, not +inf cost, not the source
 __device__ __forceinline__ bool child_open(const Front& F, int64_t y, unsigned r) {
     return y >= 0 && F.rank[y] > r && y != F.src && F.cost[y] < Real<double>::inf();
 }
@@ -136,23 +192,25 @@ __global__ void exact_order_kernel(Front F0, Front F1, int64_t n) {
 // 1. every child slot of every ranked pop from the field's values -- valid under the current ranks
 //    or not, so that a slot a later pass's ranks make valid never holds garbage (later passes keep
 //    the relaxed values as their start)
-__global__ __launch_bounds__(256) void exact_init_kernel(Front F0, Front F1, int64_t H, int64_t W) {
+template <class G>
+__global__ __launch_bounds__(256) void exact_init_kernel(Front F0, Front F1, G g) {
     const Front& F = blockIdx.y ? F1 : F0;
     const double inf = Real<double>::inf();
-    const int64_t e1 = 4ll * F.m;
+    const int64_t e1 = (int64_t)G::K * F.m;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < e1; e += (int64_t)gridDim.x * blockDim.x) {
-        const unsigned r = (unsigned)(e >> 2);
-        const int k = (int)(e & 3);
-        const int64_t c = F.ord[r], cyy = (unsigned)c / (unsigned)W, cx = c - cyy * W;
-        const int64_t y = nb_of(c, cx, cyy, k, H, W);
+        const unsigned r = (unsigned)(e / G::K);
+        const int k = (int)(e - (int64_t)r * G::K);
+        const int64_t c = F.ord[r];
+        const typename G::Co cc = g.co(c);
+        const int64_t y = g.nb(c, cc, k);
         if (y < 0 || y == F.src || !(F.cost[y] < inf)) continue;
-        const int64_t x = cx + dx_of(k), yy = cyy + dy_of(k);
-        double v[4];
-        for (int d = 0; d < 4; ++d) {
-            const int64_t j = nb_of(y, x, yy, d, H, W);
+        const typename G::Co yc = g.step(cc, k);
+        double v[G::K];
+        for (int d = 0; d < G::K; ++d) {
+            const int64_t j = g.nb(y, yc, d);
             v[d] = j < 0 ? inf : F.T[j];
         }
-        F.ev[4 * y + (k ^ 1)] = eik_ref(__builtin_fmin(v[3], v[2]), __builtin_fmin(v[1], v[0]), F.cost[y]);
+        F.ev[G::K * y + (k ^ 1)] = g.solve(v, F.cost[y]);
     }
 }
 
@@ -162,14 +220,15 @@ __global__ __launch_bounds__(256) void exact_init_kernel(Front F0, Front F1, int
 //    (its own dependency depth + 1) sweeps -- a correction crosses a whole group per sweep instead of
 //    one dependency step per GPU-wide launch.  One workgroup: its waves share the CU's L1, so a
 //    barrier orders their global stores and loads (workgroup scope, no cache maintenance).
-// pops per group, one event per thread: a group sweep is bound by one event's chain of dependent
-// loads (~11 us), so short groups win -- on the bench's planner query (4096^2, 2.1 M pops per front)
-// 256 / 512 / 1024 / 2048 / 4096 took 376 / 473 / 438 / 477 / 575 ms (33.4 / 24.1 / 11.1 / 6.4 / 3.7 k
-// sweeps); global Jacobi sweeps over all events instead needed 1513 launches, 1.95 s: the band's
-// tentative values chain along the front (profiles/r06m_exact_ab.log)
+// pops per group, about one event per thread: a group sweep is bound by one event's chain of
+// dependent loads (~11 us), so short groups win -- on the bench's planner query (4096^2, 2.1 M pops
+// per front) 256 / 512 / 1024 / 2048 / 4096 took 376 / 473 / 438 / 477 / 575 ms (33.4 / 24.1 / 11.1 /
+// 6.4 / 3.7 k sweeps); global Jacobi sweeps over all events instead needed 1513 launches, 1.95 s: the
+// band's tentative values chain along the front (profiles/r06m_exact_ab.log)
 constexpr unsigned kGroup = 256;
 constexpr unsigned kGroupSweepCap = 1u << 16;
-__global__ __launch_bounds__(1024) void exact_relax_kernel(Front F0, Front F1, int64_t H, int64_t W, Ctl* ctl) {
+template <class G>
+__global__ __launch_bounds__(1024) void exact_relax_kernel(Front F0, Front F1, G g, Ctl* ctl) {
     const int f = blockIdx.y;
     const Front& F = f ? F1 : F0;
     if (!ctl->act[f]) return;
@@ -178,16 +237,17 @@ __global__ __launch_bounds__(1024) void exact_relax_kernel(Front F0, Front F1, i
         const unsigned g1 = min(g0 + kGroup, F.m);
         for (unsigned it = 0;; ++it) {
             bool ch = false;
-            for (unsigned e = 4u * g0 + threadIdx.x; e < 4u * g1; e += blockDim.x) {
-                const unsigned r = e >> 2;
-                const int k = (int)(e & 3u);
-                const int64_t c = F.ord[r], cyy = (unsigned)c / (unsigned)W, cx = c - cyy * W;
-                const int64_t y = nb_of(c, cx, cyy, k, H, W);
+            for (unsigned e = G::K * g0 + threadIdx.x; e < G::K * g1; e += blockDim.x) {
+                const unsigned r = e / G::K;
+                const int k = (int)(e - r * G::K);
+                const int64_t c = F.ord[r];
+                const typename G::Co cc = g.co(c);
+                const int64_t y = g.nb(c, cc, k);
                 if (!child_open(F, y, r)) continue;
-                const double g = event_value(F, y, cx + dx_of(k), cyy + dy_of(k), r, F.cost[y], H, W);
-                double* slot = F.ev + 4 * y + (k ^ 1);
-                if (__double_as_longlong(*slot) != __double_as_longlong(g)) {
-                    *slot = g;
+                const double v = event_value(g, F, y, g.step(cc, k), r, F.cost[y]);
+                double* slot = F.ev + G::K * y + (k ^ 1);
+                if (__double_as_longlong(*slot) != __double_as_longlong(v)) {
+                    *slot = v;
                     ch = true;
                 }
             }
@@ -203,41 +263,51 @@ __global__ __launch_bounds__(1024) void exact_relax_kernel(Front F0, Front F1, i
 }
 
 // the LIFO key of the cell y popped at rank r: its value (the min over its events before r) and seq
-// = 4 x the time of the first event reaching that value (the last strict decrease, :70) + y's child
-// index in that update -- the later the insertion, the earlier among equal T (bisect_left, :76)
-__device__ __forceinline__ double pop_key(const Front& F, int64_t y, unsigned r, int64_t H, int64_t W, unsigned* seq) {
+// = K x the time of the first event reaching that value (the last strict decrease) + y's child
+// index in that update -- the later the insertion, the earlier among equal T (bisect_left)
+template <class G>
+__device__ __forceinline__ double pop_key(const G& g, const Front& F, int64_t y, unsigned r, unsigned* seq) {
     if (y == F.src) {
         *seq = ~0u;  // pops first
         return 0.0;
     }
-    const int64_t yy = (unsigned)y / (unsigned)W, x = y - yy * W;
+    const typename G::Co c = g.co(y);
     double best = Real<double>::inf();
     unsigned bt = kNoRank, s = 0u;
-    for (int d = 0; d < 4; ++d) {
-        const int64_t nb = nb_of(y, x, yy, d, H, W);
+    for (int d = 0; d < G::K; ++d) {
+        const int64_t nb = g.nb(y, c, d);
         if (nb < 0) continue;
         const unsigned t = F.rank[nb];
         if (t >= r) continue;
-        const double v = F.ev[4 * y + d];
+        const double v = F.ev[G::K * y + d];
         if (v < best || (v == best && t < bt)) {
             best = v;
             bt = t;
-            s = 4u * t + (unsigned)(d ^ 1);
+            s = (unsigned)G::K * t + (unsigned)(d ^ 1);
         }
     }
     *seq = s;
     return best;
 }
 
-// 3a. the keys of every pop of rank >= from
-__global__ void exact_keys_kernel(Front F, int64_t H, int64_t W, unsigned long long* kT, unsigned* kS,
-                                  unsigned* val) {
+// 3a. the keys of every pop of rank >= from.  The value key is max(value, its setter's value): a pop
+//     can give a neighbour a value below its own by rounding (an inversion: the reference's c3 cube
+//     drops 2.8e-14 at its pop 1484), and the list then pops that neighbour NEXT -- so it sorts into
+//     its setter's run, whose stack order (exact_ties_kernel) puts it right after the setter
+template <class G>
+__global__ void exact_keys_kernel(Front F, G g, unsigned long long* kT, unsigned* kS, unsigned* val) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t cnt = (int64_t)F.m - F.from;
     if (j >= cnt) return;
     const unsigned r = F.from + (unsigned)j;
     unsigned seq;
-    const double t = pop_key(F, F.ord[r], r, H, W, &seq);
+    double t = pop_key(g, F, F.ord[r], r, &seq);
+    if (seq != ~0u) {
+        const unsigned bt = seq / G::K;  // the setter's rank
+        unsigned sq;
+        const double ts = pop_key(g, F, F.ord[bt], bt, &sq);
+        t = ts > t ? ts : t;
+    }
     kT[j] = (unsigned long long)__double_as_longlong(t);  // T >= 0 (or +inf): orders as unsigned
     kS[j] = ~seq;                                         // ascending ~seq = most recent insertion first
     val[j] = r;
@@ -256,21 +326,23 @@ __global__ void exact_moved_kernel(Front F, const unsigned* sorted, int64_t cnt,
     ord2[j] = F.ord[sorted[j]];
 }
 
-// 3c. runs of exactly equal T v pop as the reference's list does: entries of equal T pop most recent
-//     insertion first (bisect_left), and a pop may insert a child at exactly v (getEikonal's two-sided
-//     form at |Thor - Tver| = cost gives Thor), which then pops NEXT, before older entries of v.  So
-//     a run is a stack: its roots (members whose value v was set by a pop below the run) pushed in
-//     insertion order (seq), then each pop pushes its children in updateNode's order (:46-54) whose
-//     update from it is exactly v and that are not on the stack yet (an equal value is no strict
-//     decrease, :70).  seq reads the ranks of earlier pops, themselves possibly in a run, so a tie
-//     level settles once the levels below it have: each launch re-forms every run (its first
-//     thread, runs are short) from the current ranks until a launch moves nothing.  The events stay
-//     as the relaxation left them (a cell's value does not depend on the order of equal-T pops); the
-//     pass's final check (every rank against the relaxation's order) catches any exception.
-//     Launch s returns at once when launch s - 1 moved nothing.
+// 3c. runs of equal keys pop as the reference's list does: entries of equal T pop most recent
+//     insertion first (bisect_left), and a pop may insert a child at exactly its own T (getEikonal's
+//     two-sided form at |Thor - Tver| = cost gives Thor) or, by rounding, below it -- which then
+//     pops NEXT, before older entries.  So a run is a stack: its roots (members whose value was set
+//     by a pop before the run) pushed in insertion order (seq), then each pop pushes, in updateNode's
+//     child order, the members it set (their value's first event is its update).  A member's value
+//     and setter are read over the events of every pop up to the run's end (an equal or larger value
+//     from a later pop is no strict decrease).  seq reads the ranks of earlier pops, themselves
+//     possibly in a run, so a tie level settles once the levels below it have: each launch re-forms
+//     every run (its first thread, runs are short) from the current ranks until a launch moves
+//     nothing.  The events stay as the relaxation left them; the pass's final check (every rank
+//     against the relaxation's order) catches any exception.  Launch s returns at once when launch
+//     s - 1 moved nothing.
 constexpr int64_t kMaxRun = 4096;
-__global__ void exact_ties_kernel(Front F, int64_t H, int64_t W, const unsigned long long* kT, int64_t cnt,
-                                  unsigned* flags, int s, unsigned* longrun, unsigned* out_buf, unsigned* stack_buf) {
+template <class G>
+__global__ void exact_ties_kernel(Front F, G g, const unsigned long long* kT, int64_t cnt, unsigned* flags, int s,
+                                  unsigned* longrun, unsigned* out_buf, unsigned* stack_buf) {
     if (s > 0 && flags[s - 1] == 0u) return;
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j + 1 >= cnt || kT[j + 1] != kT[j] || (j > 0 && kT[j - 1] == kT[j])) return;  // run starts only
@@ -281,8 +353,7 @@ __global__ void exact_ties_kernel(Front F, int64_t H, int64_t W, const unsigned 
         return;
     }
     const int L = (int)(e - j);
-    const unsigned r0 = F.from + (unsigned)j;
-    const double v = __longlong_as_double((long long)kT[j]);
+    const unsigned r0 = F.from + (unsigned)j, r1 = r0 + (unsigned)L;
     unsigned* out = out_buf + j;
     unsigned* stk = stack_buf + j;
     unsigned pushed[kMaxRun / 32];
@@ -291,23 +362,10 @@ __global__ void exact_ties_kernel(Front F, int64_t H, int64_t W, const unsigned 
     int sp = 0;
     unsigned* sseq = out;  // (the roots' seq, beside the stack, until the output is written)
     for (int a = 0; a < L; ++a) {
-        const int64_t y = F.ord[r0 + a], yy = (unsigned)y / (unsigned)W, x = y - yy * W;
-        unsigned bt = kNoRank, sq = 0u;
-        if (y == F.src) {
-            bt = 0u;
-            sq = ~0u;
-        } else {
-            for (int d = 0; d < 4; ++d) {
-                const int64_t nb = nb_of(y, x, yy, d, H, W);
-                if (nb < 0) continue;
-                const unsigned t = F.rank[nb];
-                if (t < r0 && t < bt && F.ev[4 * y + d] == v) {
-                    bt = t;
-                    sq = 4u * t + (unsigned)(d ^ 1);
-                }
-            }
-        }
-        if (bt == kNoRank) continue;  // a child of a run member
+        const int64_t y = F.ord[r0 + a];
+        unsigned sq;
+        (void)pop_key(g, F, y, r1, &sq);
+        if (sq != ~0u && sq / G::K >= r0) continue;  // set by a run member: pushed by its pop
         int b = sp++;
         while (b > 0 && sseq[b - 1] > sq) {
             stk[b] = stk[b - 1];
@@ -322,16 +380,20 @@ __global__ void exact_ties_kernel(Front F, int64_t H, int64_t W, const unsigned 
     // only read while sorting the roots in)
     int no = 0;
     while (sp > 0) {
-        const int64_t p = stk[--sp], py = (unsigned)p / (unsigned)W, px = p - py * W;
+        const int64_t p = stk[--sp];
+        const typename G::Co pc = g.co(p);
+        const unsigned rp = F.rank[p];
         out[no++] = (unsigned)p;
-        for (int k = 0; k < 4; ++k) {
-            const int64_t y = nb_of(p, px, py, k, H, W);
+        for (int k = 0; k < G::K; ++k) {
+            const int64_t y = g.nb(p, pc, k);
             if (y < 0) continue;
             const unsigned ry = F.rank[y];
-            if (ry < r0 || ry >= r0 + (unsigned)L) continue;  // not in this run
+            if (ry < r0 || ry >= r1) continue;  // not in this run
             const int a = (int)(ry - r0);
             if (pushed[a >> 5] & (1u << (a & 31))) continue;
-            if (F.ev[4 * y + (k ^ 1)] != v) continue;  // p's update of y is not exactly v
+            unsigned sq;
+            (void)pop_key(g, F, y, r1, &sq);
+            if (sq != (unsigned)G::K * rp + (unsigned)k) continue;  // p's update did not set y's value
             pushed[a >> 5] |= 1u << (a & 31);
             stk[sp++] = (unsigned)y;
         }
@@ -366,23 +428,55 @@ __global__ void exact_apply_kernel(Front F, const unsigned* ord2, int64_t cnt) {
     F.rank[i] = r;
 }
 
-// 5. biComputeTmap's returned fields at the meeting k: popped cells (rank <= k) their value,
-//    band cells (an open cell with a popped neighbour) their value as of the last pop, else +inf
-__global__ void exact_fields_kernel(Front F0, Front F1, int64_t H, int64_t W, const unsigned long long* best) {
+// 5. the returned field after the pop of rank k: popped cells (rank <= k) their value, band cells
+//    (an open cell with a popped neighbour) their value as of that pop, every other cell +inf.
+//    biComputeTmap: k = the meeting iteration (*best >> 30), each front in place.  FM3D's early
+//    exit: k = the rank of `start` (kNoRank: never popped -- the full field), into Te.
+template <class G>
+__device__ __forceinline__ double field_value(const G& g, const Front& F, int64_t i, unsigned k) {
+    if (i == F.src) return 0.0;
+    if (!(F.cost[i] < Real<double>::inf())) return Real<double>::inf();
+    const unsigned r = F.rank[i];
+    const unsigned lim = r <= k ? r : (k == kNoRank ? kNoRank : k + 1u);
+    return events_below(g, F, i, g.co(i), lim);  // (+inf when no neighbour popped)
+}
+
+__global__ void exact_fields_bidir_kernel(Front F0, Front F1, Geo2 g, const unsigned long long* best) {
     const Front& F = blockIdx.y ? F1 : F0;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const unsigned long long b = *best;
-    if (i >= H * W || b == ~0ull) return;  // never met: the caller reports it
-    const unsigned k = (unsigned)(b >> 30);
-    const int64_t yy = i / W, x = i - yy * W;
-    const unsigned r = F.rank[i];
-    double t = Real<double>::inf();
-    if (i == F.src) {
-        t = 0.0;
-    } else if (F.cost[i] < Real<double>::inf()) {
-        t = events_below(F, i, x, yy, r <= k ? r : k + 1u, H, W);  // (+inf when no neighbour popped)
+    if (i >= g.H * g.W || b == ~0ull) return;  // never met: the caller reports it
+    F.T[i] = field_value(g, F, i, (unsigned)(b >> 30));
+}
+
+__global__ void exact_fields_early_kernel(Front F, Geo3 g, int64_t start, double* __restrict__ Te) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= g.H * g.W * g.L) return;
+    Te[i] = field_value(g, F, i, F.rank[start]);
+}
+
+// FM3D: the cells ranked -- T <= T[start] x (1 + 2^-30), every cell the replay can pop up to start
+// (the converged field is within a few ulps of the reference's values); all finite cells when start
+// is unreachable (the reference then empties its band)
+__global__ void exact_thr_kernel(const double* T, int64_t start, Ctl* ctl) {
+    const double ts = T[start];
+    ctl->thr = ts < Real<double>::inf() ? ts * (1.0 + 0x1p-30) : Real<double>::inf();
+}
+struct Fm3dMember {
+    const double* T;
+    const Ctl* ctl;
+    __device__ bool operator()(const unsigned& i) const {
+        const double t = T[i];
+        return t < Real<double>::inf() && t <= ctl->thr;
     }
-    F.T[i] = t;
+};
+__global__ void exact_tkeys_kernel(const double* T, const unsigned* list, int64_t m, unsigned long long* keys) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < m) keys[j] = (unsigned long long)__double_as_longlong(T[list[j]]);
+}
+__global__ void exact_scatter_rank_kernel(const unsigned* ord, int64_t m, unsigned* rank) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < m) rank[ord[j]] = (unsigned)j;
 }
 
 struct ExactLayout {
@@ -399,16 +493,20 @@ struct ExactLayout {
 
 size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
 
-ExactLayout exact_layout(void* work, int64_t n, int64_t m0, int64_t m1) {
+// K events per cell; per-front arrays only for fronts with members; sel: room for FM3D's selection
+ExactLayout exact_layout(void* work, int64_t n, int K, int64_t m0, int64_t m1, bool sel) {
     ExactLayout L{};
     const int64_t mx = std::max<int64_t>(1, std::max(m0, m1));
-    size_t sort64 = 0, sort32 = 0;
+    size_t sort64 = 0, sort32 = 0, sel_b = 0;
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort32, (unsigned*)nullptr, (unsigned*)nullptr, (unsigned*)nullptr,
                                              (unsigned*)nullptr, (int)mx, 0, 32, (hipStream_t)0);
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort64, (unsigned long long*)nullptr,
                                              (unsigned long long*)nullptr, (unsigned*)nullptr, (unsigned*)nullptr,
                                              (int)mx, 0, 64, (hipStream_t)0);
-    L.cub_bytes = align256(std::max(sort32, sort64));
+    if (sel)
+        (void)hipcub::DeviceSelect::If(nullptr, sel_b, hipcub::CountingInputIterator<unsigned>(0u), (unsigned*)nullptr,
+                                       (unsigned*)nullptr, n, Fm3dMember{nullptr, nullptr}, (hipStream_t)0);
+    L.cub_bytes = align256(std::max(std::max(sort32, sort64), sel_b));
     char* p = static_cast<char*>(work);
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -418,8 +516,9 @@ ExactLayout exact_layout(void* work, int64_t n, int64_t m0, int64_t m1) {
     };
     const int64_t m[2] = {m0, m1};
     for (int f = 0; f < 2; ++f) {
-        L.ev[f] = reinterpret_cast<double*>(take(sizeof(double) * 4 * (size_t)n));
-        L.rank[f] = reinterpret_cast<unsigned*>(take(sizeof(unsigned) * (size_t)n));
+        const bool on = m[f] > 0;
+        L.ev[f] = reinterpret_cast<double*>(take(sizeof(double) * (on ? (size_t)K * n : 1)));
+        L.rank[f] = reinterpret_cast<unsigned*>(take(sizeof(unsigned) * (on ? (size_t)n : 1)));
         L.ord[f] = reinterpret_cast<unsigned*>(take(sizeof(unsigned) * (size_t)std::max<int64_t>(1, m[f])));
     }
     L.kT = reinterpret_cast<unsigned long long*>(take(8 * (size_t)mx));
@@ -446,70 +545,51 @@ __global__ void exact_ctl_kernel(Ctl* ctl, unsigned a0, unsigned a1) {
     ctl->longrun = 0u;
 }
 
-}  // namespace
-
-size_t bidir_exact_work_bytes(int64_t n, int64_t m0, int64_t m1) { return exact_layout(nullptr, n, m0, m1).total; }
-
-hipError_t bidir_exact(double* d_TG, double* d_TS, const double* d_cost, int64_t H, int64_t W, int64_t gnode,
-                       int64_t snode, const unsigned* d_rg, const unsigned* d_rs, const int64_t members[2],
-                       void* d_work, size_t work_bytes, unsigned long long* d_best, hipStream_t st,
-                       unsigned long long info[4]) {
-    const int64_t n = H * W;
-    if (n >= (1ll << 29) || members[0] < 0 || members[1] < 0 || members[0] > n || members[1] > n)
-        return hipErrorInvalidValue;
-    const ExactLayout L = exact_layout(d_work, n, members[0], members[1]);
-    if (L.total > work_bytes) return hipErrorOutOfMemory;
-    Front F[2];
-    double* T[2] = {d_TG, d_TS};
-    const int64_t src[2] = {gnode, snode};
-    const unsigned* rin[2] = {d_rg, d_rs};
-    hipError_t e = hipSuccess;
-    for (int f = 0; f < 2; ++f) {
-        F[f] = Front{d_cost, T[f], L.rank[f], L.ord[f], L.ev[f], src[f], (unsigned)members[f], 0u};
-        e = hipMemcpyAsync(L.rank[f], rin[f], sizeof(unsigned) * (size_t)n, hipMemcpyDeviceToDevice, st);
-        if (e != hipSuccess) return e;
-    }
-    const unsigned ng = (unsigned)((n + 255) / 256);
-    hipLaunchKernelGGL(exact_order_kernel, dim3(ng, 2), dim3(256), 0, st, F[0], F[1], n);
-    e = hipMemsetAsync(L.ctl, 0, sizeof(Ctl), st);
+// steps 1-3 for nf fronts (F[0..nf-1]) whose rank / ord arrays hold a first order of their m cells
+template <class G>
+hipError_t replay(const G& g, Front F[2], int nf, const ExactLayout& L, hipStream_t st, unsigned long long info[4]) {
+    hipError_t e = hipMemsetAsync(L.ctl, 0, sizeof(Ctl), st);
     if (e != hipSuccess) return e;
     {
-        const int64_t mx = std::max(members[0], members[1]);
-        const unsigned gi = (unsigned)std::max<int64_t>(1, std::min<int64_t>(4096, (4 * mx + 255) / 256));
-        hipLaunchKernelGGL(exact_init_kernel, dim3(gi, 2), dim3(256), 0, st, F[0], F[1], H, W);
+        const int64_t mx = std::max(F[0].m, nf > 1 ? F[1].m : 0u);
+        const unsigned gi = (unsigned)std::max<int64_t>(1, std::min<int64_t>(4096, ((int64_t)G::K * mx + 255) / 256));
+        hipLaunchKernelGGL(exact_init_kernel<G>, dim3(gi, nf), dim3(256), 0, st, F[0], F[1], g);
     }
-    bool active[2] = {members[0] > 0, members[1] > 0};
+    bool active[2] = {F[0].m > 0, nf > 1 && F[1].m > 0};
     static const bool debug = getenv("EIK_EXACT_DEBUG") != nullptr;  // per-pass trace on stderr (diagnostics)
     unsigned passes = 0;
     for (;;) {
-        if (++passes > kMaxPasses) return hipErrorNotReady;
+        if (++passes > kMaxPasses) {
+            if (debug) fprintf(stderr, "[exact] no fixed point after %u passes\n", kMaxPasses);
+            return hipErrorNotReady;
+        }
         hipLaunchKernelGGL(exact_ctl_kernel, dim3(1), dim3(1), 0, st, L.ctl, active[0] ? 1u : 0u, active[1] ? 1u : 0u);
-        hipLaunchKernelGGL(exact_relax_kernel, dim3(1, 2), dim3(1024), 0, st, F[0], F[1], H, W, L.ctl);
+        hipLaunchKernelGGL(exact_relax_kernel<G>, dim3(1, nf), dim3(1024), 0, st, F[0], F[1], g, L.ctl);
         // re-rank every active front from its first relaxed rank
-        for (int f = 0; f < 2; ++f) {
+        for (int f = 0; f < nf; ++f) {
             if (!active[f]) continue;
             const int64_t cnt = (int64_t)F[f].m - F[f].from;
             if (cnt <= 0) continue;
-            const unsigned g = (unsigned)((cnt + 255) / 256);
-            hipLaunchKernelGGL(exact_keys_kernel, dim3(g), dim3(256), 0, st, F[f], H, W, L.kT, L.kS, L.val);
+            const unsigned gk = (unsigned)((cnt + 255) / 256);
+            hipLaunchKernelGGL(exact_keys_kernel<G>, dim3(gk), dim3(256), 0, st, F[f], g, L.kT, L.kS, L.val);
             size_t b = L.cub_bytes;
             e = hipcub::DeviceRadixSort::SortPairs(L.cub_tmp, b, L.kS, L.kS2, L.val, L.val2, (int)cnt, 0, 32, st);
             if (e != hipSuccess) return e;
-            hipLaunchKernelGGL(exact_gather_kernel, dim3(g), dim3(256), 0, st, L.kT, L.val2, F[f].from, cnt, L.kT2);
+            hipLaunchKernelGGL(exact_gather_kernel, dim3(gk), dim3(256), 0, st, L.kT, L.val2, F[f].from, cnt, L.kT2);
             b = L.cub_bytes;
             e = hipcub::DeviceRadixSort::SortPairs(L.cub_tmp, b, L.kT2, L.kT3, L.val2, L.val3, (int)cnt, 0, 64, st);
             if (e != hipSuccess) return e;
-            hipLaunchKernelGGL(exact_moved_kernel, dim3(g), dim3(256), 0, st, F[f], L.val3, cnt, L.ord2);
+            hipLaunchKernelGGL(exact_moved_kernel, dim3(gk), dim3(256), 0, st, F[f], L.val3, cnt, L.ord2);
             e = hipMemcpyAsync(L.ordp, F[f].ord + F[f].from, sizeof(unsigned) * (size_t)cnt, hipMemcpyDeviceToDevice, st);
             if (e != hipSuccess) return e;
-            hipLaunchKernelGGL(exact_apply_kernel, dim3(g), dim3(256), 0, st, F[f], L.ord2, cnt);
+            hipLaunchKernelGGL(exact_apply_kernel, dim3(gk), dim3(256), 0, st, F[f], L.ord2, cnt);
             // the tie runs, in batches of kTieBatch launches until one moves nothing
             for (unsigned tb = 0;; ++tb) {
                 if (tb >= kMaxTieBatches) return hipErrorNotReady;
                 e = hipMemsetAsync(L.flags, 0, sizeof(unsigned) * kTieBatch, st);
                 if (e != hipSuccess) return e;
                 for (int q = 0; q < kTieBatch; ++q)
-                    hipLaunchKernelGGL(exact_ties_kernel, dim3(g), dim3(256), 0, st, F[f], H, W, L.kT3, cnt, L.flags, q,
+                    hipLaunchKernelGGL(exact_ties_kernel<G>, dim3(gk), dim3(256), 0, st, F[f], g, L.kT3, cnt, L.flags, q,
                                        &L.ctl->longrun, L.ord2, L.val2);
                 unsigned hf[kTieBatch];
                 e = hipMemcpyAsync(hf, L.flags, sizeof hf, hipMemcpyDeviceToHost, st);
@@ -519,39 +599,116 @@ hipError_t bidir_exact(double* d_TG, double* d_TS, const double* d_cost, int64_t
                 while (q < kTieBatch && hf[q]) ++q;
                 info[3] += (unsigned long long)(q < kTieBatch ? q + 1 : kTieBatch);
                 if (q < kTieBatch) break;
+                if (debug && (tb & (tb - 1)) == 0)
+                    fprintf(stderr, "[exact] pass %u front %d: tie runs still moving after %u batches\n", passes, f, tb + 1);
             }
             // ordp: the relaxation's order (the old ord after the copy above)
-            hipLaunchKernelGGL(exact_cmp_kernel, dim3(g), dim3(256), 0, st, F[f], L.ordp, cnt, &L.ctl->first_bad[f]);
+            hipLaunchKernelGGL(exact_cmp_kernel, dim3(gk), dim3(256), 0, st, F[f], L.ordp, cnt, &L.ctl->first_bad[f]);
         }
         Ctl h{};
         e = hipMemcpyAsync(&h, L.ctl, sizeof h, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) return e;
-        if (h.stuck[0] || h.stuck[1]) return hipErrorNotReady;
+        if (h.stuck[0] || h.stuck[1]) {
+            if (debug) fprintf(stderr, "[exact] a relaxation group did not settle (pass %u)\n", passes);
+            return hipErrorNotReady;
+        }
         if (h.longrun) return hipErrorNotSupported;
-        const unsigned* bad = h.first_bad;
-        const unsigned* sw = h.sweeps;
-        info[1] += sw[0];
-        info[2] += sw[1];
+        info[1] += h.sweeps[0];
+        info[2] += h.sweeps[1];
         if (debug)
             fprintf(stderr, "[exact] pass %u from %u/%u sweeps so far %llu/%llu m %u/%u first moved %d/%d tie launches %llu\n",
-                    passes, F[0].from, F[1].from, info[1], info[2], F[0].m, F[1].m, bad[0] == kNoRank ? -1 : (int)bad[0],
-                    bad[1] == kNoRank ? -1 : (int)bad[1], info[3]);
+                    passes, F[0].from, F[1].from, info[1], info[2], F[0].m, F[1].m,
+                    h.first_bad[0] == kNoRank ? -1 : (int)h.first_bad[0], h.first_bad[1] == kNoRank ? -1 : (int)h.first_bad[1],
+                    info[3]);
         e = hipMemsetAsync(L.ctl->sweeps, 0, sizeof h.sweeps, st);
         if (e != hipSuccess) return e;
-        for (int f = 0; f < 2; ++f) {
+        for (int f = 0; f < nf; ++f) {
             if (!active[f]) continue;
-            if (bad[f] == kNoRank) active[f] = false;
-            else F[f].from = bad[f];
+            if (h.first_bad[f] == kNoRank) active[f] = false;
+            else F[f].from = h.first_bad[f];
         }
         if (!active[0] && !active[1]) break;
     }
     info[0] = passes;
+    return hipSuccess;
+}
+
+}  // namespace
+
+size_t bidir_exact_work_bytes(int64_t n, int64_t m0, int64_t m1) {
+    return exact_layout(nullptr, n, Geo2::K, m0, m1, false).total;
+}
+
+hipError_t bidir_exact(double* d_TG, double* d_TS, const double* d_cost, int64_t H, int64_t W, int64_t gnode,
+                       int64_t snode, const unsigned* d_rg, const unsigned* d_rs, const int64_t members[2],
+                       void* d_work, size_t work_bytes, unsigned long long* d_best, hipStream_t st,
+                       unsigned long long info[4]) {
+    const int64_t n = H * W;
+    if (n >= (1ll << 29) || members[0] < 0 || members[1] < 0 || members[0] > n || members[1] > n)
+        return hipErrorInvalidValue;
+    const ExactLayout L = exact_layout(d_work, n, Geo2::K, members[0], members[1], false);
+    if (L.total > work_bytes) return hipErrorOutOfMemory;
+    const Geo2 g{H, W};
+    Front F[2];
+    double* T[2] = {d_TG, d_TS};
+    const int64_t src[2] = {gnode, snode};
+    const unsigned* rin[2] = {d_rg, d_rs};
+    hipError_t e = hipSuccess;
+    for (int f = 0; f < 2; ++f) {
+        F[f] = Front{d_cost, T[f], L.rank[f], L.ord[f], L.ev[f], src[f], (unsigned)members[f], 0u};
+        if (members[f] > 0) e = hipMemcpyAsync(L.rank[f], rin[f], sizeof(unsigned) * (size_t)n, hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) return e;
+    }
+    if (members[0] <= 0 || members[1] <= 0) return hipErrorInvalidValue;  // (the join found no meeting)
+    const unsigned ng = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(exact_order_kernel, dim3(ng, 2), dim3(256), 0, st, F[0], F[1], n);
+    e = replay(g, F, 2, L, st, info);
+    if (e != hipSuccess) return e;
     e = hipMemsetAsync(d_best, 0xFF, sizeof(unsigned long long), st);
     if (e != hipSuccess) return e;
     e = bidir_join_min(L.rank[0], L.rank[1], n, d_best, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(exact_fields_kernel, dim3(ng, 2), dim3(256), 0, st, F[0], F[1], H, W, d_best);
+    hipLaunchKernelGGL(exact_fields_bidir_kernel, dim3(ng, 2), dim3(256), 0, st, F[0], F[1], g, d_best);
+    return hipGetLastError();
+}
+
+size_t fm3d_exact_work_bytes(int64_t n) { return exact_layout(nullptr, n, Geo3::K, n, 0, true).total; }
+
+hipError_t fm3d_exact(const double* d_cost, const double* d_T, double* d_Te, int64_t H, int64_t W, int64_t L3,
+                      int64_t goal_off, int64_t start_off, void* d_work, size_t work_bytes, hipStream_t st,
+                      unsigned long long info[4]) {
+    const int64_t n = H * W * L3;
+    if (n >= (1ll << 29) || goal_off < 0 || goal_off >= n || start_off < 0 || start_off >= n) return hipErrorInvalidValue;
+    const ExactLayout L = exact_layout(d_work, n, Geo3::K, n, 0, true);
+    if (L.total > work_bytes) return hipErrorOutOfMemory;
+    const Geo3 g{H, W, L3};
+    // the cells to rank (node order), their first order by T (stable: ties by node)
+    hipLaunchKernelGGL(exact_thr_kernel, dim3(1), dim3(1), 0, st, d_T, start_off, L.ctl);
+    size_t b = L.cub_bytes;
+    hipError_t e = hipcub::DeviceSelect::If(L.cub_tmp, b, hipcub::CountingInputIterator<unsigned>(0u), L.val, &L.ctl->msel,
+                                            n, Fm3dMember{d_T, L.ctl}, st);
+    if (e != hipSuccess) return e;
+    unsigned m = 0;
+    e = hipMemcpyAsync(&m, &L.ctl->msel, sizeof m, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return e;
+    if (m == 0) return hipErrorInvalidValue;  // (the goal is always selected)
+    const unsigned gm = (unsigned)((m + 255) / 256);
+    hipLaunchKernelGGL(exact_tkeys_kernel, dim3(gm), dim3(256), 0, st, d_T, L.val, (int64_t)m, L.kT);
+    b = L.cub_bytes;
+    e = hipcub::DeviceRadixSort::SortPairs(L.cub_tmp, b, L.kT, L.kT2, L.val, L.ord[0], (int)m, 0, 64, st);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(L.rank[0], 0xFF, sizeof(unsigned) * (size_t)n, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(exact_scatter_rank_kernel, dim3(gm), dim3(256), 0, st, L.ord[0], (int64_t)m, L.rank[0]);
+    Front F[2];
+    F[0] = Front{d_cost, const_cast<double*>(d_T), L.rank[0], L.ord[0], L.ev[0], goal_off, m, 0u};
+    F[1] = Front{d_cost, nullptr, L.rank[1], L.ord[1], L.ev[1], -1, 0u, 0u};
+    e = replay(g, F, 1, L, st, info);
+    if (e != hipSuccess) return e;
+    const unsigned gn = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(exact_fields_early_kernel, dim3(gn), dim3(256), 0, st, F[0], g, start_off, d_Te);
     return hipGetLastError();
 }
 

@@ -266,6 +266,13 @@ hipError_t bidir_exact(double* d_TG, double* d_TS, const double* d_cost, int64_t
                        int64_t snode, const unsigned* d_rg, const unsigned* d_rs, const int64_t members[2],
                        void* d_work, size_t work_bytes, unsigned long long* d_best, hipStream_t st,
                        unsigned long long info[4]);
+// ... and FastMarching3D.computeTmap's early exit (:137-142) in the same replay: d_T the converged fp64
+// field from goal_off, d_Te the reference's own partial field after popping start_off (its band's
+// tentative values, its LIFO ties)
+size_t fm3d_exact_work_bytes(int64_t n);
+hipError_t fm3d_exact(const double* d_cost, const double* d_T, double* d_Te, int64_t H, int64_t W, int64_t L,
+                      int64_t goal_off, int64_t start_off, void* d_work, size_t work_bytes, hipStream_t st,
+                      unsigned long long info[4]);
 // the capped fronts' device block (eikonal_api.cpp solve_fronts)
 struct FrontsCheck {
     double caps[2];                   // per front: activation cap of the full-resolution solve

@@ -1293,7 +1293,7 @@ static int join_and_partial(eik_ctx* c, double* dT, int64_t n, int64_t H, int64_
     HIPCHK(c, c->work.ensure(bidir_join_work_bytes(n)));
     HIPCHK(c, c->misc.ensure(64));
     HIPCHK(c, bidir_join(dT, dT + n, n, c->work.p, c->work.bytes, (unsigned long long*)c->misc.p, st, members));
-    if (d_cost && src && c->exact_band) {
+    if (d_cost && src && c->exact_band && members[0] > 0 && members[1] > 0) {
         // the reference's own band values, LIFO ties and nodeJoin, replayed from the join's ranks
         const unsigned *rg = nullptr, *rs = nullptr;
         bidir_join_ranks(c->work.p, n, &rg, &rs);
@@ -1937,8 +1937,43 @@ int eik_fim3d_early_exit(eik_ctx* c, const void* d_cost, const void* d_T, void* 
     if (!c || !d_cost || !d_T || !d_Te || !goal || !start || H < 1 || W < 1 || L < 1 || d_T == d_Te)
         return c ? set_err(c, EIK_ERR_ARG, "bad early-exit arguments") : EIK_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, fim3d_early(d_cost, d_T, d_Te, H, W, L, early_offset(goal, start, H, W, L), dtype == EIK_F64,
-                          (hipStream_t)stream));
+    const int64_t ts_off = early_offset(goal, start, H, W, L);
+    for (auto& v : c->exact_info) v = 0;
+    if (c->exact_band && dtype == EIK_F64 && ts_off >= 0) {
+        // the reference's own band values and LIFO ties (bidir_exact.hip fm3d_exact)
+        const int64_t n = H * W * L;
+        if (n >= (1ll << 29)) return set_err(c, EIK_ERR_ARG, "exact band replay: volumes of < 2^29 cells");
+        HIPCHK(c, c->exact.ensure(fm3d_exact_work_bytes(n)));
+        hipStream_t st = (hipStream_t)stream;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        HIPCHK(c, hipEventCreate(&e0));
+        HIPCHK(c, hipEventCreate(&e1));
+        HIPCHK(c, hipEventRecord(e0, st));
+        unsigned long long info[4] = {0, 0, 0, 0};
+        const int64_t goal_off = (goal[1] * W + goal[0]) * L + goal[2];
+        const hipError_t e = fm3d_exact(static_cast<const double*>(d_cost), static_cast<const double*>(d_T),
+                                        static_cast<double*>(d_Te), H, W, L, goal_off, ts_off, c->exact.p,
+                                        c->exact.bytes, st, info);
+        if (e == hipErrorNotReady || e == hipErrorNotSupported) {
+            (void)hipEventDestroy(e0);
+            (void)hipEventDestroy(e1);
+            return set_err(c, EIK_ERR_NOCONVERGE, e == hipErrorNotReady
+                                                      ? "FM3D early exit: the exact band replay did not settle"
+                                                      : "FM3D early exit: the exact band replay met a run of more "
+                                                        "than 4096 cells of exactly equal T (a zero-cost region)");
+        }
+        HIPCHK(c, e);
+        HIPCHK(c, hipEventRecord(e1, st));
+        HIPCHK(c, hipEventSynchronize(e1));
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        for (int q = 0; q < 4; ++q) c->exact_info[q] = info[q];
+        c->exact_info[4] = (unsigned long long)(ms * 1000.0f);
+        return EIK_OK;
+    }
+    HIPCHK(c, fim3d_early(d_cost, d_T, d_Te, H, W, L, ts_off, dtype == EIK_F64, (hipStream_t)stream));
     return EIK_OK;
 }
 

@@ -38,54 +38,7 @@ __device__ __forceinline__ R godunov3(R a, R b, R c, R C) {
     return a + C;
 }
 
-// FastMarching3D.py:59-75 in the reference's own arithmetic, for the fp64 solver: Tarray =
-// [Tx, Ty, Tz]; Tmax = the FIRST largest entry (Python max); sumT = left fold of (Tmax - Ta)^2 from
-// 0; accept when C^2 > sumT with Tr = (S + sqrt(n C^2 + S^2 - n Q)) / n, S and Q right-associated
-// sums (sumlist, :103-107) in list order; else remove that Tmax (list.remove: first occurrence)
-// and retry.  No contraction, correctly rounded sqrt and division: the same bits as the reference
-// on the same neighbours, so exact ties stay exact ties (FastMarching3D.computeTmap's early exit
-// compares against T[start], fim3d_early_kernel).  All +inf -> +inf (the reference never solves
-// a cell without a popped neighbour).
-__device__ __forceinline__ double solve3_ref(double v0, double v1, double v2, double C) {
-#pragma clang fp contract(off)
-    // select form of the reference's loop (no divergence): the three acceptance tests first, then
-    // ONE square root and ONE division on the accepted list
-    const double C2 = C * C;
-    // n = 3: Tmax = first largest (Python max: replaced only by a strictly larger item)
-    const bool m1 = v1 > v0;
-    const double t01 = m1 ? v1 : v0;
-    const bool m2 = v2 > t01;
-    const double tmax = m2 ? v2 : t01;
-    const int im = m2 ? 2 : (m1 ? 1 : 0);
-    const double d0 = tmax - v0, d1 = tmax - v1, d2 = tmax - v2;
-    const bool ok3 = C2 > (d0 * d0 + d1 * d1) + d2 * d2;  // ((0 + d0^2) + d1^2) + d2^2; NaN -> false
-    // n = 2: the list without its first largest entry, in list order
-    const double u0 = im == 0 ? v1 : v0, u1 = im == 2 ? v1 : v2;
-    const bool n1 = u1 > u0;
-    const double t2 = n1 ? u1 : u0;
-    const double e0 = t2 - u0, e1 = t2 - u1;
-    const bool ok2 = C2 > e0 * e0 + e1 * e1;
-    // n = 1: the remaining entry (sumT = (w - w)^2: 0, or NaN for +inf)
-    const double w = n1 ? u0 : u1;
-    const double dw = w - w;
-    const bool ok1 = C2 > dw * dw;
-    double S, Q, nn;
-    if (ok3) {
-        S = v0 + (v1 + v2);  // sumlist: right-associated
-        Q = v0 * v0 + (v1 * v1 + v2 * v2);
-        nn = 3.0;
-    } else if (ok2) {
-        S = u0 + u1;
-        Q = u0 * u0 + u1 * u1;
-        nn = 2.0;
-    } else {
-        S = w;
-        Q = w * w;
-        nn = 1.0;
-    }
-    const double tr = (S + __builtin_sqrt((nn * C2 + S * S) - nn * Q)) / nn;
-    return (ok3 || ok2 || ok1) ? tr : Real<double>::inf();
-}
+// (solve3_ref, the reference's FastMarching3D.py:59-75 in its own arithmetic: eik_common.hpp)
 
 // the solver's local update: the reference's arithmetic in fp64, the cancellation-free form in fp32
 template <typename R>
