@@ -20,9 +20,9 @@
 // own getEikonal arithmetic for this mode (fim2d.hip sweep_quadrant REF), so that the popped cells'
 // final values mostly start exact:
 //  1. init:    every event from the field's values (an estimate: the fixed point does not depend on it);
-//  2. relax:   one workgroup per front walks the pops in rank order, groups of kGroup swept in place
-//              until a sweep changes no event's bits (earlier groups are final; the band's tentative
-//              values chain along the front, which in-order groups resolve as they go);
+//  2. relax:   chunks of kChunk pops in rank order, every event of a chunk swept in place across the
+//              GPU until a sweep changes no event's bits (earlier chunks are final), each event's
+//              inputs resolved once per chunk;
 //  3. re-rank: key every popped cell (value, seq) and sort the ranks from the first one relaxed, then
 //              re-form the runs of exactly equal T as stacks (seq reads earlier runs' ranks: one tie
 //              level per launch, on the device); if a rank moved against the relaxation's order,
@@ -33,9 +33,7 @@
 // fp64 without contraction, correctly rounded sqrt), so the values are the reference's bits.  The
 // fields and the join are checked bit for bit against the reference's biComputeTmap fixtures (ties
 // included) and the oracle's sequential band on seeded rasters (tests/test_gpu_bidir_exact.py).
-// Cost (profiles/r06m_exact_ab.log): the bench's planner step 1 (4096^2, 2.1 M pops per front)
-// 12.7 ms -> ~0.39 s, of which the relaxation is ~95 % (one event's chain of dependent loads per
-// group sweep, ~11 us, times ~33 k sweeps); an opt-in for bit-identity, not the default.
+// Cost: profiles/r06m_exact_ab.log (the bench's planner step 1, 4096^2, 2.1 M pops per front).
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -66,10 +64,10 @@ struct Front {
 };
 
 struct Ctl {
+    unsigned chunk[2], done[2], changed[2], arrive[2], fresh[2];  // the relaxation's chunk walk
     unsigned act[2];        // fronts still re-ranking
-    unsigned sweeps[2];     // group sweeps of the relaxation (accumulated over passes)
+    unsigned sweeps[2];     // chunk sweeps of the relaxation (per pass)
     unsigned first_bad[2];  // this pass: first rank that moved against the relaxation's order
-    unsigned stuck[2];      // a group did not settle within kGroupSweepCap sweeps
     unsigned longrun;       // a run of equal T too long for exact_ties_kernel (1), or not closed (2)
     unsigned msel;          // FM3D: cells selected for ranking
     double thr;             // FM3D: the selection's bound on T
@@ -154,28 +152,6 @@ __device__ __forceinline__ double events_below(const G& g, const Front& F, int64
     return v;
 }
 
-// V(z, t): what cell z holds when the t-th pop updates its neighbours
-template <class G>
-__device__ __forceinline__ double value_at(const G& g, const Front& F, int64_t z, typename G::Co c, unsigned t) {
-    if (z == F.src) return 0.0;                                          // the source: 0, closed
-    if (!(F.cost[z] < Real<double>::inf())) return Real<double>::inf();  // closed from the start, never updated
-    const unsigned rz = F.rank[z];
-    return events_below(g, F, z, c, rz < t ? rz : t);
-}
-
-// the update of y made by the t-th pop, over y's neighbours as of that pop
-template <class G>
-__device__ __forceinline__ double event_value(const G& g, const Front& F, int64_t y, typename G::Co c, unsigned t,
-                                              double cy) {
-    double v[G::K];
-#pragma unroll
-    for (int d = 0; d < G::K; ++d) {
-        const int64_t j = g.nb(y, c, d);
-        v[d] = j < 0 ? Real<double>::inf() : value_at(g, F, j, g.step(c, d), t);
-    }
-    return g.solve(v, cy);
-}
-
 // is y updated by the pop of rank r?  open: not popped before, not +inf cost, not the source
 __device__ __forceinline__ bool child_open(const Front& F, int64_t y, unsigned r) {
     return y >= 0 && F.rank[y] > r && y != F.src && F.cost[y] < Real<double>::inf();
@@ -214,52 +190,129 @@ __global__ __launch_bounds__(256) void exact_init_kernel(Front F0, Front F1, G g
     }
 }
 
-// 2. relaxation in rank order, Gauss-Seidel: one workgroup per front walks its pops from `from` in
-//    groups of kGroup, sweeping each group's events in place until a sweep changes no event's bits.
-//    An event reads only events of earlier ranks: the groups before are final, so a group settles in
-//    (its own dependency depth + 1) sweeps -- a correction crosses a whole group per sweep instead of
-//    one dependency step per GPU-wide launch.  One workgroup: its waves share the CU's L1, so a
-//    barrier orders their global stores and loads (workgroup scope, no cache maintenance).
-// pops per group, about one event per thread: a group sweep is bound by one event's chain of
-// dependent loads (~11 us), so short groups win -- on the bench's planner query (4096^2, 2.1 M pops
-// per front) 256 / 512 / 1024 / 2048 / 4096 took 376 / 473 / 438 / 477 / 575 ms (33.4 / 24.1 / 11.1 /
-// 6.4 / 3.7 k sweeps); global Jacobi sweeps over all events instead needed 1513 launches, 1.95 s: the
-// band's tentative values chain along the front (profiles/r06m_exact_ab.log)
-constexpr unsigned kGroup = 256;
-constexpr unsigned kGroupSweepCap = 1u << 16;
+// 2. relaxation, chunk by chunk in rank order: each launch sweeps every event of the current chunk of
+//    kChunk pops of each front in place (all of the GPU), and the front's last workgroup advances the
+//    chunk when the sweep changed no event's bits -- the chunk's events are then the unique solution
+//    given the earlier chunks (an event reads only events of earlier ranks).  A chunk's first sweep
+//    resolves every event's inputs (EvDesc: slot, cost, per neighbour its events row, which of them
+//    precede the pop, source / never updated) and stores them; later sweeps of the chunk reload them,
+//    so a sweep is one level of descriptor loads and one of event loads.
+//    History (profiles/r06m_exact_ab.log, the bench's planner query: 4096^2, 2.1 M pops per front):
+//    one in-order workgroup per front (Gauss-Seidel groups of 256 pops) 297 ms -- it settles a group
+//    per latency period where a GPU-wide sweep settles a chunk; GPU-wide Jacobi sweeps over ALL events
+//    1.95 s (1513 launches: the band's tentative values chain along the front).
+constexpr unsigned kChunk = 16384;  // pops per chunk (4 / 6 events each)
+constexpr int kBatch = 32;          // sweeps queued between two reads of the done flags
+constexpr unsigned long long kMaxSweeps = 1ull << 24;
 template <class G>
-__global__ __launch_bounds__(1024) void exact_relax_kernel(Front F0, Front F1, G g, Ctl* ctl) {
-    const int f = blockIdx.y;
-    const Front& F = f ? F1 : F0;
-    if (!ctl->act[f]) return;
-    unsigned sweeps = 0;
-    for (unsigned g0 = (F.from / kGroup) * kGroup; g0 < F.m; g0 += kGroup) {
-        const unsigned g1 = min(g0 + kGroup, F.m);
-        for (unsigned it = 0;; ++it) {
-            bool ch = false;
-            for (unsigned e = G::K * g0 + threadIdx.x; e < G::K * g1; e += blockDim.x) {
-                const unsigned r = e / G::K;
-                const int k = (int)(e - r * G::K);
-                const int64_t c = F.ord[r];
-                const typename G::Co cc = g.co(c);
-                const int64_t y = g.nb(c, cc, k);
-                if (!child_open(F, y, r)) continue;
-                const double v = event_value(g, F, y, g.step(cc, k), r, F.cost[y]);
-                double* slot = F.ev + G::K * y + (k ^ 1);
-                if (__double_as_longlong(*slot) != __double_as_longlong(v)) {
-                    *slot = v;
-                    ch = true;
-                }
-            }
-            ++sweeps;
-            if (!__syncthreads_or(ch)) break;
-            if (it >= kGroupSweepCap) {  // a DAG settles within its depth: never on valid input
-                if (threadIdx.x == 0) ctl->stuck[f] = 1u;
-                return;
-            }
+struct EvDesc {
+    double* slot;  // nullptr: the child is not open (no event)
+    double cost;
+    const double* zev[G::K];
+    unsigned long long mask;  // K bits per neighbour: its events that precede the pop
+    unsigned kinds;           // 2 bits per neighbour: 0 events, 1 source, 2 +inf (never updated, outside)
+};
+template <class G>
+__device__ __forceinline__ void make_desc(const G& g, const Front& F, unsigned e, EvDesc<G>& D) {
+    const unsigned r = e / G::K;
+    const int k = (int)(e - r * G::K);
+    const int64_t c = F.ord[r];
+    const typename G::Co cc = g.co(c);
+    const int64_t y = g.nb(c, cc, k);
+    D.slot = nullptr;
+    if (!child_open(F, y, r)) return;
+    const typename G::Co yc = g.step(cc, k);
+    D.slot = F.ev + G::K * y + (k ^ 1);
+    D.cost = F.cost[y];
+    D.mask = 0ull;
+    D.kinds = 0u;
+#pragma unroll
+    for (int d = 0; d < G::K; ++d) {
+        const int64_t z = g.nb(y, yc, d);
+        D.zev[d] = nullptr;
+        if (z < 0 || (z != F.src && !(F.cost[z] < Real<double>::inf()))) {
+            D.kinds |= 2u << (2 * d);
+            continue;
+        }
+        if (z == F.src) {
+            D.kinds |= 1u << (2 * d);
+            continue;
+        }
+        const unsigned rz = F.rank[z], lim = rz < r ? rz : r;  // V(z, t): events of time < min(t, rank z)
+        const typename G::Co zc = g.step(yc, d);
+        D.zev[d] = F.ev + G::K * z;
+        for (int q = 0; q < G::K; ++q) {
+            const int64_t w = g.nb(z, zc, q);
+            if (w >= 0 && F.rank[w] < lim) D.mask |= 1ull << (G::K * d + q);
         }
     }
-    if (threadIdx.x == 0) ctl->sweeps[f] += sweeps;
+}
+template <class G>
+__device__ __forceinline__ double desc_value(const G& g, const EvDesc<G>& D) {
+    double v[G::K];
+#pragma unroll
+    for (int d = 0; d < G::K; ++d) {
+        const unsigned kd = (D.kinds >> (2 * d)) & 3u;
+        double m = kd == 1u ? 0.0 : Real<double>::inf();
+        if (kd == 0u) {
+#pragma unroll
+            for (int q = 0; q < G::K; ++q)
+                if ((D.mask >> (G::K * d + q)) & 1ull) m = __builtin_fmin(m, D.zev[d][q]);
+        }
+        v[d] = m;
+    }
+    return g.solve(v, D.cost);
+}
+template <class G>
+__global__ __launch_bounds__(256) void exact_sweep_kernel(Front F0, Front F1, G g, Ctl* ctl, EvDesc<G>* desc0,
+                                                          EvDesc<G>* desc1) {
+    const int f = blockIdx.y;
+    const Front& F = f ? F1 : F0;
+    EvDesc<G>* desc = f ? desc1 : desc0;
+    __shared__ unsigned s_chunk, s_done, s_fresh;
+    if (threadIdx.x == 0) {
+        s_done = ctl->done[f];
+        s_chunk = ctl->chunk[f];
+        s_fresh = ctl->fresh[f];
+    }
+    __syncthreads();
+    if (s_done) return;
+    const unsigned r0 = s_chunk * kChunk, r1 = min(r0 + kChunk, F.m);
+    bool ch = false;
+    for (unsigned e = G::K * r0 + blockIdx.x * blockDim.x + threadIdx.x; e < G::K * r1; e += gridDim.x * blockDim.x) {
+        EvDesc<G> D;
+        if (s_fresh) {
+            make_desc(g, F, e, D);
+            desc[e - G::K * r0] = D;
+        } else {
+            D = desc[e - G::K * r0];
+        }
+        if (!D.slot) continue;
+        const double v = desc_value(g, D);
+        if (__double_as_longlong(*D.slot) != __double_as_longlong(v)) {
+            *D.slot = v;
+            ch = true;
+        }
+    }
+    const int any = __syncthreads_or(ch);
+    if (threadIdx.x == 0) {
+        if (any) atomicOr(&ctl->changed[f], 1u);
+        __threadfence();
+        if (atomicAdd(&ctl->arrive[f], 1u) == gridDim.x - 1) {  // the front's last workgroup
+            __threadfence();
+            const unsigned chg = atomicOr(&ctl->changed[f], 0u);
+            ctl->sweeps[f] += 1u;
+            if (!chg) {
+                ctl->chunk[f] = s_chunk + 1u;
+                ctl->fresh[f] = 1u;
+                if ((unsigned long long)(s_chunk + 1u) * kChunk >= F.m) ctl->done[f] = 1u;
+            } else {
+                ctl->fresh[f] = 0u;
+            }
+            ctl->changed[f] = 0u;
+            ctl->arrive[f] = 0u;
+        }
+    }
 }
 
 // the LIFO key of the cell y popped at rank r: its value (the min over its events before r) and seq
@@ -485,6 +538,7 @@ struct ExactLayout {
     double* ev[2];
     unsigned long long *kT, *kT2, *kT3;
     unsigned *kS, *kS2, *val, *val2, *val3, *ord2, *ordp, *flags;
+    void* desc[2];  // EvDesc per event of the current chunk
     char* cub_tmp;
     size_t cub_bytes;
     Ctl* ctl;
@@ -520,6 +574,7 @@ ExactLayout exact_layout(void* work, int64_t n, int K, int64_t m0, int64_t m1, b
         L.ev[f] = reinterpret_cast<double*>(take(sizeof(double) * (on ? (size_t)K * n : 1)));
         L.rank[f] = reinterpret_cast<unsigned*>(take(sizeof(unsigned) * (on ? (size_t)n : 1)));
         L.ord[f] = reinterpret_cast<unsigned*>(take(sizeof(unsigned) * (size_t)std::max<int64_t>(1, m[f])));
+        L.desc[f] = take(on ? (K == Geo2::K ? sizeof(EvDesc<Geo2>) : sizeof(EvDesc<Geo3>)) * (size_t)K * kChunk : 1);
     }
     L.kT = reinterpret_cast<unsigned long long*>(take(8 * (size_t)mx));
     L.kT2 = reinterpret_cast<unsigned long long*>(take(8 * (size_t)mx));
@@ -538,9 +593,16 @@ ExactLayout exact_layout(void* work, int64_t n, int K, int64_t m0, int64_t m1, b
     return L;
 }
 
-__global__ void exact_ctl_kernel(Ctl* ctl, unsigned a0, unsigned a1) {
+__global__ void exact_ctl_kernel(Ctl* ctl, unsigned a0, unsigned a1, unsigned c0, unsigned c1) {
     ctl->act[0] = a0;
     ctl->act[1] = a1;
+    ctl->chunk[0] = c0;
+    ctl->chunk[1] = c1;
+    ctl->done[0] = a0 ? 0u : 1u;
+    ctl->done[1] = a1 ? 0u : 1u;
+    ctl->fresh[0] = ctl->fresh[1] = 1u;
+    ctl->changed[0] = ctl->changed[1] = 0u;
+    ctl->arrive[0] = ctl->arrive[1] = 0u;
     ctl->first_bad[0] = ctl->first_bad[1] = kNoRank;
     ctl->longrun = 0u;
 }
@@ -563,8 +625,24 @@ hipError_t replay(const G& g, Front F[2], int nf, const ExactLayout& L, hipStrea
             if (debug) fprintf(stderr, "[exact] no fixed point after %u passes\n", kMaxPasses);
             return hipErrorNotReady;
         }
-        hipLaunchKernelGGL(exact_ctl_kernel, dim3(1), dim3(1), 0, st, L.ctl, active[0] ? 1u : 0u, active[1] ? 1u : 0u);
-        hipLaunchKernelGGL(exact_relax_kernel<G>, dim3(1, nf), dim3(1024), 0, st, F[0], F[1], g, L.ctl);
+        hipLaunchKernelGGL(exact_ctl_kernel, dim3(1), dim3(1), 0, st, L.ctl, active[0] ? 1u : 0u, active[1] ? 1u : 0u,
+                           F[0].from / kChunk, F[1].from / kChunk);
+        unsigned long long sweeps = 0;
+        for (;;) {  // relax until every active front's last chunk settled
+            for (int q = 0; q < kBatch; ++q)
+                hipLaunchKernelGGL(exact_sweep_kernel<G>, dim3(G::K * kChunk / 256, nf), dim3(256), 0, st, F[0], F[1], g,
+                                   L.ctl, reinterpret_cast<EvDesc<G>*>(L.desc[0]), reinterpret_cast<EvDesc<G>*>(L.desc[1]));
+            sweeps += kBatch;
+            unsigned done[2] = {0, 0};
+            e = hipMemcpyAsync(done, L.ctl->done, sizeof done, hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e != hipSuccess) return e;
+            if (done[0] && done[1]) break;
+            if (sweeps > kMaxSweeps) {
+                if (debug) fprintf(stderr, "[exact] the relaxation did not settle (pass %u)\n", passes);
+                return hipErrorNotReady;
+            }
+        }
         // re-rank every active front from its first relaxed rank
         for (int f = 0; f < nf; ++f) {
             if (!active[f]) continue;
@@ -609,10 +687,6 @@ hipError_t replay(const G& g, Front F[2], int nf, const ExactLayout& L, hipStrea
         e = hipMemcpyAsync(&h, L.ctl, sizeof h, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) return e;
-        if (h.stuck[0] || h.stuck[1]) {
-            if (debug) fprintf(stderr, "[exact] a relaxation group did not settle (pass %u)\n", passes);
-            return hipErrorNotReady;
-        }
         if (h.longrun) return hipErrorNotSupported;
         info[1] += h.sweeps[0];
         info[2] += h.sweeps[1];
