@@ -71,6 +71,8 @@ struct Ctl {
     unsigned longrun;       // a run of equal T too long for exact_ties_kernel (1), or not closed (2)
     unsigned msel;          // FM3D: cells selected for ranking
     double thr;             // FM3D: the selection's bound on T
+    unsigned long long nmin[2];  // biComputeTmap: bits of the smallest field value of an unranked finite cell
+    unsigned edge;               // biComputeTmap: the meeting's value is not clear of that bound
 };
 
 // The grids.  Children (= neighbours) in the reference's updateNode order, opposite directions
@@ -494,6 +496,42 @@ __device__ __forceinline__ double field_value(const G& g, const Front& F, int64_
     return events_below(g, F, i, g.co(i), lim);  // (+inf when no neighbour popped)
 }
 
+// biComputeTmap ranks only the join's member prefix (every cell of field value up to a bucket edge);
+// the replay's order is valid if no unranked cell could pop before the meeting: the meeting's exact
+// value must stay below every unranked finite cell's field value by more than their ~1e-13 agreement
+__global__ __launch_bounds__(256) void exact_nmin_kernel(Front F0, Front F1, int64_t n, Ctl* ctl) {
+    const int f = blockIdx.y;
+    const Front& F = f ? F1 : F0;
+    unsigned long long m = ~0ull;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const double t = F.T[i];
+        if (F.rank[i] == kNoRank && t < Real<double>::inf()) {
+            const unsigned long long v = (unsigned long long)__double_as_longlong(t);
+            m = v < m ? v : m;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(m, off, 64);
+        m = o < m ? o : m;
+    }
+    if ((threadIdx.x & 63) == 0 && m != ~0ull) atomicMin(&ctl->nmin[f], m);
+}
+__global__ void exact_edge_kernel(Front F0, Front F1, Geo2 g, const unsigned long long* best, Ctl* ctl) {
+    const unsigned long long b = *best;
+    if (threadIdx.x >= 2 || b == ~0ull) return;
+    const Front& F = threadIdx.x ? F1 : F0;
+    const unsigned k = (unsigned)(b >> 30);
+    if (k >= F.m) {
+        ctl->edge = 1u;
+        return;
+    }
+    const unsigned long long nm = ctl->nmin[threadIdx.x];
+    if (nm == ~0ull) return;  // every finite cell is ranked
+    unsigned sq;
+    const double t = pop_key(g, F, F.ord[k], k, &sq);
+    if (!(t < __longlong_as_double((long long)nm) * (1.0 - 0x1p-30))) ctl->edge = 1u;
+}
+
 __global__ void exact_fields_bidir_kernel(Front F0, Front F1, Geo2 g, const unsigned long long* best) {
     const Front& F = blockIdx.y ? F1 : F0;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -610,8 +648,7 @@ __global__ void exact_ctl_kernel(Ctl* ctl, unsigned a0, unsigned a1, unsigned c0
 // steps 1-3 for nf fronts (F[0..nf-1]) whose rank / ord arrays hold a first order of their m cells
 template <class G>
 hipError_t replay(const G& g, Front F[2], int nf, const ExactLayout& L, hipStream_t st, unsigned long long info[4]) {
-    hipError_t e = hipMemsetAsync(L.ctl, 0, sizeof(Ctl), st);
-    if (e != hipSuccess) return e;
+    hipError_t e = hipSuccess;  // (the caller cleared Ctl)
     {
         const int64_t mx = std::max(F[0].m, nf > 1 ? F[1].m : 0u);
         const unsigned gi = (unsigned)std::max<int64_t>(1, std::min<int64_t>(4096, ((int64_t)G::K * mx + 255) / 256));
@@ -737,12 +774,25 @@ hipError_t bidir_exact(double* d_TG, double* d_TS, const double* d_cost, int64_t
     if (members[0] <= 0 || members[1] <= 0) return hipErrorInvalidValue;  // (the join found no meeting)
     const unsigned ng = (unsigned)((n + 255) / 256);
     hipLaunchKernelGGL(exact_order_kernel, dim3(ng, 2), dim3(256), 0, st, F[0], F[1], n);
+    e = hipMemsetAsync(L.ctl, 0, sizeof(Ctl), st);
+    if (e == hipSuccess) e = hipMemsetAsync(L.ctl->nmin, 0xFF, sizeof(L.ctl->nmin), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(exact_nmin_kernel, dim3((unsigned)std::min<int64_t>(1024, ng), 2), dim3(256), 0, st, F[0], F[1], n,
+                       L.ctl);
     e = replay(g, F, 2, L, st, info);
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(d_best, 0xFF, sizeof(unsigned long long), st);
     if (e != hipSuccess) return e;
     e = bidir_join_min(L.rank[0], L.rank[1], n, d_best, st);
     if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(exact_edge_kernel, dim3(1), dim3(64), 0, st, F[0], F[1], g, d_best, L.ctl);
+    {
+        unsigned edge = 0;
+        e = hipMemcpyAsync(&edge, &L.ctl->edge, sizeof edge, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return e;
+        if (edge) return hipErrorIllegalState;
+    }
     hipLaunchKernelGGL(exact_fields_bidir_kernel, dim3(ng, 2), dim3(256), 0, st, F[0], F[1], g, d_best);
     return hipGetLastError();
 }
@@ -757,10 +807,12 @@ hipError_t fm3d_exact(const double* d_cost, const double* d_T, double* d_Te, int
     const ExactLayout L = exact_layout(d_work, n, Geo3::K, n, 0, true);
     if (L.total > work_bytes) return hipErrorOutOfMemory;
     const Geo3 g{H, W, L3};
+    hipError_t e = hipMemsetAsync(L.ctl, 0, sizeof(Ctl), st);
+    if (e != hipSuccess) return e;
     // the cells to rank (node order), their first order by T (stable: ties by node)
     hipLaunchKernelGGL(exact_thr_kernel, dim3(1), dim3(1), 0, st, d_T, start_off, L.ctl);
     size_t b = L.cub_bytes;
-    hipError_t e = hipcub::DeviceSelect::If(L.cub_tmp, b, hipcub::CountingInputIterator<unsigned>(0u), L.val, &L.ctl->msel,
+    e = hipcub::DeviceSelect::If(L.cub_tmp, b, hipcub::CountingInputIterator<unsigned>(0u), L.val, &L.ctl->msel,
                                             n, Fm3dMember{d_T, L.ctl}, st);
     if (e != hipSuccess) return e;
     unsigned m = 0;

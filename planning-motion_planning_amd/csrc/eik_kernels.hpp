@@ -260,7 +260,8 @@ hipError_t bidir_join_min(const unsigned* d_rg, const unsigned* d_rs, int64_t n,
 // order from the join's ranks d_rg / d_rs (members[f] cells ranked per front) over the device cost;
 // d_TG / d_TS (the converged fields) become the partial fields, *d_best the exact join.  info
 // (accumulated): passes, relaxation sweeps G, S, tie-run launches.  hipErrorNotReady: no fixed point
-// within the caps; hipErrorNotSupported: a run of more than 4096 exactly equal T (a zero-cost region).
+// within the caps; hipErrorNotSupported: a run of more than 4096 exactly equal T (a zero-cost region);
+// hipErrorIllegalState: the exact meeting is not clear of the ranked prefix's bound (never expected).
 size_t bidir_exact_work_bytes(int64_t n, int64_t m0, int64_t m1);
 hipError_t bidir_exact(double* d_TG, double* d_TS, const double* d_cost, int64_t H, int64_t W, int64_t gnode,
                        int64_t snode, const unsigned* d_rg, const unsigned* d_rs, const int64_t members[2],

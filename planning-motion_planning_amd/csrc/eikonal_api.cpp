@@ -1305,13 +1305,15 @@ static int join_and_partial(eik_ctx* c, double* dT, int64_t n, int64_t H, int64_
         unsigned long long info[4] = {0, 0, 0, 0};
         const hipError_t e = bidir_exact(dT, dT + n, d_cost, H, W, src[0], src[1], rg, rs, members, c->exact.p,
                                          c->exact.bytes, (unsigned long long*)c->misc.p, st, info);
-        if (e == hipErrorNotReady || e == hipErrorNotSupported) {
+        if (e == hipErrorNotReady || e == hipErrorNotSupported || e == hipErrorIllegalState) {
             (void)hipEventDestroy(e0);
             (void)hipEventDestroy(e1);
-            return set_err(c, EIK_ERR_NOCONVERGE, e == hipErrorNotReady
-                                                      ? "biComputeTmap: the exact band replay did not settle"
-                                                      : "biComputeTmap: the exact band replay met a run of more than "
-                                                        "4096 cells of exactly equal T (a zero-cost region)");
+            return set_err(c, EIK_ERR_NOCONVERGE,
+                           e == hipErrorNotReady      ? "biComputeTmap: the exact band replay did not settle"
+                           : e == hipErrorNotSupported ? "biComputeTmap: the exact band replay met a run of more than "
+                                                         "4096 cells of exactly equal T (a zero-cost region)"
+                                                       : "biComputeTmap: the exact meeting is not clear of the ranked "
+                                                         "cells' bound");
         }
         HIPCHK(c, e);
         HIPCHK(c, hipEventRecord(e1, st));
