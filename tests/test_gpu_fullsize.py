@@ -5,6 +5,8 @@
   path against the oracle's walk on the oracle's field; the fp32 field -- masks equal, max
   relative error <= 2e-5 -- and the path kernel on it against the oracle's walk on
   the same field, <= 1e-9 cells.
+* C2 bidirectional with EIK_OPT_EXACT_BAND: nodeJoin and both partial fields bit-identical to the
+  oracle's sequential band (biComputeTmap, goal at the centre, start at (256, 256)).
 * C3, 128 x 1024^2 batch: one batched solve, four of its maps against the oracle.
 * C4, 16384^2 DEM raster on one GPU: too large for the oracle inside a test, so size-independent
   properties of the converged field, evaluated on the device in fp64: T[goal] = 0; every reached
@@ -114,6 +116,34 @@ def test_c2_full_size_fp64_vs_oracle(env):
     ref, rst = O.gdm2d(R, np.array(start, float), np.array(goal, float))
     assert st == rst == 0 and path.shape == ref.shape and len(path) > 1000
     assert np.abs(path - ref).max() <= 1e-6
+
+
+def test_c2_full_size_bidirectional_exact_band(env):
+    """biComputeTmap on the 4096^2 C2 raster with EIK_OPT_EXACT_BAND (goal at the centre, start at
+    (256, 256), the bench's ms-to-path query): nodeJoin and both partial fields bit-identical to the
+    oracle's sequential band (orc_fmm2d_bidir, the reference's algorithm) -- the replay at full size,
+    ~2 M pops per front, on the capped-fronts path."""
+    torch, eikonal, L, terrain, dev, ctx = env
+    N = 4096
+    cost = terrain.cost_block(0, 0, N, N, N, N, seed=42, device=dev).double().contiguous().cpu().numpy()
+    goal, start = (N // 2, N // 2), (256, 256)
+    c = eikonal.Context(0)
+    try:
+        c.set_option(L.OPT_EXACT_BAND, 1)
+        TG, TS, join = c.tmap2d_bidir(cost, goal, start)
+        info, fr = c.exact_info(), c.fronts_info()
+    finally:
+        c.close()
+    O.set_strict(False)
+    try:
+        RG, RS, rj = O.fmm2d_bidir(cost, goal, start)
+    finally:
+        O.set_strict(True)
+    assert info["passes"] >= 1 and fr["capped"], (info, fr)
+    assert np.array_equal(join, rj), (join, rj)
+    for A, B in ((TG, RG), (TS, RS)):
+        assert np.array_equal(np.isfinite(A), np.isfinite(B))
+        assert np.array_equal(A.view(np.uint64), B.view(np.uint64)), int((A != B).sum())
 
 
 def test_c2_full_size_fp64_priority_bands(env):
