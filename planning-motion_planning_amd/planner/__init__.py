@@ -7,8 +7,12 @@ FM.getPathGDM descents from nodeJoin (:1225-1226) -> one path in metres with z a
 (eik_rover_path_f64: cost builder, both fronts as one fp64 batch, device join, path kernels),
 with the host tail (eik_rover_assemble) bit-identical to the reference's numpy statements.
 The join is evaluated from the two full fields' pop ranks (ties ranked by node index), see
-FastMarching.biComputeTmap.
+FastMarching.biComputeTmap; EIKONAL_EXACT_BAND=1 (read per call, as the FastMarching drop-ins do)
+replays the reference's own band instead -- its nodeJoin and partial fields bit for bit, and the
+end-effector early exit's band (EIK_OPT_EXACT_BAND).
 """
+import os
+
 import numpy as np
 
 from eikonal import _lib as L
@@ -25,6 +29,7 @@ def _ctx():
         import eikonal
 
         _ctx_obj = eikonal.Context(0)
+    _ctx_obj.set_option(L.OPT_EXACT_BAND, 1 if os.environ.get("EIKONAL_EXACT_BAND", "0") not in ("", "0") else 0)
     return _ctx_obj
 
 

@@ -94,6 +94,27 @@ def test_rover_path_exact_band_matches_oracle_chain(n, seed):
     assert np.abs(got_p[:, :2] - ref_p[:, :2]).max() / RES <= 1e-6
 
 
+def test_rover_path_exact_switch(monkeypatch):
+    """planner.rover_path reads EIKONAL_EXACT_BAND per call, like the FastMarching drop-ins."""
+    n, seed = 160, 5
+    Z = terrain_np.dem(n, n, seed=seed) + 3.0
+    size = RES * n
+    cref, _ = PO.CO.cost_map(Z, RES, size)
+    cT = cref.T
+    sx, sy = free_cell(cT, int(0.78 * n), int(0.72 * n))
+    rx, ry = free_cell(cT, int(0.2 * n), int(0.25 * n))
+    xm, ym, xr, yr = RES * (sx + 1), RES * (sy + 1), RES * (rx + 1), RES * (ry + 1)
+    ref_p, _, ref_j, _ = PO.rover_path(Z, xm, ym, xr, yr, 0.4, RES, size)
+    monkeypatch.setenv("EIKONAL_EXACT_BAND", "1")
+    got_p, _, got_j = planner.rover_path(Z, xm, ym, xr, yr, 0.4, RES, size)
+    assert planner._ctx().exact_info()["passes"] >= 1
+    assert np.array_equal(got_j, ref_j) and got_p.shape == ref_p.shape
+    assert np.abs(got_p[:, :2] - ref_p[:, :2]).max() / RES <= 1e-6
+    monkeypatch.setenv("EIKONAL_EXACT_BAND", "0")
+    planner.rover_path(Z, xm, ym, xr, yr, 0.4, RES, size)
+    assert planner._ctx().exact_info()["passes"] == 0
+
+
 def test_rover_path_unreachable():
     """Rover on the corner node (0, 0): both its neighbours are +inf border cells.  The reference's
     fronts still "meet" there by popping +inf band entries and return a degenerate path; the GPU
