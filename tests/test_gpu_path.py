@@ -75,7 +75,8 @@ def test_bidirectional(ctx, golden, i):
     fronts' PARTIAL fields (finite masks; closed values equal, band values at their final value,
     bracketed GPU <= reference <= 1.03 x GPU) and the rover path, truncated or not, as the
     reference returns it.  Maps with exact ties of T (uniform, b0/b1): the reference pops ties
-    LIFO, the GPU by node index, so a few tied cells at the fronts' edges may differ."""
+    LIFO, the default mode by node index, so a few tied cells at the fronts' edges may differ
+    (EIK_OPT_EXACT_BAND removes both tolerances: tests/test_gpu_bidir_exact.py)."""
     d = golden("fmm2d_bidir")
     p = f"b{i}_"
     ties = i < 2
