@@ -73,13 +73,21 @@ int main(int argc, char** argv) {
     // priority bands as eikonal_api.cpp sets them up (width multiplier 1)
     CK(hipMalloc(&a.ecol, esz * 2 * 64ull * tiles));
     const bool prio = getenv("EIK_TRACE_PRIO") && atoi(getenv("EIK_TRACE_PRIO")) == 1;
+    // (rings of >= 2 x the tiles, then the per-tile band-membership words, as setup_bands lays them
+    // out; width EIK_TRACE_PRIO_W, default 0.25 = the library's default at 4096^2; dispatch batch 16)
+    size_t bbytes = 0;
     if (prio) {
         unsigned long long bc = 1024; while (bc < 2ull * tiles) bc <<= 1;
-        CK(hipMalloc(&a.bslot, 4ull * kBands * bc)); CK(hipMemset(a.bslot, 0, 4ull * kBands * bc));
+        const size_t ring = 4ull * kBands * bc, moff = (ring + 255) & ~(size_t)255;
+        bbytes = moff + 8ull * tiles;
+        CK(hipMalloc(&a.bslot, bbytes)); CK(hipMemset(a.bslot, 0, bbytes));
+        a.bmem = (unsigned long long*)((char*)a.bslot + moff);
         CK(hipMalloc(&a.bctl, 128 * kBands + 128)); a.bmask = (unsigned)(bc - 1);
         float* pd = (float*)((char*)a.bctl + 128 * kBands);
-        CK(fim2d_prio_delta(cost, f64, (int64_t)N * N, 1.f, pd, 0));
+        const float w = getenv("EIK_TRACE_PRIO_W") ? (float)atof(getenv("EIK_TRACE_PRIO_W")) : 0.25f;
+        CK(fim2d_prio_delta(cost, f64, (int64_t)N * N, w, pd, 0));
         a.pdelta = pd;
+        a.disp = 16;
     }
     a.fresh_first = getenv("EIK_FRESH_FIRST") && atoi(getenv("EIK_FRESH_FIRST")) == 1;
     a.sched = getenv("EIK_SCHED") ? atoi(getenv("EIK_SCHED")) : 1;  // library default
@@ -89,6 +97,7 @@ int main(int argc, char** argv) {
     for (int rep = 0; rep < 4; ++rep) {
         CK(hipMemset(a.visits, 0, 256)); CK(hipMemset(ev, 0, 8ull * kCap * grid));
         if (a.bctl) CK(hipMemset(a.bctl, 0, 128 * kBands));
+        if (a.bslot) CK(hipMemset(a.bslot, 0, bbytes));
         CK(fim2d_init(a, f64, 1, goals, nullptr, 0));
         CK(hipEventRecord(e0, 0));
         CK(fim2d_persist(a, f64, grid, 0));
