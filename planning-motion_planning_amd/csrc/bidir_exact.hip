@@ -397,7 +397,7 @@ __global__ void exact_moved_kernel(Front F, const unsigned* sorted, int64_t cnt,
 constexpr int64_t kMaxRun = 4096;
 template <class G>
 __global__ void exact_ties_kernel(Front F, G g, const unsigned long long* kT, int64_t cnt, unsigned* flags, int s,
-                                  unsigned* longrun, unsigned* out_buf, unsigned* stack_buf) {
+                                  unsigned* longrun, unsigned* out_buf, unsigned* stack_buf, unsigned* pushed_buf) {
     if (s > 0 && flags[s - 1] == 0u) return;
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j + 1 >= cnt || kT[j + 1] != kT[j] || (j > 0 && kT[j - 1] == kT[j])) return;  // run starts only
@@ -411,8 +411,8 @@ __global__ void exact_ties_kernel(Front F, G g, const unsigned long long* kT, in
     const unsigned r0 = F.from + (unsigned)j, r1 = r0 + (unsigned)L;
     unsigned* out = out_buf + j;
     unsigned* stk = stack_buf + j;
-    unsigned pushed[kMaxRun / 32];
-    for (int w = 0; w < kMaxRun / 32; ++w) pushed[w] = 0u;
+    unsigned* pushed = pushed_buf + j;  // per member (the run's own slice of a free buffer, no scratch)
+    for (int a = 0; a < L; ++a) pushed[a] = 0u;
     // roots in ascending seq: the top of the stack is the latest insertion
     int sp = 0;
     unsigned* sseq = out;  // (the roots' seq, beside the stack, until the output is written)
@@ -429,7 +429,7 @@ __global__ void exact_ties_kernel(Front F, G g, const unsigned long long* kT, in
         }
         stk[b] = (unsigned)y;
         sseq[b] = sq;
-        pushed[a >> 5] |= 1u << (a & 31);
+        pushed[a] = 1u;
     }
     // pop: the output overwrites sseq from the front, which the stack no longer needs (sseq[i] is
     // only read while sorting the roots in)
@@ -445,11 +445,11 @@ __global__ void exact_ties_kernel(Front F, G g, const unsigned long long* kT, in
             const unsigned ry = F.rank[y];
             if (ry < r0 || ry >= r1) continue;  // not in this run
             const int a = (int)(ry - r0);
-            if (pushed[a >> 5] & (1u << (a & 31))) continue;
+            if (pushed[a]) continue;
             unsigned sq;
             (void)pop_key(g, F, y, r1, &sq);
             if (sq != (unsigned)G::K * rp + (unsigned)k) continue;  // p's update did not set y's value
-            pushed[a >> 5] |= 1u << (a & 31);
+            pushed[a] = 1u;
             stk[sp++] = (unsigned)y;
         }
     }
@@ -705,7 +705,7 @@ hipError_t replay(const G& g, Front F[2], int nf, const ExactLayout& L, hipStrea
                 if (e != hipSuccess) return e;
                 for (int q = 0; q < kTieBatch; ++q)
                     hipLaunchKernelGGL(exact_ties_kernel<G>, dim3(gk), dim3(256), 0, st, F[f], g, L.kT3, cnt, L.flags, q,
-                                       &L.ctl->longrun, L.ord2, L.val2);
+                                       &L.ctl->longrun, L.ord2, L.val2, L.val3);
                 unsigned hf[kTieBatch];
                 e = hipMemcpyAsync(hf, L.flags, sizeof hf, hipMemcpyDeviceToHost, st);
                 if (e == hipSuccess) e = hipStreamSynchronize(st);
