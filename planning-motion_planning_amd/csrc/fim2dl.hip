@@ -54,6 +54,33 @@ template <> struct LCell<double> {
 #define EIK_L32_ROWS 64
 #endif
 template <typename R> constexpr int kRowsOf = sizeof(R) == 4 ? EIK_L32_ROWS : EIK_L64_ROWS;
+// EIK_LSPLIT (round 6, verdict r05 item 5): more than one wave per SIMD for the layered sweep.  The
+// tile (one per CU: 156 KB of LDS fp32, 155 KB fp64) is swept by 4 x G waves: wave w runs quadrant
+// direction w & 3 on the layer group g = w >> 2 (kLZ0: {0, 1} and {2} for 3 layers in 2 groups).  A layer's chain
+// only ever reads its own register state and the other layers through LDS (the z neighbours are the
+// read-ahead LDS values, Jacobi in z within a step -- sweep_layered), so the layers partition across
+// waves with no new synchronisation: each SIMD interleaves G dependent chains instead of one wave's NL
+// chains.  Waves 4.. only sweep (staging, write-back, halo and queue roles stay on waves 0..3) and pass
+// the same workgroup barriers.  G = min(NL, EIK_LSPLIT_F32 / _F64); 1 = the one-wave-per-SIMD kernel.
+#ifndef EIK_LSPLIT_F32
+#define EIK_LSPLIT_F32 2
+#endif
+#ifndef EIK_LSPLIT_F64
+#define EIK_LSPLIT_F64 2
+#endif
+template <typename R, int NL>
+constexpr int kLGroups = (sizeof(R) == 4 ? EIK_LSPLIT_F32 : EIK_LSPLIT_F64) < NL ? (sizeof(R) == 4 ? EIK_LSPLIT_F32 : EIK_LSPLIT_F64) : NL;
+template <typename R, int NL> constexpr int kLThreads = kLGroups<R, NL> * kThreads;
+// first layer of group g: the groups' sizes rounded up from the first (3 layers in 2 groups: {0, 1}, {2} --
+// the main waves take the larger share: 6.3 -> 7.2 Gcells/s on C5 fp32, against 6.7 for {0}, {1, 2})
+#ifndef EIK_LSPLIT_CEIL
+#define EIK_LSPLIT_CEIL 1
+#endif
+// EIK_LSPLIT_ROWS: the sweep-only waves share the staging and write-back rows (1, default) or only sweep (0)
+#ifndef EIK_LSPLIT_ROWS
+#define EIK_LSPLIT_ROWS 1
+#endif
+template <int NL, int G> constexpr int kLZ0(int g) { return EIK_LSPLIT_CEIL ? (g * NL + G - 1) / G : g * NL / G; }
 
 // EIK_FRESH_SKIP_L: a full tile's first visit stages only the cost -- its T layers are still the init
 // kernel's +inf (the seed kernel queues the goal's tile as visited), as fim2d.hip's kFreshSkip
@@ -190,7 +217,7 @@ __device__ __forceinline__ double min_nn(double a, double b) { return fmin_nn(a,
 #define EIK_STRL_(x) #x
 #define EIK_UNROLL_L_(n) _Pragma(EIK_STRL_(unroll n))
 #define EIK_UNROLL_L(n) EIK_UNROLL_L_(n)
-template <typename R, int TH, int NL, int DX, int DY>
+template <typename R, int TH, int NL, int DX, int DY, int Z0 = 0, int Z1 = NL>
 __device__ __forceinline__ void sweep_layered(LCell<R>* __restrict__ Ts, int lane) {
     constexpr R INF = Real<R>::inf();
     constexpr int S = (int)sizeof(LCell<R>);
@@ -212,9 +239,9 @@ __device__ __forceinline__ void sweep_layered(LCell<R>* __restrict__ Ts, int lan
         return r;
     };
     const LCell<R> h = ld((DY > 0 ? 0 : TH + 1) * kRow + col * S);
-    R cur[NL];
+    R cur[NL];  // (layers outside [Z0, Z1) are another wave's: unused here)
 #pragma unroll
-    for (int z = 0; z < NL; ++z) cur[z] = h.get(z);
+    for (int z = Z0; z < Z1; ++z) cur[z] = h.get(z);
     LCell<R> q_old[D], q_upx[D], q_c[D];
     int gb = clampb(raw);  // lowest row of the group being fetched
     raw += DY * D * kRow;
@@ -235,7 +262,7 @@ __device__ __forceinline__ void sweep_layered(LCell<R>* __restrict__ Ts, int lan
         for (int u = 0; u < D; ++u) {
             R* const cell = reinterpret_cast<R*>(base + gcur + off(u));
 #pragma unroll
-            for (int z = 0; z < NL; ++z) {
+            for (int z = Z0; z < Z1; ++z) {
                 const R old = q_old[u].get(z);
                 const R ux = upstream_x(cur[z], q_upx[u].get(z));
                 // layer neighbours; an end layer has one (the minima are inline asm, which the
@@ -268,20 +295,31 @@ __device__ __forceinline__ void sweep_layered(LCell<R>* __restrict__ Ts, int lan
 #endif
 
 // Stage, sweep and write back one layered tile (cf. process_tile in fim2d.hip).  Thread t owns
-// cells t + 256 j (j < TH / 4): row (t >> 6) + 4 j, column t & 63 -- a wave reads whole tile rows,
+// cells t + 64 RW j (j < TH / RW): row (t >> 6) + RW j, column t & 63 -- a wave reads whole tile rows,
 // i.e. 64 * ls contiguous values per layer load.  Leaves L.flags (bits 0..3: neighbour N/S/W/E
 // can improve; 128: some cell decreased by more than the tolerance).
 template <typename R, int NL, bool COH>
 __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int tile, TileLdsL<R, kRowsOf<R>>& L,
                                                      float keep) {
     constexpr int TH = kRowsOf<R>;
-    constexpr int NJ = TH / 4;  // cells per thread
+    // staging and write-back rows: wave r of the RW row waves owns rows r, r + RW, ... (EIK_LSPLIT: the
+    // sweep-only waves share them when the rows divide -- half the told[] registers and half the rows per
+    // thread at a pass boundary)
+    constexpr int G = kLGroups<R, NL>;
+    constexpr int RW = EIK_LSPLIT_ROWS && TH % (4 * G) == 0 ? 4 * G : 4;
+    constexpr int NJ = TH / RW;  // cells per thread
     constexpr R INF = Real<R>::inf();
     const R INFS[4] = {INF, INF, INF, INF};
     const LCell<R> INFC = LCell<R>::make(INFS);
     LCell<R>* const Ts = L.Tbuf + kGuard * kLds;
     LCell<R>* const Cs = L.Cbuf + kGuard * kLds;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    // waves 0..3: halo ring and queue roles, the first layer group's sweeps; waves 4.. (EIK_LSPLIT): the other
+    // groups' sweeps; the RW row waves: staging and write-back
+    const int wave = (tid >> 6) & 3;
+    const bool main = tid < kThreads;
+    const int rw = tid >> 6;
+    const bool stager = rw < RW;
     const int map = tile / a.tiles_per_map;
     const int rem = tile - map * a.tiles_per_map;
     const int ty = rem / a.ntx, tx = rem - (rem / a.ntx) * a.ntx;
@@ -312,7 +350,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
     else if (wave == 1) { h = (TH + 1) * kLds + lane + 1;   hy = y0 + TH;     hx = x0 + lane; }
     else if (wave == 2) { h = (lane + 1) * kLds + 0;        hy = y0 + lane;   hx = x0 - 1; }
     else                { h = (lane + 1) * kLds + kLds - 1; hy = y0 + lane;   hx = x0 + kTile; }
-    const bool hcell = wave < 2 || lane < TH;
+    const bool hcell = main && (wave < 2 || lane < TH);
     const bool hin = hcell && hy >= 0 && hy < a.H && hx >= 0 && hx < a.W;
     const int64_t hgi = hin ? (hy * a.W + hx) * ls + a.z0 : 0;
     // domain decomposition: the halo cell just outside the block comes from the side's ghost strip, nl
@@ -344,7 +382,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
     auto store_tile = [&](const R (&cc)[NJ][NL], LCell<R> hv) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-            const int ry = wave + 4 * j;
+            const int ry = rw + RW * j;
             R t4[4] = {INF, INF, INF, INF}, c4[4] = {INF, INF, INF, INF};
 #pragma unroll
             for (int z = 0; z < NL; ++z) {
@@ -361,11 +399,13 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
         if constexpr (sizeof(R) == 8) return (c >= R(0) && c < 0x1p-500) ? R(0x1p-500) : c;  // NaN stays NaN
         else return c;
     };
-    if (COH && kFreshSkipL && y0 + TH <= a.H && x0 + kTile <= a.W && __builtin_amdgcn_readfirstlane(L.fresh)) {
+    if (!stager) {
+        // (EIK_LSPLIT: the sweep-only waves stage nothing unless they own rows)
+    } else if (COH && kFreshSkipL && y0 + TH <= a.H && x0 + kTile <= a.W && __builtin_amdgcn_readfirstlane(L.fresh)) {
         R cc[NJ][NL];
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-            const int64_t gi = ((y0 + wave + 4 * j) * a.W + x0 + lane) * ls + a.z0;
+            const int64_t gi = ((y0 + rw + RW * j) * a.W + x0 + lane) * ls + a.z0;
 #pragma unroll
             for (int z = 0; z < NL; ++z) {
                 told[j][z] = INF;
@@ -378,7 +418,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
         R cc[NJ][NL];
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-            const int64_t gi = ((y0 + wave + 4 * j) * a.W + x0 + lane) * ls + a.z0;
+            const int64_t gi = ((y0 + rw + RW * j) * a.W + x0 + lane) * ls + a.z0;
 #pragma unroll
             for (int z = 0; z < NL; ++z) {
                 told[j][z] = Tz[z].ld(gi - b0);
@@ -390,7 +430,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
         R cc[NJ][NL];
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-            const int64_t gy = y0 + wave + 4 * j, gx = x0 + lane;
+            const int64_t gy = y0 + rw + RW * j, gx = x0 + lane;
             const bool in = gy < a.H && gx < a.W;
             const int64_t gi = in ? (gy * a.W + gx) * ls + a.z0 : 0;
             // a block's south / east ghost cells inside a tile cut by the block's end: the ghost's
@@ -408,7 +448,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
         store_tile(cc, load_halo());
     }
     if (hcell) Cs[h] = INFC;
-    if (lane < 4) {
+    if (main && lane < 4) {
         const int corner = (lane >> 1) * (TH + 1) * kLds + (lane & 1) * (kLds - 1);
         Cs[corner] = INFC;
         Ts[corner] = INFC;
@@ -426,19 +466,32 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
             act_tile = -1;
         }
         if ((dirs >> wave) & 1u) {
-            if (wave == 0)      sweep_layered<R, TH, NL, +1, +1>(Ts, lane);
-            else if (wave == 1) sweep_layered<R, TH, NL, -1, +1>(Ts, lane);
-            else if (wave == 2) sweep_layered<R, TH, NL, +1, -1>(Ts, lane);
-            else                sweep_layered<R, TH, NL, -1, -1>(Ts, lane);
+            const int grp = tid >> 8;  // wave-uniform
+            auto run = [&](auto gc) {
+                constexpr int g = decltype(gc)::value, Z0 = kLZ0<NL, G>(g), Z1 = kLZ0<NL, G>(g + 1);
+                if (wave == 0)      sweep_layered<R, TH, NL, +1, +1, Z0, Z1>(Ts, lane);
+                else if (wave == 1) sweep_layered<R, TH, NL, -1, +1, Z0, Z1>(Ts, lane);
+                else if (wave == 2) sweep_layered<R, TH, NL, +1, -1, Z0, Z1>(Ts, lane);
+                else                sweep_layered<R, TH, NL, -1, -1, Z0, Z1>(Ts, lane);
+            };
+            if (grp == 0) run(std::integral_constant<int, 0>{});
+            else if constexpr (G > 1) {
+                if (grp == 1) run(std::integral_constant<int, 1>{});
+                else if constexpr (G > 2) {
+                    if (grp == 2) run(std::integral_constant<int, 2>{});
+                    else if constexpr (G > 3) run(std::integral_constant<int, 3>{});
+                }
+            }
         }
         __syncthreads();
         // ---- write back changed cells, collect side flags (priority bands: and the entering keys,
         // the smallest improved value per side and overall, as fim2d.hip's write-back)
         unsigned fl = 0;
         R kmin_self = INF, kmin[4] = {INF, INF, INF, INF};
+        if (stager) {  // (EIK_LSPLIT: only the row waves store)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-            const int ry = wave + 4 * j;
+            const int ry = rw + RW * j;
             const int64_t gy = y0 + ry, gx = x0 + lane;
             const bool in = gy < a.H && gx < a.W;
             const int64_t gi = (gy * a.W + gx) * ls + a.z0;
@@ -459,6 +512,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
                 told[j][z] = nv;  // what memory holds now
             }
         }
+        }
         if (fl) atomicOr(&L.flags, fl);
         if (a.bctl) {  // priority bands: the entering keys (f32 bits: T >= 0)
             if (kmin_self < INF) atomicMin(&L.key[0], __float_as_uint((float)kmin_self));
@@ -472,7 +526,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
         if (!(f & 128u) || pass + 1 >= kPasses) break;
         // the halo reload is issued first and the budget charge goes to wave 1, so wave 0's
         // activation atomics are the only round trips the next pass waits for
-        const LCell<R> hv = load_halo();
+        const LCell<R> hv = hcell ? load_halo() : INFC;
         if (tid == 64) charge_inplace_pass(a);  // in-place passes: stats and the visit budget
         if constexpr (COH && EIK_ACT_SPLIT_L)
             act_tile = activate_neighbours_issue(a, tile, f, act_old, L.key, act_k, act_kold);  // queued as the next pass starts
@@ -545,7 +599,7 @@ __device__ __forceinline__ void live_agent_layered(const Fim2dArgs& a, unsigned*
 // Persistent driver (cf. fim2d_persist_kernel): one launch per solve, device FIFO of tiles.  A live
 // launch (a.live: a decomposition block on dd.solve_live) keeps workgroup 0 as its halo agent.
 template <typename R, int NL>
-__global__ __launch_bounds__(kThreads) void fim2dl_persist_kernel(Fim2dArgs a) {
+__global__ __launch_bounds__((kLThreads<R, NL>)) void fim2dl_persist_kernel(Fim2dArgs a) {
     constexpr int TH = kRowsOf<R>;
     __shared__ TileLdsL<R, TH> L;
     if (a.live && blockIdx.x == 0) {
@@ -555,7 +609,7 @@ __global__ __launch_bounds__(kThreads) void fim2dl_persist_kernel(Fim2dArgs a) {
     }
     constexpr R INF = Real<R>::inf();
     const R INFS[4] = {INF, INF, INF, INF};
-    for (int i = threadIdx.x; i < kGuard * kLds; i += kThreads) {  // guard rows: read by sweeps, never lowered
+    for (int i = threadIdx.x; i < kGuard * kLds; i += kLThreads<R, NL>) {  // guard rows: read by sweeps, never lowered
         L.Tbuf[i] = LCell<R>::make(INFS);
         L.Tbuf[(TH + 2 + kGuard) * kLds + i] = LCell<R>::make(INFS);
         L.Cbuf[i] = LCell<R>::make(INFS);
@@ -765,7 +819,7 @@ hipError_t fim2dl_init(const Fim2dArgs& a, bool f64, int64_t gx, int64_t gy, int
 template <typename R, int NL>
 static int resident_of(int cus) {
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fim2dl_persist_kernel<R, NL>, kThreads, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fim2dl_persist_kernel<R, NL>, kLThreads<R, NL>, 0) != hipSuccess ||
         per_cu < 1)
         per_cu = 1;
     return per_cu * cus;
@@ -790,17 +844,17 @@ int fim2dl_persist_resident(int nl, bool f64, int cus) {
 hipError_t fim2dl_persist(const Fim2dArgs& a, int nl, bool f64, int grid, hipStream_t st) {
     if (f64) {
         switch (nl) {
-            case 1: hipLaunchKernelGGL((fim2dl_persist_kernel<double, 1>), dim3(grid), dim3(kThreads), 0, st, a); break;
-            case 2: hipLaunchKernelGGL((fim2dl_persist_kernel<double, 2>), dim3(grid), dim3(kThreads), 0, st, a); break;
-            case 3: hipLaunchKernelGGL((fim2dl_persist_kernel<double, 3>), dim3(grid), dim3(kThreads), 0, st, a); break;
+            case 1: hipLaunchKernelGGL((fim2dl_persist_kernel<double, 1>), dim3(grid), dim3(kLThreads<double, 1>), 0, st, a); break;
+            case 2: hipLaunchKernelGGL((fim2dl_persist_kernel<double, 2>), dim3(grid), dim3(kLThreads<double, 2>), 0, st, a); break;
+            case 3: hipLaunchKernelGGL((fim2dl_persist_kernel<double, 3>), dim3(grid), dim3(kLThreads<double, 3>), 0, st, a); break;
             default: return hipErrorInvalidValue;
         }
     } else {
         switch (nl) {
-            case 1: hipLaunchKernelGGL((fim2dl_persist_kernel<float, 1>), dim3(grid), dim3(kThreads), 0, st, a); break;
-            case 2: hipLaunchKernelGGL((fim2dl_persist_kernel<float, 2>), dim3(grid), dim3(kThreads), 0, st, a); break;
-            case 3: hipLaunchKernelGGL((fim2dl_persist_kernel<float, 3>), dim3(grid), dim3(kThreads), 0, st, a); break;
-            case 4: hipLaunchKernelGGL((fim2dl_persist_kernel<float, 4>), dim3(grid), dim3(kThreads), 0, st, a); break;
+            case 1: hipLaunchKernelGGL((fim2dl_persist_kernel<float, 1>), dim3(grid), dim3(kLThreads<float, 1>), 0, st, a); break;
+            case 2: hipLaunchKernelGGL((fim2dl_persist_kernel<float, 2>), dim3(grid), dim3(kLThreads<float, 2>), 0, st, a); break;
+            case 3: hipLaunchKernelGGL((fim2dl_persist_kernel<float, 3>), dim3(grid), dim3(kLThreads<float, 3>), 0, st, a); break;
+            case 4: hipLaunchKernelGGL((fim2dl_persist_kernel<float, 4>), dim3(grid), dim3(kLThreads<float, 4>), 0, st, a); break;
             default: return hipErrorInvalidValue;
         }
     }

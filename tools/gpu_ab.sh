@@ -16,7 +16,8 @@ import json, sys
 d = json.load(open(f"gpurun_out/ab_{sys.argv[1]}.json"))
 r = d["roofline"]; x = d.get("extra_configs", {})
 print(sys.argv[1], "C2 %.3f ms %.2f Gcells/s visits %.0f inplace %.0f path %.2f" % (d["ms_per_step"], d["value"], r["tile_visits_per_solve"], r["inplace_passes_per_solve"], d.get("ms_to_path") or 0),
-      " | C3 %s" % (x.get("C3", {}).get("value")), " | costmap %s" % (x.get("costmap", {}).get("ms_per_step")), " | C4 %s | C5 %s" % (x.get("C4_1gpu", {}).get("value"), x.get("C5", {}).get("value")))
+      " | C3 %s" % (x.get("C3", {}).get("value")), " | costmap %s" % (x.get("costmap", {}).get("ms_per_step")), " | C4 %s | C5 %s / f32 %s" % (x.get("C4_1gpu", {}).get("value"), x.get("C5", {}).get("value"), x.get("C5_f32", {}).get("value")),
+      " C5 visits %s / %s" % (x.get("C5", {}).get("tile_visits_per_solve"), x.get("C5_f32", {}).get("tile_visits_per_solve")))
 PY
   done
 done
