@@ -62,11 +62,14 @@ template <typename R> constexpr int kRowsOf = sizeof(R) == 4 ? EIK_L32_ROWS : EI
 // waves with no new synchronisation: each SIMD interleaves G dependent chains instead of one wave's NL
 // chains.  Waves 4.. only sweep (staging, write-back, halo and queue roles stay on waves 0..3) and pass
 // the same workgroup barriers.  G = min(NL, EIK_LSPLIT_F32 / _F64); 1 = the one-wave-per-SIMD kernel.
+// Measured on C5 (4096^2 x 3, same box, 2 alternations, profiles/r06s7/): G = 1 / 2 / 3 gives fp64 3.70-3.73 /
+// 4.34-4.37 / 4.45 and fp32 6.23-6.27 / 7.60-7.66 / 7.09-7.18 Gcells/s (fp32 at G = 3: 168 VGPRs and three
+// waves per SIMD cost more than the third chain gives), so fp64 runs three groups and fp32 two.
 #ifndef EIK_LSPLIT_F32
 #define EIK_LSPLIT_F32 2
 #endif
 #ifndef EIK_LSPLIT_F64
-#define EIK_LSPLIT_F64 2
+#define EIK_LSPLIT_F64 3
 #endif
 template <typename R, int NL>
 constexpr int kLGroups = (sizeof(R) == 4 ? EIK_LSPLIT_F32 : EIK_LSPLIT_F64) < NL ? (sizeof(R) == 4 ? EIK_LSPLIT_F32 : EIK_LSPLIT_F64) : NL;
@@ -306,8 +309,8 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
     // sweep-only waves share them when the rows divide -- half the told[] registers and half the rows per
     // thread at a pass boundary)
     constexpr int G = kLGroups<R, NL>;
-    constexpr int RW = EIK_LSPLIT_ROWS && TH % (4 * G) == 0 ? 4 * G : 4;
-    constexpr int NJ = TH / RW;  // cells per thread
+    constexpr int RW = EIK_LSPLIT_ROWS ? 4 * G : 4;
+    constexpr int NJ = (TH + RW - 1) / RW;  // cells per thread (the last one only on the first TH % RW row waves)
     constexpr R INF = Real<R>::inf();
     const R INFS[4] = {INF, INF, INF, INF};
     const LCell<R> INFC = LCell<R>::make(INFS);
@@ -320,6 +323,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
     const bool main = tid < kThreads;
     const int rw = tid >> 6;
     const bool stager = rw < RW;
+    auto rowok = [&](int j) { return TH % RW == 0 || rw + RW * j < TH; };  // wave-uniform
     const int map = tile / a.tiles_per_map;
     const int rem = tile - map * a.tiles_per_map;
     const int ty = rem / a.ntx, tx = rem - (rem / a.ntx) * a.ntx;
@@ -382,6 +386,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
     auto store_tile = [&](const R (&cc)[NJ][NL], LCell<R> hv) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
+            if (!rowok(j)) continue;
             const int ry = rw + RW * j;
             R t4[4] = {INF, INF, INF, INF}, c4[4] = {INF, INF, INF, INF};
 #pragma unroll
@@ -405,6 +410,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
         R cc[NJ][NL];
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
+            if (!rowok(j)) continue;
             const int64_t gi = ((y0 + rw + RW * j) * a.W + x0 + lane) * ls + a.z0;
 #pragma unroll
             for (int z = 0; z < NL; ++z) {
@@ -418,6 +424,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
         R cc[NJ][NL];
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
+            if (!rowok(j)) continue;
             const int64_t gi = ((y0 + rw + RW * j) * a.W + x0 + lane) * ls + a.z0;
 #pragma unroll
             for (int z = 0; z < NL; ++z) {
@@ -430,6 +437,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
         R cc[NJ][NL];
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
+            if (!rowok(j)) continue;
             const int64_t gy = y0 + rw + RW * j, gx = x0 + lane;
             const bool in = gy < a.H && gx < a.W;
             const int64_t gi = in ? (gy * a.W + gx) * ls + a.z0 : 0;
@@ -491,6 +499,7 @@ __device__ __forceinline__ void process_tile_layered(const Fim2dArgs& a, int til
         if (stager) {  // (EIK_LSPLIT: only the row waves store)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
+            if (!rowok(j)) continue;
             const int ry = rw + RW * j;
             const int64_t gy = y0 + ry, gx = x0 + lane;
             const bool in = gy < a.H && gx < a.W;
