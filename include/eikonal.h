@@ -125,8 +125,8 @@ typedef enum {
     EIK_OPT_PRIO_RING = 17,  /* slots per priority band (rounded up to a power of two; 0, the
                                 default: >= 2 x the tiles).  A band whose ring fills stops the
                                 launch; eik_fim2d_solve then solves again with the FIFO.         */
-    EIK_OPT_PRIO_DISPATCH = 18, /* band entries moved to the FIFO per dispatch, 1..64 (0, the
-                                default: 64 on maps of >= 16384 tiles, else 16)                 */
+    EIK_OPT_PRIO_DISPATCH = 18, /* band entries moved to the FIFO per dispatch, 1..128 (0, the
+                                default: 128 on maps of >= 16384 tiles, else 16)                */
     EIK_OPT_EXACT_BAND = 19  /* biComputeTmap / rover path and fp64 FM3D early exits: 1 replays the
                                 reference's sequential narrow band in pop order from the converged
                                 fields (csrc/bidir_exact.hip): its tentative band values, its LIFO

@@ -151,7 +151,7 @@ struct eik_ctx {
     // Gcells/s (profiles/r05ac_layered_prio_ab.log, r05ad_prio_width_ab.log).
     double prio = -1.0;
     int prio_ring = 0;           // EIK_OPT_PRIO_RING: slots per priority band (0: pow2 >= 2 x the tiles)
-    int prio_dispatch = 0;       // EIK_OPT_PRIO_DISPATCH: band entries per dispatch (0: 64 on maps of >= kWideTiles, else 16)
+    int prio_dispatch = 0;       // EIK_OPT_PRIO_DISPATCH: band entries per dispatch (0: 128 on maps of >= kWideTiles, else 16)
     // EIK_OPT_LAYER_PLANAR (default 1): the layered solver works on layer-planar copies.  C5 kernel
     // traffic per launch 9.06 -> 3.92 GB (fp32), 20.3 -> 8.6 GB (fp64), the time within noise
     // (the layered sweep is VALU-bound; profiles/r05c_pmc_traffic_c5*.json, r05h_prio_planar_ab.log)
@@ -402,7 +402,7 @@ int eik_set_option(eik_ctx* c, int opt, double v) {
         case EIK_OPT_LIVE_PACK: c->live_pack = v != 0; break;
         case EIK_OPT_PRIO: c->prio = v; break;
         case EIK_OPT_PRIO_RING: c->prio_ring = v < 0 ? 0 : (int)std::min(v, 1073741824.0); break;
-        case EIK_OPT_PRIO_DISPATCH: c->prio_dispatch = v < 0 ? 0 : (int)std::min(v, 64.0); break;
+        case EIK_OPT_PRIO_DISPATCH: c->prio_dispatch = v < 0 ? 0 : (int)std::min(v, 128.0); break;
         case EIK_OPT_LAYER_PLANAR: c->layer_planar = v != 0; break;
         case EIK_OPT_PATH_LOOP: c->path_loop = std::max(0, std::min(4, (int)v)); break;
         case EIK_OPT_EXACT_BAND: c->exact_band = v != 0; break;
@@ -636,7 +636,7 @@ int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
         HIPCHK(c, fim2d_prio_delta(d_cost, f->f64, f->H * f->W, (float)prio, pd, f->stream));
         f->a.pdelta = pd;
         f->a.disp = c->prio_dispatch > 0 ? (unsigned)c->prio_dispatch
-                                         : f->a.tiles_per_map >= kWideTiles ? 64u : 16u;  // (fim_engine.hpp band_dispatch)
+                                         : f->a.tiles_per_map >= kWideTiles ? 128u : 16u;  // (fim_engine.hpp band_dispatch)
     }
     HIPCHK(c, fim2d_init(f->a, f->f64, (int)f->B, (const int64_t*)f->goals.p, (unsigned*)f->edge.p, f->stream));
     f->started = true;

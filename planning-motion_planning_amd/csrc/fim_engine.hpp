@@ -559,13 +559,15 @@ __device__ __forceinline__ unsigned wave_incl_sum(unsigned v) {
 // and the batch is the bands' throughput: C4 takes ~9 tiles per us, and one band per dispatch (a few
 // entries each, ~3 round trips) held narrow bands to a fraction of that (C4 2.7 vs 10.9 Gcells/s).
 // The batch a dispatch moves: Fim2dArgs::disp, set per solve (eikonal_api.cpp, EIK_OPT_PRIO_DISPATCH),
-// else kDispatch; at most 64 (one lane per entry).  64 on maps of >= kWideTiles tiles: C4 at one GPU
-// 13.8-14.3 -> 16.3-16.7 Gcells/s (48: 15.5-15.7); 16 below: C2 2.22-2.27 (32) -> 2.16-2.19 ms (8:
+// else kDispatch; at most kMaxDispatch = 128 (two entries per lane).  128 on maps of >= kWideTiles tiles:
+// C4 at one GPU 13.8-14.3 (32) -> 15.5-15.7 (48) -> 16.3-16.7 (64) -> 17.3-17.6 Gcells/s (128; 96: 17.0-17.3,
+// round 6, profiles/r06s7/r06s7_disp_ab.log); 16 below: C2 2.22-2.27 (32) -> 2.16-2.19 ms (8:
 // 2.20-2.22, 48: 2.31) -- a larger batch leaves a FIFO backlog that no longer follows the bands'
 // order, a smaller one dispatches more often.  (A batch limited to the waiting workgroups, qhead -
 // qtail: C4 10.6 -- the backlog is what feeds a busy chip.  profiles/r05x_dispatch_ab.log,
 // r05z2_dispatch_sweep.log.)
 constexpr unsigned kDispatch = 32;
+constexpr unsigned kMaxDispatch = 128;  // two entries per lane
 __device__ __forceinline__ bool band_dispatch(const Fim2dArgs& a) {
     const int lane = threadIdx.x & 63;
     unsigned long long h = 0, t = 0;
@@ -574,7 +576,7 @@ __device__ __forceinline__ bool band_dispatch(const Fim2dArgs& a) {
         t = __hip_atomic_load(&a.bctl[16 * lane + 8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (lane == 0) qcount(a, 2);  // (EIK_QDEBUG: dispatch attempts, 2 x 64 band words read each)
-    const unsigned lim = a.disp ? (a.disp < 64u ? a.disp : 64u) : kDispatch;
+    const unsigned lim = a.disp ? (a.disp < kMaxDispatch ? a.disp : kMaxDispatch) : kDispatch;
     const unsigned avail = t > h ? (unsigned)(t - h < lim ? t - h : lim) : 0u;
     if (!__ballot(avail != 0u)) return false;
     // lowest bands first.  (Reserving a quarter of the batch for the highest band -- the front's
@@ -590,38 +592,44 @@ __device__ __forceinline__ bool band_dispatch(const Fim2dArgs& a) {
     unsigned long long base = 0;
     if (lane == 0) base = atomicAdd(a.qtail, (unsigned long long)total);
     base = __shfl(base, 0);
-    // lane e < total moves entry e: band b where start_b <= e < end_b, offset e - start_b
-    int b = -1;
-    unsigned long long src = 0;
-    unsigned long long mask = __ballot(got != 0u);
-    while (mask) {
-        const int j = __builtin_ctzll(mask);
-        mask &= mask - 1;
-        const unsigned sj = __shfl(start, j), ej = __shfl(end, j);
-        const unsigned long long hj = __shfl(h, j);
-        if ((unsigned)lane >= sj && (unsigned)lane < ej) {
-            b = j;
-            src = hj + (lane - sj);
-        }
-    }
-    if (b >= 0) {
-        // the entry's producer may still be storing it (it took the tail first)
-        unsigned* slot = &a.bslot[(size_t)b * (a.bmask + 1ull) + (src & a.bmask)];
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        unsigned v;
-        while ((v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
-            if (__builtin_amdgcn_s_memrealtime() - t0 > a.qtimeout) {
-                atomicOr(a.qerror, 1u);
-                v = 1u;  // (the error flag ends the solve; the FIFO slot gets a harmless entry)
-                break;
+    // entry e < total: lane e, and lane e - 64 for a batch past 64 -- band b where start_b <= e < end_b,
+    // offset e - start_b
+    const unsigned long long gotmask = __ballot(got != 0u);
+    auto move = [&](unsigned e) {
+        int b = -1;
+        unsigned long long src = 0;
+        unsigned long long mask = gotmask;
+        while (mask) {
+            const int j = __builtin_ctzll(mask);
+            mask &= mask - 1;
+            const unsigned sj = __shfl(start, j), ej = __shfl(end, j);
+            const unsigned long long hj = __shfl(h, j);
+            if (e >= sj && e < ej) {
+                b = j;
+                src = hj + (e - sj);
             }
-            __builtin_amdgcn_s_sleep(1);
         }
-        __hip_atomic_store(slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // tagged with its band: the taker clears the tile's membership bit (qgrab_prio)
-        __hip_atomic_store(&a.qslot[(base + lane) & a.qmask], v | ((unsigned)b + 1u) << kBandTagShift, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
+        if (b >= 0) {
+            // the entry's producer may still be storing it (it took the tail first)
+            unsigned* slot = &a.bslot[(size_t)b * (a.bmask + 1ull) + (src & a.bmask)];
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            unsigned v;
+            while ((v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > a.qtimeout) {
+                    atomicOr(a.qerror, 1u);
+                    v = 1u;  // (the error flag ends the solve; the FIFO slot gets a harmless entry)
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            __hip_atomic_store(slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // tagged with its band: the taker clears the tile's membership bit (qgrab_prio)
+            __hip_atomic_store(&a.qslot[(base + e) & a.qmask], v | ((unsigned)b + 1u) << kBandTagShift, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+    };
+    move((unsigned)lane);
+    if (total > 64u) move((unsigned)lane + 64u);  // (uniform)
     return true;
 }
 

@@ -271,9 +271,11 @@ def test_pass_cap_option(passes):
 
 @pytest.mark.parametrize("opts", [(("SCHED", 0),), (("SCHED", 2),), (("SCHED", 3),), (("FRESH_FIRST", 1),),
                                   (("SCHED", 0), ("FRESH_FIRST", 1)), (("PRIO", 0.1),), (("PRIO", 1),),
-                                  (("PRIO", 1e4),), (("PRIO", 1), ("SCHED", 0))])
+                                  (("PRIO", 1e4),), (("PRIO", 1), ("SCHED", 0)),
+                                  (("PRIO", 0.1), ("PRIO_DISPATCH", 128)), (("PRIO", 1), ("PRIO_DISPATCH", 100))])
 def test_schedule_options(opts):
-    """The queue-scheduling options (EIK_OPT_SCHED other than the default 1, EIK_OPT_FRESH_FIRST)
+    """The queue-scheduling options (EIK_OPT_SCHED other than the default 1, EIK_OPT_FRESH_FIRST, the
+    priority bands and their dispatch batch past 64 entries -- two per lane, fim_engine.hpp band_dispatch)
     change the order of tile visits, never the fixed point: single map and batch vs the oracle."""
     import eikonal
     from eikonal import _lib as L
