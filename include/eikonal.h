@@ -116,8 +116,9 @@ typedef enum {
                                 width v x 64 x the geometric mean of the finite costs
                                 (fim_engine.hpp "priority bands"); 0 = the FIFO; < 0 (default) =
                                 0.25 x max(1, sqrt(H W) / 4096) for fp64 2D solves of rasters
-                                of >= 4096^2 cells (any size for a decomposition block) and
-                                layered solves of >= 3072^2 in either dtype; else the FIFO       */
+                                of >= 4096^2 cells (any size for a decomposition block), one
+                                fp32 2D map of >= 16384 tiles and layered solves of >= 3072^2
+                                in either dtype; else the FIFO                                   */
     EIK_OPT_LAYER_PLANAR = 16, /* few-layer 3D volumes (the layered solver): 1 (default) solves on
                                 layer-planar copies [nl][H][W] of the solved layers (one copy in,
                                 one out per solve; every tile-row access one contiguous run per

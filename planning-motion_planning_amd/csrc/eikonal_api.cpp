@@ -142,11 +142,13 @@ struct eik_ctx {
     int sched = 1;               // EIK_OPT_SCHED: in-place scheduling of persistent visits
     int live_pack = 0;           // EIK_OPT_LIVE_PACK: the halo agent packs only idle tiles' edges
     // EIK_OPT_PRIO: the priority bands' width in units of 64 x the cost's geometric mean (0: the
-    // plain FIFO; < 0, the default: default_prio() in fp64 and on the layered solver, 0 in fp32 2D;
+    // plain FIFO; < 0, the default: default_prio() in fp64, on the layered solver and on one fp32 2D map of
+    // >= kWideTiles tiles, else 0 in fp32 2D;
     // round 5's first default was 1 in fp64).  fp64 at 1: C2 2.44-2.50 -> 2.37 ms, C4 at
     // one GPU 10.5 -> 13.8 Gcells/s; 0.5 / 2 lose on C4 (6.9 / 12.9; profiles/r05i_prio_ab.log).  fp32
     // solves are twice as fast per pass and the one-dispatcher bands held them back: C2 fp32 1.6 ->
-    // 1.9 ms, C4 fp32 18.7 -> 10.8 Gcells/s (profiles/r05j_bench.json).  Batches of > 2 maps: FIFO.
+    // 1.9 ms, C4 fp32 18.7 -> 10.8 Gcells/s (profiles/r05j_bench.json) -- until the 128-entry dispatches of
+    // round 6 (C4 fp32 with bands 18.4 -> 19.5).  Batches of > 2 maps: FIFO.
     // The layered solver's bands (both dtypes, default_prio()): C5 fp64 1.92 -> 3.65, fp32 4.73 -> 6.2
     // Gcells/s (profiles/r05ac_layered_prio_ab.log, r05ad_prio_width_ab.log).
     double prio = -1.0;
@@ -623,7 +625,13 @@ int eik_fim2d_start(eik_fim2d* f, const void* d_cost, void* d_T, const int64_t* 
     // 16384^2 4 x 2 rehearsal: FIFO 3.7x the single domain's visits, width 1 0.96x (22 ms), the
     // block-sized 0.35 2.96x (61 ms), profiles/r05d_c4_rehearsal_n8_*.json, r05h_c4_rehearsal_n8.log)
     const bool dd_block = f->a.ghost[0] || f->a.ghost[1] || f->a.ghost[2] || f->a.ghost[3];
+    // fp32 keeps the FIFO below kWideTiles tiles (its passes are twice as fast and the one dispatcher held
+    // it back: C2 fp32 1.6 -> 1.9 ms with bands, round 5); one map of >= kWideTiles tiles takes the bands
+    // since the 128-entry dispatches (round 6: C4 at one GPU fp32 18.4 -> 19.5 Gcells/s mean of 5 same-box
+    // alternations, 145 k -> 108 k visits, profiles/r06s7/r06s7_c4f32_prio_ab{,2}.log)
+    const bool f32_wide = !f->f64 && f->B == 1 && f->a.tiles_per_map >= kWideTiles && !dd_block;
     const double prio = c->prio >= 0 ? c->prio
+                        : f32_wide ? default_prio(f->H, f->W, 4096.0)
                         : !f->f64  ? 0.0
                         : dd_block ? std::max(1.0, default_prio(f->H, f->W, 0.0))
                                    : default_prio(f->H, f->W, 4096.0);
